@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""bench.py — denoising steps/s of the AnimateDiff UNetMotionModel step on MI355X.
+
+Metric (BASELINE.json): denoising steps/sec (whole node) at 16-frame 512x512
+bf16.  One step = UNet forward on the CFG batch (B=2: uncond + cond) of a
+16-frame 64x64-latent video + CFG combine + DDIM update, run as
+one replay of the captured hipGraph.  Workload: BASELINE config 3 (SD-1.5 +
+motion-adapter-v1-5-2 shapes, 1.31B params, synthetic N(0, 0.02^2) weights,
+synthetic latents/text embeddings).  With N ranks the 16 frames are sharded
+F/N per GPU (frame-parallel, all-to-all around each motion module): all ranks
+together run ONE video's denoising, so value = steps/s of the node (strong
+scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Also reported: `roofline` for the spatial self-attention kernel at level 1
+(S=4096, d=40: the north-star kernel), timed with HIP events on its launch
+stream; `step_mfma` = the whole step's algorithmic FLOPs / step time vs the
+bf16 dense MFMA peak; `cpu_baseline` = the oracle (PyTorch-CPU fp32
+restatement) on a bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for p in (str(ROOT), str(ROOT / "video-diffusion-experiments_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "denoising steps/sec (whole node) at 16-frame 512×512 bf16; 1/2/4/8-GPU scaling"
+PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+STEP_TFLOP = {"full": 35.496, "tiny": 0.234}   # BASELINE.md §2 / SURVEY App. B, CFG batch, F=16 / F=4
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def time_attention(n_img, reps, stream):
+    """The L1 spatial self-attention kernel alone: 4*S^2*d*heads*n_img FLOPs per launch."""
+    from vdiff import ops
+    S, heads, d = 4096, 8, 40
+    C = heads * d
+    g = torch.Generator(device="cuda").manual_seed(7)
+    qkv = (torch.randn(n_img * S, 3 * C, device="cuda", generator=g) * 1.5).to(torch.bfloat16)
+    out = torch.empty(n_img * S, C, device="cuda", dtype=torch.bfloat16)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    for _ in range(3):
+        ops.attention(q, k, v, n_img, heads, S, S, d, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        ops.attention(q, k, v, n_img, heads, S, S, d, out=out)
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    flop = 4.0 * S * S * d * heads * n_img
+    byts = 4.0 * n_img * S * C * 2            # Q, K, V read once + O written once (bf16)
+    tf = flop / (ms * 1e-3) / 1e12
+    return {"kernel": "flash_attn_kernel<40> (spatial self-attn, L1: S=4096, d=40, 8 heads, "
+                      f"{n_img} images)",
+            "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": None,
+            "avg_launch_ms": round(ms, 4), "algorithmic_flop_per_launch": flop,
+            "algorithmic_bytes_per_launch": byts}
+
+
+def cpu_baseline(unet_gpu, cfg_name, frames_sample, frames_full):
+    """Oracle (oracle/unet_ref.py, fp32 PyTorch-CPU) on `frames_sample` frames of the
+    same CFG-batch step; scaled to steps/s of the full `frames_full`-frame video."""
+    from oracle import ddim_ref, unet_ref
+    from vdiff.config import get_config
+    cfg = get_config(cfg_name)
+    sd = {k: v.detach().float().cpu() for k, v in unet_gpu.state_dict().items()}
+    g = torch.Generator().manual_seed(42)
+    lat = torch.randn((1, 4, frames_sample, 64, 64), generator=g)
+    ehs = torch.randn((2, 77, cfg["cross_attention_dim"]), generator=torch.Generator().manual_seed(1))
+    acp = ddim_ref.alphas_cumprod()
+    times = []
+    with torch.no_grad():
+        for _ in range(2):
+            t0 = time.perf_counter()
+            eps = unet_ref.unet_forward(sd, cfg, torch.cat([lat, lat]), 981, ehs)
+            ddim_ref.ddim_step(ddim_ref.cfg_combine(eps, 7.5), 981, lat, 50, acp)
+            times.append(time.perf_counter() - t0)
+    t = min(times)
+    return {"value": round(1.0 / (t * frames_full / frames_sample), 5), "unit": "denoising steps/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"1 CFG step (UNet fwd B=2 + CFG + DDIM) of the {cfg_name} model on {frames_sample} "
+                      f"of {frames_full} frames, fp32, min of 2 runs = {t:.2f} s, scaled x"
+                      f"{frames_full // frames_sample} to the full video"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="full", choices=["full", "tiny"])
+    ap.add_argument("--frames", type=int, default=None)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--attn-reps", type=int, default=20)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    fs = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        from vdiff.dist import FrameShard
+        fs = FrameShard()
+
+    import vdiff
+    from vdiff import DDIMScheduler, DenoiseLoop
+    from vdiff.weights import materialize_synthetic
+
+    cfg_name = args.config
+    frames = args.frames or (16 if cfg_name == "full" else 4)
+    t0 = time.time()
+    unet = materialize_synthetic(cfg_name, device="cuda", seed=0)
+    unet.dist = fs
+    unet.prepare()
+    log(f"[bench] model ready in {time.time() - t0:.1f}s; world={world}")
+    cfg = unet.config
+    fl = frames // world
+    g = torch.Generator().manual_seed(42)
+    lat = torch.randn((1, 4, frames, 64, 64), generator=g)[:, :, rank * fl:(rank + 1) * fl].cuda()
+    ehs = torch.randn((2, 77, cfg["cross_attention_dim"]), generator=torch.Generator().manual_seed(1))
+    sched = DDIMScheduler.from_config(DDIMScheduler().config, beta_schedule="linear", steps_offset=1,
+                                      clip_sample=False)
+    sched.set_timesteps(50)
+    total = args.warmup + args.steps
+    ts = sched.timesteps.repeat((total + 49) // 50)[:max(total, 50)]
+    loop = DenoiseLoop(unet, sched, lat, ehs.cuda(), 7.5, timesteps=ts, use_graph=not args.no_graph)
+    loop.prime()
+    log(f"[bench] primed: graph={'yes' if loop.graph is not None else 'no'} {loop.graph_error or ''}")
+    loop.run(args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    loop.run(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+    assert torch.isfinite(loop.lat).all(), "non-finite latents"
+    sps = args.steps / elapsed
+    ms = 1e3 * elapsed / args.steps
+
+    roof = time_attention(2 * fl, args.attn_reps, torch.cuda.current_stream())
+    step_tf = STEP_TFLOP[cfg_name] * (frames / (16 if cfg_name == "full" else 4)) / (ms * 1e-3) / world
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("[bench] timing the CPU oracle baseline ...")
+        cpu = cpu_baseline(unet, cfg_name, min(args.cpu_frames, frames), frames)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(sps, 4),
+            "unit": "denoising steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (latents randn seed 42, text embeddings randn seed 1, weights N(0,0.02^2))",
+            "config": {
+                "workload": ("BASELINE config 3: AnimateDiff UNetMotionModel (SD-1.5 + motion-adapter-"
+                             "v1-5-2 shapes, 1.31B params), 16 frames x 64x64 latents (512x512), CFG "
+                             "batch 2, guidance 7.5, DDIM 50-step schedule, one hipGraph replay per step")
+                if cfg_name == "full" else "BASELINE config 2: tiny UNetMotionModel, 4 frames x 64x64",
+                "model": f"UNetMotionModel[{cfg_name}]",
+                "frames": frames, "latent_hw": 64, "global_batch": 2, "seq_len": 4096,
+                "parallelism": f"frame-shard x{world}" if world > 1 else "single-GPU",
+                "hipgraph": loop.graph is not None,
+            },
+            "roofline": roof,
+            "step_mfma": {"algorithmic_tflop_per_step_per_gpu": round(STEP_TFLOP[cfg_name] * frames /
+                                                                     (16 if cfg_name == "full" else 4) / world, 3),
+                          "achieved": round(step_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                          "frac": round(step_tf / PEAK_BF16_TFLOPS, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

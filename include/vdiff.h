@@ -1,0 +1,173 @@
+/*
+ * vdiff.h — C ABI of libvdiff_hip.so, the MI355X (gfx950) kernels behind the
+ * video-diffusion denoising step.
+ *
+ * The reference has no native code: every op below replaces a stock
+ * torch/cuDNN/cuBLAS/SDPA call that diffusers issues inside
+ * `UNetMotionModel.forward` (called at
+ * /root/reference/experiments/03_trace_forward_pass.py:109-113) and
+ * `DDIMScheduler.step` (configured at
+ * /root/reference/experiments/05_grid_search_ablation.py:136-141, stepped
+ * inside the pipe(...) call at :158-167).  Per-entry citations name the
+ * diffusers op replaced.
+ *
+ * Conventions:
+ *  - plain device pointers + explicit int64 sizes/strides (in ELEMENTS);
+ *  - activations bf16 ("bf16" = raw 16-bit storage), statistics and
+ *    latents fp32, weights bf16 packed [N][K] (K contiguous);
+ *  - every call takes the hipStream_t to launch on, never allocates, never
+ *    synchronises, never retains a pointer: all calls are hipGraph-capturable;
+ *  - returns 0 (VD_OK) or a vd_status / hipError_t code; vd_strerror() names it.
+ *  - activation layout is NHWC rows: pixel/token m of image n at row
+ *    n*H*W + h*W + w; video b, frame f -> image n = b*F + f.
+ */
+#ifndef VDIFF_H
+#define VDIFF_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* vd_stream_t; /* hipStream_t */
+
+enum vd_status {
+  VD_OK = 0,
+  VD_EINVAL = 1000,       /* bad shape / alignment / unsupported parameter */
+  VD_EUNSUPPORTED = 1001, /* valid request outside the compiled variants    */
+  VD_ERCCL = 1002         /* RCCL call failed                                */
+};
+
+const char* vd_strerror(int code);
+int vd_version(void);
+
+/* ---------------------------------------------------------------- GEMM / conv
+ * out[m, n] = epi( sum_k A[m, k] * W[n, k] )          (bf16 MFMA, fp32 accumulate)
+ *
+ * a_mode VD_A_DENSE : A[m, k] = a0[m*lda0 + k]              for k <  k0
+ *                              a1[m*lda1 + (k - k0)]       for k >= k0  (channel concat)
+ * a_mode VD_A_CONV3X3: implicit-GEMM 3x3 conv, pad 1, over NHWC images; the
+ *   K index is tap*(Cin) + ci with Cin = k0 + (channels of a1); channels
+ *   [0,k0) come from a0 (pixel stride lda0), the rest from a1 (pixel stride
+ *   lda1) — this is the up-block torch.cat([x, skip], 1) without materialising
+ *   it.  stride 2 = Downsample2D; upsample 1 = Upsample2D (nearest x2 of the
+ *   h_in x w_in input, then conv).  M = n_img*h_out*w_out.
+ *   Replaces torch conv2d in ResnetBlock2D.conv1/conv2, Down/Upsample2D.conv,
+ *   conv_in/conv_out and nn.Linear / 1x1 convs (a5, a8, a10).
+ * epilogue, in order: + bias[n] (fp32) ; + rowbias[(m / rb_div) * ld_rb + n]
+ *   (fp32, the ResnetBlock2D time_emb_proj broadcast) ; act ; + res[m*ld_res + n]
+ *   (bf16) ; store bf16 (or fp32 if out_f32).
+ * act VD_ACT_GEGLU: W rows are packed in 16-row blocks alternating (hidden,
+ *   gate); out has N/2 columns: h * gelu_erf(g)  (diffusers GEGLU, a10).
+ */
+enum { VD_A_DENSE = 0, VD_A_CONV3X3 = 1 };
+enum { VD_ACT_NONE = 0, VD_ACT_SILU = 1, VD_ACT_GEGLU = 2 };
+
+typedef struct vd_gemm_desc {
+  const void* a0; int64_t lda0; int64_t k0;
+  const void* a1; int64_t lda1;
+  int32_t a_mode;
+  int32_t n_img, h_in, w_in, h_out, w_out, stride, upsample;
+  const void* w; int64_t ldw;
+  int64_t M, N, K;
+  const float* bias;
+  const float* rowbias; int64_t ld_rb; int64_t rb_div;
+  const void* res; int64_t ld_res;
+  int32_t act;
+  void* out; int64_t ldc; int32_t out_f32;
+} vd_gemm_desc;
+
+int vd_gemm(const vd_gemm_desc* d, vd_stream_t stream);
+
+/* ---------------------------------------------------------------- GroupNorm
+ * torch GroupNorm over NHWC rows, for ResnetBlock2D.norm1/2 (eps 1e-5, +SiLU),
+ * Transformer2DModel.norm (eps 1e-6) and the motion-module norm whose
+ * statistics span (C/G, F, H, W) (eps 1e-6) — SURVEY.md §8a a11.
+ * An "instance" is a run of pix_per_inst consecutive NHWC rows sharing
+ * statistics (one image, or all F frames of a video).  Channels [0,c0) come
+ * from x0 (row stride ldx0), [c0,C) from x1 (row stride ldx1).
+ *   vd_gn_partial : per (inst, split, channel) {count, mean, M2, 0} -> ws
+ *                   ws has n_inst*n_split*C float4 entries.
+ *   vd_gn_finalize: combines n_split_total partial splits (Chan), groups of
+ *                   C/groups channels, -> scale_shift[inst][C] float2 {a, b}
+ *                   with y = x*a + b = (x-mean)*rstd*gamma + beta.
+ *   vd_gn_apply   : y = x*a + b (then SiLU if silu) -> bf16 rows (ldy).
+ */
+int vd_gn_partial(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1,
+                  int64_t C, int64_t n_inst, int64_t pix_per_inst, int32_t n_split,
+                  float* ws, vd_stream_t stream);
+int vd_gn_finalize(const float* ws, int64_t n_inst, int32_t n_split_total, int64_t C,
+                   int32_t groups, float eps, const float* gamma, const float* beta,
+                   float* scale_shift, vd_stream_t stream);
+int vd_gn_apply(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1,
+                int64_t C, int64_t n_inst, int64_t pix_per_inst, const float* scale_shift,
+                int32_t silu, void* y, int64_t ldy, vd_stream_t stream);
+
+/* ---------------------------------------------------------------- LayerNorm
+ * BasicTransformerBlock.norm1/2/3 (eps 1e-5) over the last dim of bf16 rows,
+ * optionally + pe[(row / pe_div) % pe_period][c] (fp32; the motion block's
+ * SinusoidalPositionalEmbedding, applied after norm1 and norm2 — App. A.4).
+ */
+int vd_layernorm(const void* x, int64_t ldx, int64_t rows, int64_t C, const float* gamma,
+                 const float* beta, float eps, const float* pe, int64_t pe_div,
+                 int64_t pe_period, void* y, int64_t ldy, vd_stream_t stream);
+
+/* ---------------------------------------------------------------- attention
+ * softmax(q k^T * scale) v per (batch b, head h): replaces
+ * F.scaled_dot_product_attention in Attention/AttnProcessor2_0 (a6 spatial
+ * self-attention, a7 cross-attention).  Row (b, s) of q at q + (b*sq + s)*ldq,
+ * head h at column h*d.  K/V batch index = b / kv_div (cross-attention reads the
+ * un-repeated encoder_hidden_states projection once per video).
+ * d in {32, 40, 64, 80, 128, 160}; flash (online softmax) with bf16 MFMA.
+ */
+int vd_attention(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                 int64_t ldv, void* o, int64_t ldo, int64_t batch, int32_t heads, int64_t sq,
+                 int64_t skv, int32_t d, int64_t kv_div, float scale, vd_stream_t stream);
+
+/* Temporal (motion-module) self-attention over frames (a9): token (b, f, p) is
+ * row (b*frames + f)*positions + p of q/k/v/o (the NHWC layout, no permute);
+ * frames <= 32. */
+int vd_temporal_attention(const void* q, const void* k, const void* v, int64_t ld,
+                          void* o, int64_t ldo, int64_t batch, int32_t frames,
+                          int64_t positions, int32_t heads, int32_t d, float scale,
+                          vd_stream_t stream);
+
+/* ---------------------------------------------------------------- step glue
+ * vd_timestep_embed: diffusers Timesteps(dim, flip_sin_to_cos=True, shift 0)
+ *   (a12) -> bf16 [B][dim].  Timestep = ts[*step_idx] if step_idx else ts[b].
+ * vd_pack_latents: x (B,C,F,H,W) fp32 -> NHWC bf16 rows [(dup*B*F*H*W)][cpad],
+ *   channels >= C zero; dup = 2 repeats the batch (the CFG cat([x, x])).
+ * vd_unpack_nhwc: NHWC rows (fp32 if src_f32 else bf16, row stride ld) ->
+ *   (B,C,F,H,W) fp32.
+ * vd_ddim_cfg_step: eps rows NHWC fp32 [(ncfg*B*F*H*W)][ld_eps]; if ncfg == 2
+ *   eps = e_u + g*(e_c - e_u) (uncond first); DDIM eta=0 epsilon update of
+ *   latents (B,C,F,H,W) fp32 in place with coef[4*step] = {sqrt(a_t),
+ *   sqrt(1-a_t), sqrt(a_prev), sqrt(1-a_prev)}, step = *step_idx (or 0 if
+ *   NULL); optional x0_out (B,C,F,H,W) fp32; optional next_in = the packed
+ *   bf16 UNet input of the next step (dup = ncfg) — a1 + a13 fused.
+ * vd_step_advance: ++*step_idx (one thread; the last node of a captured step).
+ */
+int vd_timestep_embed(const float* ts, const int32_t* step_idx, int64_t B, int32_t dim,
+                      void* out, vd_stream_t stream);
+int vd_pack_latents(const float* x, int64_t B, int64_t C, int64_t F, int64_t H, int64_t W,
+                    int32_t dup, void* out, int64_t cpad, vd_stream_t stream);
+int vd_unpack_nhwc(const void* src, int32_t src_f32, int64_t ld, int64_t B, int64_t C,
+                   int64_t F, int64_t H, int64_t W, float* dst, vd_stream_t stream);
+int vd_ddim_cfg_step(const float* eps, int64_t ld_eps, int32_t ncfg, float guidance,
+                     float* latents, int64_t B, int64_t C, int64_t F, int64_t H, int64_t W,
+                     const float* coef, const int32_t* step_idx, float* x0_out,
+                     void* next_in, int64_t cpad, vd_stream_t stream);
+int vd_step_advance(int32_t* step_idx, vd_stream_t stream);
+
+/* Row-block permute for the frame<->position re-shard around motion modules:
+ * dst[(a*nb + b)*nc + c] = src[(b*na + a)*nc + c] for bf16 rows of `width`
+ * elements (a transpose of the [nb][na] grid of row blocks, nc rows each). */
+int vd_block_transpose(const void* src, void* dst, int64_t nb, int64_t na, int64_t nc,
+                       int64_t width, vd_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VDIFF_H */

@@ -1,0 +1,81 @@
+"""Generate the committed golden fixtures (run in the build container, CPU only):
+
+    python tests/golden/make_golden.py
+
+tiny_unet.npz  — BASELINE config 1: tiny UNetMotionModel,
+                 synthetic weights seed 0, latents randn seed 42
+                 (1,4,4,64,64), encoder_hidden_states randn seed 1 (2,77,64),
+                 CFG batch cat([x, x]); oracle (fp32) eps at t in {961, 500, 1},
+                 the bf16-storage-emulated oracle eps at t=961, the CFG+DDIM
+                 step from t=961 (50-step schedule), and a 3-step loop result.
+ddim_tables.npz — DDIM leading timesteps and {sqrt a_t, sqrt 1-a_t, sqrt a_p,
+                 sqrt 1-a_p} tables for N in {15, 25, 50}.
+
+Both come from oracle/ (the CPU restatement); see the oracle header for what
+that pins and what it cannot (diffusers numerics are unpinned).
+"""
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "video-diffusion-experiments_amd")]
+
+from oracle import ddim_ref, unet_ref  # noqa: E402
+from vdiff.config import TINY  # noqa: E402
+from vdiff.models import UNetMotionModel  # noqa: E402
+from vdiff.weights import init_synthetic_  # noqa: E402
+
+
+def tiny_inputs():
+    m = init_synthetic_(UNetMotionModel("tiny"), seed=0)
+    sd = {k: v.float() for k, v in m.state_dict().items()}
+    lat = torch.randn((1, 4, 4, 64, 64), generator=torch.Generator().manual_seed(42))
+    ehs = torch.randn((2, 77, 64), generator=torch.Generator().manual_seed(1))
+    lat = lat.to(torch.bfloat16).float()  # the device path stores its input rows in bf16
+    ehs = ehs.to(torch.bfloat16).float()
+    return sd, lat, ehs
+
+
+def main():
+    torch.manual_seed(0)
+    sd, lat, ehs = tiny_inputs()
+    x_in = torch.cat([lat, lat])
+    out = {"latents": lat.numpy(), "ehs": ehs.numpy()}
+    with torch.no_grad():
+        for t in (961, 500, 1):
+            out[f"eps_t{t}"] = unet_ref.unet_forward(sd, TINY, x_in, t, ehs).numpy()
+        out["eps_t961_bf16emu"] = unet_ref.unet_forward(sd, TINY, x_in, 961, ehs, act="bf16").numpy()
+        acp = ddim_ref.alphas_cumprod()
+        ts50 = ddim_ref.timesteps_leading(50)
+        x1, x0 = ddim_ref.ddim_step(ddim_ref.cfg_combine(
+            torch.from_numpy(unet_ref.unet_forward(sd, TINY, x_in, int(ts50[0]), ehs).numpy()), 7.5),
+            int(ts50[0]), lat, 50, acp)
+        out["ddim_step0_x"] = x1.numpy()
+        out["ddim_step0_x0"] = x0.numpy()
+        fn = lambda x, t, e: unet_ref.unet_forward(sd, TINY, x, t, e)  # noqa: E731
+        out["loop3_x"] = ddim_ref.denoise_loop(fn, lat, ehs, 50, 7.5, acp, steps=3).numpy()
+    np.savez_compressed(HERE / "tiny_unet.npz", **out)
+
+    tab = {}
+    acp = ddim_ref.alphas_cumprod()
+    for n in (15, 25, 50):
+        ts = ddim_ref.timesteps_leading(n)
+        rows = []
+        for t in ts:
+            prev = t - 1000 // n
+            a_t = acp[t]
+            a_p = acp[prev] if prev >= 0 else acp[0]
+            rows.append([a_t ** 0.5, (1 - a_t) ** 0.5, a_p ** 0.5, (1 - a_p) ** 0.5])
+        tab[f"ts{n}"] = ts
+        tab[f"coef{n}"] = torch.tensor(rows).numpy()
+    tab["alphas_cumprod"] = acp.numpy()
+    np.savez_compressed(HERE / "ddim_tables.npz", **tab)
+    print({k: v.shape for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,72 @@
+"""The C-ABI boundary (CPU): include/vdiff.h <-> libvdiff_hip.so <-> ctypes."""
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+import torch
+
+import vdiff._lib as L
+from vdiff import ops
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "vdiff.h"
+
+
+def header_functions():
+    txt = HEADER.read_text()
+    return set(re.findall(r"^\s*(?:const\s+char\s*\*|int)\s+(vd_\w+)\s*\(", txt, re.M))
+
+
+def test_header_declares_exactly_the_bound_symbols():
+    assert header_functions() == set(L.SIGNATURES)
+
+
+def test_library_loads_and_exports_every_symbol():
+    h = L.lib()
+    for name in header_functions():
+        assert hasattr(h, name), name
+    assert h.vd_version() == 1
+    assert h.vd_strerror(1000).decode().startswith("vdiff: invalid argument")
+    out = subprocess.run(["nm", "-D", "--defined-only", str(L.LIB_PATH)], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (vd_\w+)", out))
+    assert header_functions() <= exported
+
+
+def test_argument_counts_match_header():
+    txt = HEADER.read_text()
+    for name, (argt, _) in L.SIGNATURES.items():
+        m = re.search(rf"{name}\s*\(([^;]*?)\);", txt, re.S)
+        assert m, name
+        params = m.group(1).strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        assert n == len(argt), (name, n, len(argt))
+
+
+def test_gemm_desc_layout_matches_c(tmp_path):
+    fields = [f for f, _ in L.GemmDesc._fields_]
+    src = tmp_path / "probe.c"
+    body = "".join(f'printf("{f} %zu\\n", offsetof(vd_gemm_desc, {f}));' for f in fields)
+    src.write_text(f'#include <stdio.h>\n#include <stddef.h>\n#include "vdiff.h"\n'
+                   f'int main(void){{ {body} printf("size %zu\\n", sizeof(vd_gemm_desc)); return 0; }}\n')
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split("\n") if line)
+    for f in fields:
+        assert int(got[f]) == getattr(L.GemmDesc, f).offset, f
+    assert int(got["size"]) == ctypes.sizeof(L.GemmDesc)
+
+
+def test_ops_refuse_cpu_tensors():
+    a = torch.zeros(16, 64, dtype=torch.bfloat16)
+    w = torch.zeros(64, 64, dtype=torch.bfloat16)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ops.gemm(a, w)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ops.layer_norm(a, torch.ones(64), torch.zeros(64))
+
+
+def test_error_path_raises_with_message():
+    with pytest.raises(L.VdiffError, match="invalid argument"):
+        L.check(1000, "probe")

@@ -1,0 +1,255 @@
+"""Kernel parity on the MI355X: every HIP entry point vs a plain PyTorch
+fp32/fp64 reference of the same op on the same bf16-rounded inputs.
+
+Tolerances (written per test): fp32-output kernels must meet the north-star
+rtol=1e-3 / atol=1e-4 (scaled by the output's magnitude where noted);
+bf16-output kernels are allowed one bf16 rounding of the output
+(rel 2^-8) plus a small absolute floor.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from vdiff import ops
+from vdiff.dist import block_transpose_reference
+from vdiff.models.layers import pack_conv3x3, pack_geglu
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def bf(x):
+    return x.to(BF)
+
+
+def close_bf16(got, want, rel=1 / 128, abs_frac=2e-3):
+    want = want.double().cpu()
+    got = got.double().cpu()
+    scale = want.abs().max().item() + 1e-12
+    err = (got - want).abs()
+    bound = rel * want.abs() + abs_frac * scale
+    bad = (err > bound).sum().item()
+    assert bad == 0, f"{bad} / {want.numel()} elements out of tolerance; max err {err.max().item():.3e} (scale {scale:.3e})"
+
+
+def close_f32(got, want, rtol=1e-3, atol=1e-4):
+    torch.testing.assert_close(got.double().cpu(), want.double().cpu(), rtol=rtol, atol=atol)
+
+
+def rnd(*shape, std=1.0, dev="cuda"):
+    return bf(torch.randn(*shape, device=dev) * std)
+
+
+# ---------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("M,N,K", [(300, 320, 640), (128, 64, 64), (1000, 160, 128), (2, 1280, 1280),
+                                   (154, 640, 768), (4096, 1280, 320)])
+def test_gemm_fp32_out_bias(cuda, M, N, K):
+    a, w = rnd(M, K), rnd(N, K, std=K ** -0.5)
+    b = torch.randn(N, device=cuda)
+    got = ops.gemm(a, w, bias=b, out_f32=True)
+    want = a.double() @ w.double().T + b.double()
+    close_f32(got, want, rtol=1e-3, atol=1e-4)
+
+
+def test_gemm_epilogues(cuda):
+    M, N, K = 520, 320, 192
+    a, a1, w = rnd(M, 128), rnd(M, 64), rnd(N, K, std=0.1)
+    b = torch.randn(N, device=cuda)
+    temb = torch.randn(3, 400, device=cuda)[:, 40:40 + N]       # column-slice view, like Ctx.temb_all
+    res = rnd(M, N)
+    rb_div = 200
+    got = ops.gemm(a, w, a1=a1, bias=b, rowbias=temb, rb_div=rb_div, res=res)
+    x = torch.cat([a, a1], 1).double()
+    idx = torch.arange(M, device=cuda) // rb_div
+    want = x @ w.double().T + b.double() + temb.double()[idx] + res.double()
+    close_bf16(got, want)
+    got = ops.gemm(a, w, a1=a1, bias=b, act=ops.ACT_SILU)
+    close_bf16(got, F.silu(x @ w.double().T + b.double()))
+
+
+def test_gemm_geglu(cuda):
+    M, C = 333, 64
+    n = rnd(M, C)
+    w = rnd(8 * C, C, std=0.2)
+    b = torch.randn(8 * C, device=cuda) * 0.1
+    got = ops.gemm(n, pack_geglu(w), bias=pack_geglu(b), act=ops.ACT_GEGLU)
+    hg = n.double() @ w.double().T + b.double()
+    h, g = hg.chunk(2, -1)
+    close_bf16(got, h * F.gelu(g))
+
+
+# ---------------------------------------------------------------- conv
+@pytest.mark.parametrize("case", ["s1", "s2", "up", "concat", "cin8", "cout4"])
+def test_conv3x3(cuda, case):
+    torch.manual_seed(1)
+    n, h, w = 3, 12, 10
+    c0, c1, co = 64, 0, 128
+    stride, up = 1, False
+    if case == "s2":
+        stride = 2
+    if case == "up":
+        up = True
+    if case == "concat":
+        c1 = 32
+    if case == "cin8":
+        c0, co = 8, 64
+    if case == "cout4":
+        co = 4
+    x0 = rnd(n * h * w, c0)
+    x1 = rnd(n * h * w, c1) if c1 else None
+    wt = bf(torch.randn(co, c0 + c1, 3, 3, device=cuda) * 0.05)
+    b = torch.randn(co, device=cuda)
+    out, ho, wo = ops.conv3x3(x0, n, h, w, pack_conv3x3(wt), x1=x1, stride=stride, upsample=up, bias=b,
+                              out_f32=True)
+    xin = x0 if x1 is None else torch.cat([x0, x1], 1)
+    img = xin.double().reshape(n, h, w, -1).permute(0, 3, 1, 2)
+    if up:
+        img = F.interpolate(img, scale_factor=2.0, mode="nearest")
+    want = F.conv2d(img.cpu(), wt.double().cpu(), b.double().cpu(), stride=stride, padding=1)
+    want = want.permute(0, 2, 3, 1).reshape(-1, co)
+    assert out.shape == want.shape
+    close_f32(out, want, rtol=1e-3, atol=1e-4 * max(1.0, want.abs().max().item()))
+
+
+# ---------------------------------------------------------------- norms
+@pytest.mark.parametrize("kind", ["image", "video", "concat"])
+def test_group_norm(cuda, kind):
+    torch.manual_seed(2)
+    frames = 4 if kind == "video" else 1
+    n_img, hw, C = 8, 96, 320
+    c0 = 192 if kind == "concat" else C
+    x = rnd(n_img * hw, c0) * 3 + 1.5          # non-zero mean: exercises the shifted statistics
+    x1 = rnd(n_img * hw, C - c0) if kind == "concat" else None
+    g = torch.rand(C, device=cuda) + 0.5
+    be = torch.randn(C, device=cuda)
+    n_inst, pix = n_img // frames, frames * hw
+    got = ops.group_norm(x, n_inst, pix, 32, 1e-5, g, be, silu=True, x1=x1)
+    xx = x if x1 is None else torch.cat([x, x1], 1)
+    t = xx.double().reshape(n_inst, pix, C).permute(0, 2, 1)             # (inst, C, pix)
+    want = F.silu(F.group_norm(t, 32, g.double(), be.double(), 1e-5)).permute(0, 2, 1).reshape(-1, C)
+    close_bf16(got, want)
+
+
+def test_layer_norm_pe(cuda):
+    rows, C, frames, pos = 4 * 16 * 24, 320, 16, 24
+    x = rnd(rows, C) * 2 + 0.3
+    g, b = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda)
+    pe = torch.randn(32, C, device=cuda)
+    got = ops.layer_norm(x, g, b, pe=pe, pe_div=pos, pe_period=frames)
+    f = (torch.arange(rows, device=cuda) // pos) % frames
+    want = F.layer_norm(x.double(), (C,), g.double(), b.double(), 1e-5) + pe.double()[f]
+    close_bf16(got, want)
+    got = ops.layer_norm(x, g, b)
+    close_bf16(got, F.layer_norm(x.double(), (C,), g.double(), b.double(), 1e-5))
+
+
+# ---------------------------------------------------------------- attention
+def sdpa_ref(q, k, v, batch, heads, sq, skv, d, kv_div=1):
+    q = q.double().reshape(batch, sq, heads, d).transpose(1, 2)
+    kb = k.double().reshape(batch // kv_div, skv, heads, d).transpose(1, 2).repeat_interleave(kv_div, 0)
+    vb = v.double().reshape(batch // kv_div, skv, heads, d).transpose(1, 2).repeat_interleave(kv_div, 0)
+    w = torch.softmax(q @ kb.transpose(-1, -2) / math.sqrt(d), -1)
+    return (w @ vb).transpose(1, 2).reshape(batch * sq, heads * d)
+
+
+@pytest.mark.parametrize("d", [32, 40, 64, 80, 128, 160])
+@pytest.mark.parametrize("sq", [64, 300, 1024])
+def test_flash_attention_self(cuda, d, sq):
+    torch.manual_seed(3)
+    batch, heads = 2, 3
+    C = heads * d
+    qkv = rnd(batch * sq, 3 * C, std=1.5)     # fused-QKV row layout, like the product path
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    got = ops.attention(q, k, v, batch, heads, sq, sq, d)
+    close_bf16(got, sdpa_ref(q, k, v, batch, heads, sq, sq, d))
+
+
+@pytest.mark.parametrize("d", [40, 80, 160])
+def test_flash_attention_cross(cuda, d):
+    frames, videos, heads, sq, L = 4, 2, 2, 256, 77
+    C = heads * d
+    q = rnd(videos * frames * sq, C, std=1.5)
+    kv = rnd(videos * L, 2 * C, std=1.5)
+    got = ops.attention(q, kv[:, :C], kv[:, C:], videos * frames, heads, sq, L, d, kv_div=frames)
+    close_bf16(got, sdpa_ref(q, kv[:, :C], kv[:, C:], videos * frames, heads, sq, L, d, kv_div=frames))
+
+
+def test_flash_attention_rescale_spike(cuda):
+    """Force the online-softmax rescale branch: one key in a LATE tile dominates
+    (cdna_hip_programming.md §5.4 rule 26)."""
+    batch, heads, sq, d = 1, 1, 128, 64
+    q = rnd(sq, d)
+    k = rnd(sq, d) * 0.1
+    v = rnd(sq, d)
+    k[100] = bf(q[5].float() * 4)   # spike for query 5 at key 100 (tile 1)
+    got = ops.attention(q, k, v, batch, heads, sq, sq, d)
+    close_bf16(got, sdpa_ref(q, k, v, batch, heads, sq, sq, d))
+
+
+@pytest.mark.parametrize("frames,d", [(16, 40), (16, 160), (4, 32), (32, 80), (5, 64)])
+def test_temporal_attention(cuda, frames, d):
+    batch, pos, heads = 2, 37, 3
+    C = heads * d
+    qkv = rnd(batch * frames * pos, 3 * C, std=1.5)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    got = ops.temporal_attention(q, k, v, batch, frames, pos, heads, d)
+
+    def tok(t):  # rows (b, f, p) -> (b*p, f, C)
+        return t.double().reshape(batch, frames, pos, C).permute(0, 2, 1, 3).reshape(batch * pos, frames, C)
+
+    want = sdpa_ref(tok(q), tok(k), tok(v), batch * pos, heads, frames, frames, d)
+    want = want.reshape(batch, pos, frames, C).permute(0, 2, 1, 3).reshape(-1, C)
+    close_bf16(got, want)
+
+
+# ---------------------------------------------------------------- step glue
+def test_timestep_embed(cuda):
+    from oracle.unet_ref import timestep_embedding
+    ts = torch.tensor([961.0, 1.0, 500.0], device=cuda)
+    got = ops.timestep_embed(ts, 320)
+    close_bf16(got, timestep_embedding(ts.cpu(), 320))
+    step = torch.tensor([2], device=cuda, dtype=torch.int32)
+    got = ops.timestep_embed(ts, 320, step_idx=step, batch=2)
+    close_bf16(got, timestep_embedding(torch.tensor([500.0, 500.0]), 320))
+
+
+def test_pack_unpack_roundtrip(cuda):
+    x = torch.randn(2, 4, 3, 8, 6, device=cuda)
+    rows = ops.pack_latents(x, dup=2, cpad=8)
+    assert rows.shape == (2 * 2 * 3 * 48, 8)
+    assert torch.all(rows[:, 4:] == 0)
+    back = ops.unpack_nhwc(rows[: 2 * 3 * 48], 2, 4, 3, 8, 6)
+    close_bf16(back, x)
+    back2 = ops.unpack_nhwc(rows[2 * 3 * 48:], 2, 4, 3, 8, 6)
+    assert torch.equal(back, back2)
+
+
+def test_ddim_cfg_step_matches_oracle(cuda):
+    from oracle import ddim_ref
+    acp = ddim_ref.alphas_cumprod()
+    B, Cc, Fr, H, W = 1, 4, 3, 8, 8
+    lat = torch.randn(B, Cc, Fr, H, W, device=cuda)
+    eps_rows = torch.randn(2 * Fr * H * W, 4, device=cuda)
+    t, n = 961, 50
+    prev = t - 1000 // n
+    coef = torch.stack([acp[t] ** 0.5, (1 - acp[t]) ** 0.5, acp[prev] ** 0.5, (1 - acp[prev]) ** 0.5]).float()
+    x = lat.clone()
+    x0 = torch.empty_like(x)
+    nxt = torch.empty(2 * Fr * H * W, 8, device=cuda, dtype=BF)
+    ops.ddim_cfg_step(eps_rows, 2, 7.5, x, coef.to(cuda), x0_out=x0, next_in=nxt)
+    e = eps_rows.cpu().reshape(2, Fr, H, W, 4).permute(0, 4, 1, 2, 3)
+    want, want0 = ddim_ref.ddim_step(ddim_ref.cfg_combine(e, 7.5), t, lat.cpu(), n, acp)
+    close_f32(x, want, rtol=1e-5, atol=1e-5)
+    close_f32(x0, want0, rtol=1e-5, atol=1e-5)
+    close_bf16(ops.unpack_nhwc(nxt[: Fr * H * W], 1, 4, Fr, H, W), want)
+
+
+def test_step_advance_and_block_transpose(cuda):
+    s = torch.zeros(1, device=cuda, dtype=torch.int32)
+    ops.step_advance(s)
+    ops.step_advance(s)
+    assert s.item() == 2
+    src = rnd(2 * 3 * 5, 16)
+    close_bf16(ops.block_transpose(src, 2, 3, 5), block_transpose_reference(src.cpu(), 2, 3, 5))

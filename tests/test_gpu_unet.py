@@ -1,0 +1,168 @@
+"""Module- and model-level parity on the MI355X against the CPU oracle.
+
+Module tests use random weights sharper than the §8d synthetic init (std 0.1,
+attention q/k 0.3) so attention is far from uniform and the cross-attention /
+time-embedding paths move the output well above bf16 noise — the whole-UNet
+test alone cannot see them (with std 0.02 weights cond and uncond eps differ by
+only 0.24%, below the bf16 storage noise of the network).
+
+Tolerance: the device path stores bf16 activations; the whole tiny UNet is
+compared by relative L2 error against the fp32 oracle with a bound of 3% (the
+oracle itself with bf16 storage emulated lands at 1.4%, committed in
+tests/golden/tiny_unet.npz) and against the bf16-emulating oracle at 3%;
+module tests use 2.5% rel-L2 (a few bf16 roundings in sequence).
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ddim_ref, unet_ref
+from vdiff import DDIMScheduler, DenoiseLoop, UNetMotionModel, init_synthetic_, ops
+from vdiff.config import TINY
+from vdiff.models.blocks import AnimateDiffTransformer3D, Ctx, ResnetBlock2D, Transformer2DModel
+from vdiff.models.layers import Act
+
+pytestmark = pytest.mark.gpu
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def rel_l2(got, want):
+    got, want = got.double().cpu(), want.double().cpu()
+    return ((got - want).norm() / want.norm()).item()
+
+
+def randomize_(mod, seed, std=0.1, attn_std=0.3):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for n, p in mod.named_parameters():
+            s = attn_std if (".to_q" in n or ".to_k" in n) else std
+            r = torch.randn(p.shape, generator=g) * s
+            if ("norm" in n.split(".")[-2]) and n.endswith("weight"):
+                r = r + 1.0
+            p.copy_(r.to(torch.bfloat16).float())
+    return mod
+
+
+def sd_of(mod, prefix):
+    return {f"{prefix}.{k}": v.detach().float().cpu() for k, v in mod.state_dict().items()}
+
+
+def to_rows(x):  # (N, C, H, W) -> NHWC rows bf16 on GPU
+    n, c, h, w = x.shape
+    return x.permute(0, 2, 3, 1).reshape(n * h * w, c).to("cuda", torch.bfloat16).contiguous()
+
+
+def from_rows(t, n, h, w):
+    return t.float().cpu().reshape(n, h, w, -1).permute(0, 3, 1, 2)
+
+
+def test_resnet_block_concat_shortcut(cuda):
+    cin_x, cin_s, cout, tdim = 128, 64, 128, 256
+    B, Fr, H, W = 2, 2, 16, 16
+    r = randomize_(ResnetBlock2D(cin_x + cin_s, cout, tdim), 0)
+    sd = sd_of(r, "r")
+    r = r.to("cuda", torch.bfloat16)
+    r.prepare()
+    x = torch.randn(B * Fr, cin_x, H, W).to(torch.bfloat16).float()
+    s = torch.randn(B * Fr, cin_s, H, W).to(torch.bfloat16).float()
+    temb = torch.randn(B, tdim).to(torch.bfloat16).float()
+    temb_silu = torch.nn.functional.silu(temb).to(torch.bfloat16).float()
+    temb_all = ops.gemm(temb_silu.to("cuda", torch.bfloat16), r.time_emb_proj.weight.to(torch.bfloat16),
+                        bias=r.time_emb_proj.bias.float(), out_f32=True)
+    ctx = Ctx(B, Fr, temb_all, None, 77)
+    out = r(Act(to_rows(x), B * Fr, H, W), ctx, skip=Act(to_rows(s), B * Fr, H, W))
+    want = unet_ref.resnet(sd, "r", torch.cat([x, s], 1), temb_silu.repeat_interleave(Fr, 0), 32)
+    assert rel_l2(from_rows(out.t, B * Fr, H, W), want) < 0.025
+
+
+def test_transformer2d_with_cross_attention(cuda):
+    heads, C, L, D = 2, 64, 77, 64
+    B, Fr, H, W = 2, 2, 16, 16
+    t = randomize_(Transformer2DModel(heads, C // heads, C, D), 1)
+    sd = sd_of(t, "t")
+    t = t.to("cuda", torch.bfloat16)
+    t.prepare()
+    x = torch.randn(B * Fr, C, H, W).to(torch.bfloat16).float()
+    ehs = torch.randn(B, L, D).to(torch.bfloat16).float()
+    ctx = Ctx(B, Fr, None, ehs.reshape(B * L, D).to("cuda", torch.bfloat16), L)
+    out = t(Act(to_rows(x), B * Fr, H, W), ctx)
+    want = unet_ref.transformer2d(sd, "t", x, ehs.repeat_interleave(Fr, 0), heads, 32)
+    got = from_rows(out.t, B * Fr, H, W)
+    assert rel_l2(got, want) < 0.025
+    # the cross-attention path must matter at this weight scale
+    ctx2 = Ctx(B, Fr, None, torch.zeros_like(ctx.ehs_rows), L)
+    other = from_rows(t(Act(to_rows(x), B * Fr, H, W), ctx2).t, B * Fr, H, W)
+    assert rel_l2(other, want) > 0.05
+
+
+def test_motion_module(cuda):
+    heads, C = 2, 64
+    B, Fr, H, W = 2, 8, 8, 8
+    m = randomize_(AnimateDiffTransformer3D(heads, C // heads, C), 2)
+    sd = sd_of(m, "m")
+    m = m.to("cuda", torch.bfloat16)
+    m.prepare()
+    x = (torch.randn(B * Fr, C, H, W) + 0.5).to(torch.bfloat16).float()
+    ctx = Ctx(B, Fr, None, None, 77)
+    out = m(Act(to_rows(x), B * Fr, H, W), ctx)
+    want = unet_ref.motion_module(sd, "m", x, Fr, heads, 32, 32)
+    assert rel_l2(from_rows(out.t, B * Fr, H, W), want) < 0.025
+
+
+@pytest.fixture(scope="module")
+def tiny_unet(cuda):
+    m = init_synthetic_(UNetMotionModel("tiny"), seed=0)
+    return m.to("cuda", torch.bfloat16).prepare()
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return np.load(GOLD / "tiny_unet.npz")
+
+
+@pytest.mark.parametrize("t", [961, 500, 1])
+def test_tiny_unet_matches_oracle(tiny_unet, gold, t):
+    lat = torch.from_numpy(gold["latents"]).cuda()
+    ehs = torch.from_numpy(gold["ehs"]).cuda()
+    out = tiny_unet(torch.cat([lat, lat]), t, encoder_hidden_states=ehs).sample
+    assert out.shape == (2, 4, 4, 64, 64) and out.dtype == torch.float32
+    want = torch.from_numpy(gold[f"eps_t{t}"])
+    err = rel_l2(out, want)
+    assert err < 0.03, err
+    if t == 961:
+        assert rel_l2(out, torch.from_numpy(gold["eps_t961_bf16emu"])) < 0.03
+
+
+def test_scheduler_step_api_matches_oracle(tiny_unet, gold):
+    lat = torch.from_numpy(gold["latents"]).cuda()
+    ehs = torch.from_numpy(gold["ehs"]).cuda()
+    s = DDIMScheduler.from_config(DDIMScheduler().config, beta_schedule="linear", steps_offset=1,
+                                  clip_sample=False)
+    s.set_timesteps(50)
+    t = int(s.timesteps[0])
+    eps = tiny_unet(torch.cat([lat, lat]), t, encoder_hidden_states=ehs).sample
+    u, c = eps.chunk(2)
+    out = s.step(u + 7.5 * (c - u), t, lat)
+    assert rel_l2(out.prev_sample, torch.from_numpy(gold["ddim_step0_x"])) < 0.01
+    # exact DDIM arithmetic on identical eps
+    acp = ddim_ref.alphas_cumprod()
+    e = (u + 7.5 * (c - u)).cpu()
+    want, want0 = ddim_ref.ddim_step(e, t, lat.cpu(), 50, acp)
+    torch.testing.assert_close(out.prev_sample.cpu(), want, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(out.pred_original_sample.cpu(), want0, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_denoise_loop_graph_matches_oracle(tiny_unet, gold, use_graph):
+    lat = torch.from_numpy(gold["latents"]).cuda()
+    ehs = torch.from_numpy(gold["ehs"]).cuda()
+    s = DDIMScheduler(beta_schedule="linear", steps_offset=1, clip_sample=False)
+    s.set_timesteps(50)
+    loop = DenoiseLoop(tiny_unet, s, lat, ehs, 7.5, use_graph=use_graph).prime()
+    if use_graph:
+        assert loop.graph is not None, loop.graph_error
+    x = loop.run(3)
+    assert int(loop.step_idx.item()) == 3
+    assert rel_l2(x, torch.from_numpy(gold["loop3_x"])) < 0.01

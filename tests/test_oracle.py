@@ -1,0 +1,103 @@
+"""The CPU oracle against the pinned known-answers and the committed fixtures (CPU)."""
+import math
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ddim_ref, unet_ref
+from vdiff.config import TINY
+from vdiff.sched import DDIMScheduler
+
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def test_alphas_cumprod_check_values():
+    # SURVEY.md App. A.7 check values (fp32 cumprod of linspace(0.00085, 0.012, 1000))
+    acp = ddim_ref.alphas_cumprod()
+    for t, v in [(961, 0.00247833), (921, 0.00391383), (981, 0.00195883), (1, 0.99828953), (0, 0.99914998)]:
+        assert abs(float(acp[t]) - v) < 5e-8, t
+
+
+def test_leading_timesteps():
+    assert list(ddim_ref.timesteps_leading(25)[:3]) == [961, 921, 881]
+    assert ddim_ref.timesteps_leading(25)[-1] == 1
+    assert list(ddim_ref.timesteps_leading(50)[:2]) == [981, 961]
+    assert len(ddim_ref.timesteps_leading(15)) == 15
+
+
+def test_product_scheduler_host_math_matches_oracle():
+    # the reference's override idiom: from_config(base, beta_schedule="linear", ...)
+    base = DDIMScheduler().config
+    s = DDIMScheduler.from_config(base, beta_schedule="linear", steps_offset=1, clip_sample=False)
+    tab = np.load(GOLD / "ddim_tables.npz")
+    for n in (15, 25, 50):
+        s.set_timesteps(n)
+        assert s.timesteps.tolist() == tab[f"ts{n}"].tolist()
+        np.testing.assert_array_equal(s.coefficient_table().numpy(), tab[f"coef{n}"])
+    np.testing.assert_array_equal(s.alphas_cumprod.numpy(), tab["alphas_cumprod"])
+    assert s.init_noise_sigma == 1.0 and s.order == 1
+    x = torch.randn(3)
+    assert s.scale_model_input(x, 5) is x
+
+
+def test_scheduler_spacings_and_defaults():
+    s = DDIMScheduler(beta_schedule="linear", timestep_spacing="trailing")
+    s.set_timesteps(10)
+    assert s.timesteps[0] == 999 and s.timesteps[-1] == 99
+    s = DDIMScheduler(beta_schedule="linear", timestep_spacing="linspace")
+    s.set_timesteps(10)
+    assert s.timesteps[0] == 999 and s.timesteps[-1] == 0
+    # SD-1.5 default schedule is scaled_linear
+    assert DDIMScheduler().config.beta_schedule == "scaled_linear"
+
+
+def test_timestep_embedding_closed_form():
+    e = unet_ref.timestep_embedding(torch.tensor([0.0, 500.0]), 320)
+    assert torch.allclose(e[0, :160], torch.ones(160)) and torch.allclose(e[0, 160:], torch.zeros(160))
+    j = 7
+    f = math.exp(-math.log(10000.0) * j / 160)
+    assert abs(float(e[1, j]) - math.cos(500 * f)) < 1e-4  # fp32 argument
+    assert abs(float(e[1, 160 + j]) - math.sin(500 * f)) < 1e-4
+
+
+def test_sinusoidal_pe_closed_form():
+    pe = unet_ref.sinusoidal_pe(32, 320)
+    assert pe.shape == (1, 32, 320)
+    assert float(pe[0, 3, 0]) == pytest.approx(math.sin(3.0), abs=1e-6)
+    assert float(pe[0, 3, 1]) == pytest.approx(math.cos(3.0), abs=1e-6)
+    assert float(pe[0, 5, 10]) == pytest.approx(math.sin(5 * math.exp(-10 * math.log(1e4) / 320)), abs=1e-6)
+
+
+def test_oracle_blocks_match_torch_module_semantics():
+    """Cross-check the functional oracle against torch.nn modules of the same math."""
+    torch.manual_seed(0)
+    C, heads = 64, 2
+    sd = {}
+    for n in ("to_q", "to_k", "to_v"):
+        sd[f"a.{n}.weight"] = torch.randn(C, C) * 0.1
+    sd["a.to_out.0.weight"] = torch.randn(C, C) * 0.1
+    sd["a.to_out.0.bias"] = torch.randn(C) * 0.1
+    x = torch.randn(3, 10, C)
+    ref = torch.nn.MultiheadAttention(C, heads, bias=False, batch_first=True)
+    with torch.no_grad():
+        ref.in_proj_weight.copy_(torch.cat([sd["a.to_q.weight"], sd["a.to_k.weight"], sd["a.to_v.weight"]]))
+        ref.out_proj.weight.copy_(sd["a.to_out.0.weight"])
+    want = ref(x, x, x, need_weights=False)[0] + sd["a.to_out.0.bias"]
+    got = unet_ref.attention(sd, "a", x, None, heads)
+    assert torch.allclose(got, want, atol=1e-5)
+
+
+@pytest.mark.slow
+def test_oracle_reproduces_committed_fixture():
+    """Regression pin: the oracle still produces the committed tiny-config eps."""
+    import make_golden_path  # noqa: F401  (adds tests/golden to sys.path)
+    from make_golden import tiny_inputs
+
+    sd, lat, ehs = tiny_inputs()
+    gold = np.load(GOLD / "tiny_unet.npz")
+    np.testing.assert_array_equal(gold["latents"], lat.numpy())
+    with torch.no_grad():
+        eps = unet_ref.unet_forward(sd, TINY, torch.cat([lat, lat]), 961, ehs)
+    np.testing.assert_allclose(eps.numpy(), gold["eps_t961"], rtol=1e-4, atol=1e-5)

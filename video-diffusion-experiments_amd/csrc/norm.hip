@@ -1,0 +1,293 @@
+// GroupNorm (+SiLU) and LayerNorm (+sinusoidal PE) over NHWC bf16 rows — HBM-bound.
+//
+// GroupNorm replaces torch.nn.GroupNorm in ResnetBlock2D.norm1/norm2 (with the
+// following SiLU fused), Transformer2DModel.norm, conv_norm_out and the
+// motion-module norm whose statistics span (C/G, F, H, W) (SURVEY.md §8a a11,
+// App. A.2-A.4).  Statistics are computed in three cheap stages so the big
+// pass is spread over >1000 workgroups and stays deterministic (no atomics):
+//   partial  : per (instance, pixel-split, channel) shifted sums -> {n, mean, M2}
+//   finalize : Chan-combine splits and the C/G channels of each group -> {a, b}
+//   apply    : y = x*a + b (+SiLU), 16-byte vector loads/stores.
+// With frame sharding the partial records of all ranks are all-gathered and
+// finalize simply sees more splits.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ const bf16_t* gn_src(const bf16_t* x0, int64_t ldx0, int64_t c0,
+                                                const bf16_t* x1, int64_t ldx1, int64_t row,
+                                                int64_t c) {
+  return c < c0 ? x0 + row * ldx0 + c : x1 + row * ldx1 + (c - c0);
+}
+
+__global__ __launch_bounds__(NT) void gn_partial_kernel(const bf16_t* x0, int64_t ldx0, int64_t c0,
+                                                        const bf16_t* x1, int64_t ldx1, int64_t C,
+                                                        int64_t pix_per_inst, int n_split,
+                                                        float4* ws) {
+  __shared__ float4 red[NT * 8];  // [task][8 channels] {n, mean, M2, -}
+  const int inst = blockIdx.x / n_split;
+  const int split = blockIdx.x % n_split;
+  const int64_t pb = pix_per_inst * split / n_split;
+  const int64_t pe = pix_per_inst * (split + 1) / n_split;
+  const int64_t row0 = (int64_t)inst * pix_per_inst;
+  const int nch = (int)(C / 8);
+  const int PL = nch >= NT ? 1 : NT / nch;
+  const int ntask = PL * nch;
+  float4* out = ws + ((int64_t)inst * n_split + split) * C;
+
+  for (int task = threadIdx.x; task < ((ntask + NT - 1) / NT) * NT; task += NT) {
+    const bool active = task < ntask;
+    const int pl = task / nch;
+    const int j = task - pl * nch;
+    float s1[8], s2[8], sh[8];
+    int cnt = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; sh[e] = 0.f; }
+    if (active) {
+      for (int64_t p = pb + pl; p < pe; p += PL) {
+        const uint4 u = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row0 + p, (int64_t)j * 8);
+        float f[8];
+        unpack8(u, f);
+        if (cnt == 0) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sh[e] = f[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = f[e] - sh[e];
+          s1[e] += t;
+          s2[e] = fmaf(t, t, s2[e]);
+        }
+        ++cnt;
+      }
+    }
+    if (PL == 1) {
+      if (active) {
+        for (int e = 0; e < 8; ++e) {
+          const float n = (float)cnt;
+          const float mean = cnt ? sh[e] + s1[e] / n : 0.f;
+          const float m2 = cnt ? fmaxf(s2[e] - s1[e] * s1[e] / n, 0.f) : 0.f;
+          out[(int64_t)j * 8 + e] = make_float4(n, mean, m2, 0.f);
+        }
+      }
+    } else {
+      // ntask <= NT here: one pass, reduce the PL pixel lanes of each chunk via LDS.
+      if (active) {
+        for (int e = 0; e < 8; ++e) {
+          const float n = (float)cnt;
+          const float mean = cnt ? sh[e] + s1[e] / n : 0.f;
+          const float m2 = cnt ? fmaxf(s2[e] - s1[e] * s1[e] / n, 0.f) : 0.f;
+          red[task * 8 + e] = make_float4(n, mean, m2, 0.f);
+        }
+      }
+      __syncthreads();
+      for (int c = threadIdx.x; c < nch * 8; c += NT) {
+        const int jj = c >> 3, e = c & 7;
+        float n = 0.f, mean = 0.f, m2 = 0.f;
+        for (int q = 0; q < PL; ++q) {
+          const float4 r = red[(q * nch + jj) * 8 + e];
+          if (r.x == 0.f) continue;
+          const float nn = n + r.x;
+          const float delta = r.y - mean;
+          mean += delta * (r.x / nn);
+          m2 += r.z + delta * delta * (n * r.x / nn);
+          n = nn;
+        }
+        out[c] = make_float4(n, mean, m2, 0.f);
+      }
+      break;
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void gn_finalize_kernel(const float4* ws, int n_split, int64_t C,
+                                                         int groups, float eps, const float* gamma,
+                                                         const float* beta, float2* ss) {
+  extern __shared__ float4 chs[];  // [C] {n, mean, M2}; then [groups] {mean, rstd}
+  const int inst = blockIdx.x;
+  const float4* src = ws + (int64_t)inst * n_split * C;
+  for (int64_t c = threadIdx.x; c < C; c += NT) {
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    for (int s = 0; s < n_split; ++s) {
+      const float4 r = src[(int64_t)s * C + c];
+      if (r.x == 0.f) continue;
+      const float nn = n + r.x;
+      const float delta = r.y - mean;
+      mean += delta * (r.x / nn);
+      m2 += r.z + delta * delta * (n * r.x / nn);
+      n = nn;
+    }
+    chs[c] = make_float4(n, mean, m2, 0.f);
+  }
+  __syncthreads();
+  const int cpg = (int)(C / groups);
+  float4* gst = chs + C;
+  for (int g = threadIdx.x; g < groups; g += NT) {
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    for (int q = 0; q < cpg; ++q) {
+      const float4 r = chs[g * cpg + q];
+      if (r.x == 0.f) continue;
+      const float nn = n + r.x;
+      const float delta = r.y - mean;
+      mean += delta * (r.x / nn);
+      m2 += r.z + delta * delta * (n * r.x / nn);
+      n = nn;
+    }
+    const float var = n > 0.f ? m2 / n : 0.f;
+    gst[g] = make_float4(mean, rsqrtf(var + eps), 0.f, 0.f);
+  }
+  __syncthreads();
+  for (int64_t c = threadIdx.x; c < C; c += NT) {
+    const float4 st = gst[c / cpg];
+    const float a = st.y * gamma[c];
+    ss[(int64_t)inst * C + c] = make_float2(a, beta[c] - st.x * a);
+  }
+}
+
+__global__ __launch_bounds__(NT) void gn_apply_kernel(const bf16_t* x0, int64_t ldx0, int64_t c0,
+                                                      const bf16_t* x1, int64_t ldx1, int64_t C,
+                                                      int64_t rows, int64_t pix_per_inst,
+                                                      const float2* ss, int silu, bf16_t* y,
+                                                      int64_t ldy) {
+  const int64_t nch = C / 8;
+  const int64_t total = rows * nch;
+  for (int64_t idx = (int64_t)blockIdx.x * NT + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * NT) {
+    const int64_t row = idx / nch;
+    const int64_t c = (idx - row * nch) * 8;
+    const uint4 u = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row, c);
+    const float4* sp = (const float4*)(ss + (row / pix_per_inst) * C + c);
+    float f[8];
+    unpack8(u, f);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 ab = sp[q];
+      f[2 * q] = fmaf(f[2 * q], ab.x, ab.y);
+      f[2 * q + 1] = fmaf(f[2 * q + 1], ab.z, ab.w);
+    }
+    if (silu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = silu_f(f[e]);
+    }
+    *(uint4*)(y + row * ldy + c) = pack8(f);
+  }
+}
+
+// One wave per row; up to LNCH 16-byte chunks per lane (C <= 64*8*LNCH).
+constexpr int LNCH = 4;
+__global__ __launch_bounds__(NT) void layernorm_kernel(const bf16_t* x, int64_t ldx, int64_t rows,
+                                                       int C, const float* gamma, const float* beta,
+                                                       float eps, const float* pe, int64_t pe_div,
+                                                       int64_t pe_period, bf16_t* y, int64_t ldy) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nch = C / 8;
+  float v[LNCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < LNCH; ++q) {
+    const int j = lane + 64 * q;
+    if (j < nch) {
+      unpack8(*(const uint4*)(x + row * ldx + j * 8), v[q]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[q][e];
+    }
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < LNCH; ++q) {
+    if (lane + 64 * q < nch) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float t = v[q][e] - mean;
+        s2 = fmaf(t, t, s2);
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(s2) / (float)C + eps);
+  const float* per = pe ? pe + ((row / pe_div) % pe_period) * C : nullptr;
+#pragma unroll
+  for (int q = 0; q < LNCH; ++q) {
+    const int j = lane + 64 * q;
+    if (j < nch) {
+      float o[8];
+      const float4 g0 = *(const float4*)(gamma + j * 8), g1 = *(const float4*)(gamma + j * 8 + 4);
+      const float4 b0 = *(const float4*)(beta + j * 8), b1 = *(const float4*)(beta + j * 8 + 4);
+      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fmaf((v[q][e] - mean) * rstd, gg[e], bb[e]);
+      if (per) {
+        const float4 p0 = *(const float4*)(per + j * 8), p1 = *(const float4*)(per + j * 8 + 4);
+        o[0] += p0.x; o[1] += p0.y; o[2] += p0.z; o[3] += p0.w;
+        o[4] += p1.x; o[5] += p1.y; o[6] += p1.z; o[7] += p1.w;
+      }
+      *(uint4*)(y + row * ldy + j * 8) = pack8(o);
+    }
+  }
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" int vd_gn_partial(const void* x0, int64_t ldx0, int64_t c0, const void* x1,
+                             int64_t ldx1, int64_t C, int64_t n_inst, int64_t pix_per_inst,
+                             int32_t n_split, float* ws, vd_stream_t stream) {
+  VD_CHECK_ARG(x0 && ws && C > 0 && C % 8 == 0 && c0 % 8 == 0 && c0 > 0 && c0 <= C);
+  VD_CHECK_ARG(ldx0 % 8 == 0 && al16(x0) && al16(ws));
+  if (c0 < C) VD_CHECK_ARG(x1 && ldx1 % 8 == 0 && al16(x1));
+  VD_CHECK_ARG(n_inst > 0 && pix_per_inst > 0 && n_split > 0 && n_split <= pix_per_inst);
+  VD_CHECK_ARG(n_inst * n_split < 0x7fffffff);
+  hipLaunchKernelGGL(gn_partial_kernel, dim3((unsigned)(n_inst * n_split)), dim3(NT), 0,
+                     (hipStream_t)stream, (const bf16_t*)x0, ldx0, c0, (const bf16_t*)x1, ldx1, C,
+                     pix_per_inst, n_split, (float4*)ws);
+  return vd_launch_status();
+}
+
+extern "C" int vd_gn_finalize(const float* ws, int64_t n_inst, int32_t n_split_total, int64_t C,
+                              int32_t groups, float eps, const float* gamma, const float* beta,
+                              float* scale_shift, vd_stream_t stream) {
+  VD_CHECK_ARG(ws && gamma && beta && scale_shift && n_inst > 0 && n_split_total > 0);
+  VD_CHECK_ARG(groups > 0 && C % groups == 0 && C <= 8192);
+  const size_t lds = (size_t)(C + groups) * sizeof(float4);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)n_inst), dim3(NT), lds,
+                     (hipStream_t)stream, (const float4*)ws, n_split_total, C, groups, eps, gamma,
+                     beta, (float2*)scale_shift);
+  return vd_launch_status();
+}
+
+extern "C" int vd_gn_apply(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1,
+                           int64_t C, int64_t n_inst, int64_t pix_per_inst,
+                           const float* scale_shift, int32_t silu, void* y, int64_t ldy,
+                           vd_stream_t stream) {
+  VD_CHECK_ARG(x0 && y && scale_shift && C > 0 && C % 8 == 0 && c0 % 8 == 0 && c0 > 0 && c0 <= C);
+  VD_CHECK_ARG(ldx0 % 8 == 0 && ldy % 8 == 0 && al16(x0) && al16(y) && al16(scale_shift));
+  if (c0 < C) VD_CHECK_ARG(x1 && ldx1 % 8 == 0 && al16(x1));
+  const int64_t rows = n_inst * pix_per_inst;
+  const int64_t total = rows * (C / 8);
+  const int64_t blocks = (total + NT - 1) / NT;
+  const unsigned grid = (unsigned)(blocks < 8192 ? blocks : 8192);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream,
+                     (const bf16_t*)x0, ldx0, c0, (const bf16_t*)x1, ldx1, C, rows, pix_per_inst,
+                     (const float2*)scale_shift, silu, (bf16_t*)y, ldy);
+  return vd_launch_status();
+}
+
+extern "C" int vd_layernorm(const void* x, int64_t ldx, int64_t rows, int64_t C, const float* gamma,
+                            const float* beta, float eps, const float* pe, int64_t pe_div,
+                            int64_t pe_period, void* y, int64_t ldy, vd_stream_t stream) {
+  VD_CHECK_ARG(x && y && gamma && beta && C % 8 == 0 && C <= 64 * 8 * LNCH && rows >= 0);
+  VD_CHECK_ARG(ldx % 8 == 0 && ldy % 8 == 0 && al16(x) && al16(y) && al16(gamma) && al16(beta));
+  if (pe) VD_CHECK_ARG(al16(pe) && pe_div > 0 && pe_period > 0);
+  if (rows == 0) return VD_OK;
+  const int64_t blocks = (rows + 3) / 4;
+  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, ldx, rows, (int)C, gamma, beta, eps, pe, pe_div, pe_period,
+                     (bf16_t*)y, ldy);
+  return vd_launch_status();
+}

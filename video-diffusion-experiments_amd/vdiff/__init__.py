@@ -1,0 +1,11 @@
+"""vdiff — MI355X-native video-diffusion denoising step (AnimateDiff UNetMotionModel + DDIM).
+
+Host mirror of the reference's call surface (diffusers UNetMotionModel /
+DDIMScheduler / AnimateDiffPipeline as used by tanm-ast/video-diffusion-
+experiments) over hand-written gfx950 HIP kernels in libvdiff_hip.so.
+"""
+from .config import FULL, TINY, get_config  # noqa: F401
+from .models import UNetMotionModel, UNetMotionOutput  # noqa: F401
+from .pipeline import AnimateDiffPipeline, AnimateDiffPipelineOutput, DenoiseLoop  # noqa: F401
+from .sched import DDIMScheduler, DDIMSchedulerOutput  # noqa: F401
+from .weights import init_synthetic_, load_diffusers_state_dict  # noqa: F401

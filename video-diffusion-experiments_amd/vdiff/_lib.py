@@ -1,0 +1,87 @@
+"""ctypes binding of libvdiff_hip.so (the C ABI declared in include/vdiff.h).
+
+The library must be loaded AFTER `import torch` so its libamdhip64.so.7 /
+librccl.so.1 dependencies resolve (by SONAME) to the runtime torch already
+loaded — one HIP runtime, so torch's hipStream_t handles are valid here.
+There is no fallback: if the library is missing every op raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+LIB_PATH = Path(__file__).resolve().parent / "libvdiff_hip.so"
+
+c_i64, c_i32, c_f32, c_vp = C.c_int64, C.c_int32, C.c_float, C.c_void_p
+
+# Every exported symbol and its argtypes: the single source of truth used by the
+# loader and by tests/test_abi.py (which checks it against include/vdiff.h).
+SIGNATURES = {
+    "vd_strerror": ([c_i32], C.c_char_p),
+    "vd_version": ([], c_i32),
+    "vd_gemm": ([c_vp, c_vp], c_i32),
+    "vd_gn_partial": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp], c_i32),
+    "vd_gn_finalize": ([c_vp, c_i64, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp], c_i32),
+    "vd_gn_apply": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_i64, c_vp], c_i32),
+    "vd_layernorm": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
+    "vd_attention": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_i64, c_f32, c_vp], c_i32),
+    "vd_temporal_attention": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
+    "vd_timestep_embed": ([c_vp, c_vp, c_i64, c_i32, c_vp, c_vp], c_i32),
+    "vd_pack_latents": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp], c_i32),
+    "vd_unpack_nhwc": ([c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp], c_i32),
+    "vd_ddim_cfg_step": ([c_vp, c_i64, c_i32, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
+    "vd_step_advance": ([c_vp, c_vp], c_i32),
+    "vd_block_transpose": ([c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp], c_i32),
+}
+
+
+class GemmDesc(C.Structure):
+    """Mirror of vd_gemm_desc (include/vdiff.h)."""
+
+    _fields_ = [
+        ("a0", c_vp), ("lda0", c_i64), ("k0", c_i64),
+        ("a1", c_vp), ("lda1", c_i64),
+        ("a_mode", c_i32),
+        ("n_img", c_i32), ("h_in", c_i32), ("w_in", c_i32), ("h_out", c_i32), ("w_out", c_i32),
+        ("stride", c_i32), ("upsample", c_i32),
+        ("w", c_vp), ("ldw", c_i64),
+        ("M", c_i64), ("N", c_i64), ("K", c_i64),
+        ("bias", c_vp),
+        ("rowbias", c_vp), ("ld_rb", c_i64), ("rb_div", c_i64),
+        ("res", c_vp), ("ld_res", c_i64),
+        ("act", c_i32),
+        ("out", c_vp), ("ldc", c_i64), ("out_f32", c_i32),
+    ]
+
+
+class VdiffError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raise if the HIP build is absent."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise VdiffError(
+                f"{LIB_PATH} not found: build the HIP extension first "
+                "(python video-diffusion-experiments_amd/build_ext.py or __graft_entry__.build())")
+        h = C.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+        for name, (argt, rest) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.argtypes = argt
+            fn.restype = rest
+        _lib = h
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().vd_strerror(rc).decode()
+        raise VdiffError(f"{what}: {msg} (code {rc})")

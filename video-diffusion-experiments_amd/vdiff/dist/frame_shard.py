@@ -1,0 +1,83 @@
+"""Frame sharding of the denoising step across the GPUs of one node.
+
+SURVEY.md §8e: every op of the UNet is independent per frame except the 21
+motion modules.  Each rank holds F/world frames of BOTH CFG halves (so the CFG
+combine and the DDIM update stay local).  A motion module needs:
+
+  1. GroupNorm statistics over all frames of a video: every rank computes its
+     partial {n, mean, M2} records and they are all-gathered (tiny, latency
+     bound); the finalize kernel Chan-combines world x splits records.
+  2. The temporal window: rows are re-sharded frame-sharded -> position-sharded
+     with an all-to-all (Ulysses-style), the whole transformer block runs
+     locally over all F frames of HW/world positions, and an all-to-all brings
+     the rows back.  Volume per module per rank: 2 x (world-1)/world x the
+     local activation — 1/world of an all-gather of K and V,
+     which is why this build uses all-to-all rather than the K/V all-gather.
+
+Collectives go through torch.distributed (backend "nccl" = RCCL over xGMI on
+MI355X, "gloo" in the CPU tests) on the current stream, so they are captured
+into the step's hipGraph.  The row permutations around the all-to-alls are
+`transpose(src, nb, na, nc)` — the HIP kernel vd_block_transpose in the product
+path, injected so the decomposition itself is testable on CPU.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class FrameShard:
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def frames_local(self, frames: int) -> int:
+        if frames % self.world:
+            raise ValueError(f"{frames} frames do not shard over {self.world} ranks")
+        return frames // self.world
+
+    # -- GroupNorm statistics -------------------------------------------------
+    def gather_gn_partials(self, ws: torch.Tensor) -> torch.Tensor:
+        """[inst, splits, C, 4] per rank -> [inst, world*splits, C, 4] on every rank."""
+        out = torch.empty(self.world * ws.numel(), device=ws.device, dtype=ws.dtype)
+        dist.all_gather_into_tensor(out, ws.contiguous().reshape(-1), group=self.group)
+        return out.reshape((self.world,) + tuple(ws.shape)).transpose(0, 1).reshape(ws.shape[0], self.world * ws.shape[1], *ws.shape[2:]).contiguous()
+
+    # -- temporal window re-shard ---------------------------------------------
+    def _a2a(self, x: torch.Tensor) -> torch.Tensor:
+        out = torch.empty_like(x)
+        dist.all_to_all_single(out, x, group=self.group)
+        return out
+
+    def to_position_shards(self, h, batch, frames_local, hw, transpose):
+        """rows (b, f_loc, p) of this rank's frames -> rows (b, f, p_loc) of this rank's
+        hw/world positions, f over ALL frames."""
+        W = self.world
+        if hw % W:
+            raise ValueError(f"{hw} positions do not shard over {W} ranks")
+        pl = hw // W
+        send = transpose(h, batch * frames_local, W, pl)           # (r', b, f_loc, pl)
+        recv = self._a2a(send)                                      # (r,  b, f_loc, pl)
+        return transpose(recv, W, batch, frames_local * pl)         # (b, r, f_loc, pl) = (b, f, pl)
+
+    def to_frame_shards(self, hp, batch, frames_local, hw, transpose):
+        """Inverse of to_position_shards."""
+        W = self.world
+        pl = hw // W
+        send = transpose(hp, batch, W, frames_local * pl)           # (r', b, f_loc, pl)
+        recv = self._a2a(send)                                      # (r,  b, f_loc, pl)  r = position chunk
+        return transpose(recv, W, batch * frames_local, pl)         # (b, f_loc, r, pl) = (b, f_loc, p)
+
+    def all_gather_frames(self, x: torch.Tensor) -> torch.Tensor:
+        """(B, C, F_loc, H, W) latents of every rank -> (B, C, F, H, W)."""
+        parts = torch.empty(self.world * x.numel(), device=x.device, dtype=x.dtype)
+        dist.all_gather_into_tensor(parts, x.contiguous().reshape(-1), group=self.group)
+        return torch.cat(list(parts.reshape((self.world,) + tuple(x.shape)).unbind(0)), dim=2)
+
+
+def block_transpose_reference(src: torch.Tensor, nb: int, na: int, nc: int) -> torch.Tensor:
+    """torch statement of vd_block_transpose (for CPU tests of the decomposition):
+    dst[(a*nb + b)*nc + c] = src[(b*na + a)*nc + c]."""
+    w = src.shape[1]
+    return src.reshape(nb, na, nc, w).transpose(0, 1).reshape(nb * na * nc, w).contiguous()

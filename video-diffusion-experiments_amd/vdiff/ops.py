@@ -1,0 +1,234 @@
+"""Tensor-level wrappers over the C ABI (include/vdiff.h).
+
+Every function launches HIP kernels on torch's current stream (so it is
+hipGraph-capturable) and never falls back to a CPU or torch implementation:
+non-CUDA tensors are rejected and a missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import torch
+
+from ._lib import GemmDesc, check, lib
+
+ACT_NONE, ACT_SILU, ACT_GEGLU = 0, 1, 2
+A_DENSE, A_CONV3X3 = 0, 1
+BF16 = torch.bfloat16
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("vdiff ops run on the GPU only (got a CPU tensor); no CPU fallback")
+
+
+def _rows(t, dtype=BF16):
+    """Validate a 2-D row-major operand (unit inner stride) and return its row stride."""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"expected a 2-D row-major tensor, got shape {tuple(t.shape)} strides {t.stride()}")
+    if t.dtype != dtype:
+        raise ValueError(f"expected {dtype}, got {t.dtype}")
+    return t.stride(0)
+
+
+# ---------------------------------------------------------------- GEMM / conv
+def gemm(a, w, *, a1=None, bias=None, rowbias=None, rb_div=1, res=None, act=ACT_NONE,
+         out=None, out_f32=False):
+    """out[m, n] = epi(sum_k cat(a, a1)[m, k] * w[n, k]); a/a1/w bf16, bias/rowbias fp32."""
+    _dev(a, w, a1, bias, rowbias, res, out)
+    M = a.shape[0]
+    N, K = w.shape
+    lda0 = _rows(a)
+    k0 = a.shape[1]
+    lda1 = _rows(a1) if a1 is not None else 0
+    if a1 is not None and (a1.shape[0] != M or k0 + a1.shape[1] != K):
+        raise ValueError("concat operand shapes do not add up to K")
+    if a1 is None and k0 != K:
+        raise ValueError(f"A has {k0} columns, W has K={K}")
+    nout = N // 2 if act == ACT_GEGLU else N
+    if out is None:
+        out = torch.empty(M, nout, device=a.device, dtype=torch.float32 if out_f32 else BF16)
+    d = GemmDesc(a0=_p(a), lda0=lda0, k0=k0, a1=_p(a1), lda1=lda1, a_mode=A_DENSE,
+                 w=_p(w), ldw=_rows(w), M=M, N=N, K=K,
+                 bias=_p(bias), rowbias=_p(rowbias),
+                 ld_rb=rowbias.stride(0) if rowbias is not None else 0, rb_div=rb_div,
+                 res=_p(res), ld_res=_rows(res) if res is not None else 0, act=act,
+                 out=_p(out), ldc=_rows(out, torch.float32 if out_f32 else BF16),
+                 out_f32=int(out_f32))
+    check(lib().vd_gemm(C.byref(d), _stream()), "vd_gemm")
+    return out
+
+
+def conv3x3(x, n_img, h_in, w_in, w, *, x1=None, stride=1, upsample=False, bias=None,
+            rowbias=None, rb_div=1, res=None, act=ACT_NONE, out=None, out_f32=False):
+    """3x3 pad-1 conv over NHWC rows x (+ channel-concat x1); w packed [Cout][3][3][Cin]."""
+    _dev(x, w, x1, bias, rowbias, res, out)
+    N, K = w.shape
+    c0 = x.shape[1]
+    if K % 9 or (c0 + (x1.shape[1] if x1 is not None else 0)) * 9 != K:
+        raise ValueError("conv weight K does not match input channels")
+    if upsample:
+        h_out, w_out = 2 * h_in, 2 * w_in
+    else:
+        h_out, w_out = (h_in - 1) // stride + 1, (w_in - 1) // stride + 1
+    M = n_img * h_out * w_out
+    if x.shape[0] != n_img * h_in * w_in:
+        raise ValueError("conv input rows != n_img*h*w")
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=torch.float32 if out_f32 else BF16)
+    d = GemmDesc(a0=_p(x), lda0=_rows(x), k0=c0, a1=_p(x1),
+                 lda1=_rows(x1) if x1 is not None else 0, a_mode=A_CONV3X3,
+                 n_img=n_img, h_in=h_in, w_in=w_in, h_out=h_out, w_out=w_out,
+                 stride=stride, upsample=int(bool(upsample)),
+                 w=_p(w), ldw=_rows(w), M=M, N=N, K=K,
+                 bias=_p(bias), rowbias=_p(rowbias),
+                 ld_rb=rowbias.stride(0) if rowbias is not None else 0, rb_div=rb_div,
+                 res=_p(res), ld_res=_rows(res) if res is not None else 0, act=act,
+                 out=_p(out), ldc=_rows(out, torch.float32 if out_f32 else BF16),
+                 out_f32=int(out_f32))
+    check(lib().vd_gemm(C.byref(d), _stream()), "vd_gemm(conv3x3)")
+    return out, h_out, w_out
+
+
+# ---------------------------------------------------------------- norms
+def gn_splits(n_inst: int, pix: int) -> int:
+    return max(1, min(pix // 16, math.ceil(2048 / n_inst)))
+
+
+def gn_partial(x, C, n_inst, pix, n_split, x1=None):
+    _dev(x, x1)
+    ws = torch.empty(n_inst, n_split, C, 4, device=x.device, dtype=torch.float32)
+    check(lib().vd_gn_partial(_p(x), _rows(x), x.shape[1], _p(x1), _rows(x1) if x1 is not None else 0,
+                              C, n_inst, pix, n_split, _p(ws), _stream()), "vd_gn_partial")
+    return ws
+
+
+def gn_finalize(ws, groups, eps, gamma, beta):
+    n_inst, n_split, C, _ = ws.shape
+    ss = torch.empty(n_inst, C, 2, device=ws.device, dtype=torch.float32)
+    check(lib().vd_gn_finalize(_p(ws), n_inst, n_split, C, groups, eps, _p(gamma), _p(beta), _p(ss),
+                               _stream()), "vd_gn_finalize")
+    return ss
+
+
+def gn_apply(x, ss, pix, silu, x1=None, out=None):
+    _dev(x, x1, ss)
+    n_inst, C, _ = ss.shape
+    if out is None:
+        out = torch.empty(x.shape[0], C, device=x.device, dtype=BF16)
+    check(lib().vd_gn_apply(_p(x), _rows(x), x.shape[1], _p(x1), _rows(x1) if x1 is not None else 0,
+                            C, n_inst, pix, _p(ss), int(silu), _p(out), _rows(out), _stream()),
+          "vd_gn_apply")
+    return out
+
+
+def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, gather=None):
+    """GroupNorm(+SiLU) over NHWC rows; instance = `pix` consecutive rows.
+    `gather(ws) -> ws'` (optional) merges partial statistics across ranks."""
+    C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
+    ws = gn_partial(x, C, n_inst, pix, gn_splits(n_inst, pix), x1=x1)
+    if gather is not None:
+        ws = gather(ws)
+    ss = gn_finalize(ws, groups, eps, gamma, beta)
+    return gn_apply(x, ss, pix, silu, x1=x1)
+
+
+def layer_norm(x, gamma, beta, eps=1e-5, pe=None, pe_div=1, pe_period=1, out=None):
+    _dev(x, gamma, beta, pe)
+    rows, Cc = x.shape
+    if out is None:
+        out = torch.empty(rows, Cc, device=x.device, dtype=BF16)
+    check(lib().vd_layernorm(_p(x), _rows(x), rows, Cc, _p(gamma), _p(beta), eps, _p(pe), pe_div,
+                             pe_period, _p(out), _rows(out), _stream()), "vd_layernorm")
+    return out
+
+
+# ---------------------------------------------------------------- attention
+def attention(q, k, v, batch, heads, sq, skv, d, kv_div=1, scale=None, out=None):
+    """q/k/v: 2-D row views (may be column slices of a fused QKV buffer)."""
+    _dev(q, k, v, out)
+    if out is None:
+        out = torch.empty(batch * sq, heads * d, device=q.device, dtype=BF16)
+    scale = d ** -0.5 if scale is None else scale
+    check(lib().vd_attention(_p(q), q.stride(0), _p(k), k.stride(0), _p(v), v.stride(0), _p(out),
+                             out.stride(0), batch, heads, sq, skv, d, kv_div, scale, _stream()),
+          "vd_attention")
+    return out
+
+
+def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, out=None):
+    _dev(q, k, v, out)
+    if not (q.stride(0) == k.stride(0) == v.stride(0)):
+        raise ValueError("q/k/v must share a row stride")
+    if out is None:
+        out = torch.empty(q.shape[0], heads * d, device=q.device, dtype=BF16)
+    scale = d ** -0.5 if scale is None else scale
+    check(lib().vd_temporal_attention(_p(q), _p(k), _p(v), q.stride(0), _p(out), out.stride(0), batch,
+                                      frames, positions, heads, d, scale, _stream()),
+          "vd_temporal_attention")
+    return out
+
+
+# ---------------------------------------------------------------- step glue
+def timestep_embed(ts, dim, step_idx=None, batch=None, out=None):
+    _dev(ts, step_idx)
+    B = ts.numel() if step_idx is None else batch
+    if out is None:
+        out = torch.empty(B, dim, device=ts.device, dtype=BF16)
+    check(lib().vd_timestep_embed(_p(ts), _p(step_idx), B, dim, _p(out), _stream()), "vd_timestep_embed")
+    return out
+
+
+def pack_latents(x, dup=1, cpad=8, out=None):
+    _dev(x, out)
+    x = x.contiguous().float()
+    B, Cc, Fr, H, W = x.shape
+    if out is None:
+        out = torch.empty(dup * B * Fr * H * W, cpad, device=x.device, dtype=BF16)
+    check(lib().vd_pack_latents(_p(x), B, Cc, Fr, H, W, dup, _p(out), cpad, _stream()), "vd_pack_latents")
+    return out
+
+
+def unpack_nhwc(src, B, Cc, Fr, H, W, out=None):
+    _dev(src, out)
+    if out is None:
+        out = torch.empty(B, Cc, Fr, H, W, device=src.device, dtype=torch.float32)
+    check(lib().vd_unpack_nhwc(_p(src), int(src.dtype == torch.float32), src.stride(0), B, Cc, Fr, H, W,
+                               _p(out), _stream()), "vd_unpack_nhwc")
+    return out
+
+
+def ddim_cfg_step(eps, ncfg, guidance, latents, coef, step_idx=None, x0_out=None, next_in=None):
+    _dev(eps, latents, coef, step_idx, x0_out, next_in)
+    if latents.dtype != torch.float32 or not latents.is_contiguous():
+        raise ValueError("latents must be contiguous fp32")
+    B, Cc, Fr, H, W = latents.shape
+    check(lib().vd_ddim_cfg_step(_p(eps), eps.stride(0), ncfg, guidance, _p(latents), B, Cc, Fr, H, W,
+                                 _p(coef), _p(step_idx), _p(x0_out), _p(next_in),
+                                 next_in.shape[1] if next_in is not None else 0, _stream()),
+          "vd_ddim_cfg_step")
+
+
+def step_advance(step_idx):
+    _dev(step_idx)
+    check(lib().vd_step_advance(_p(step_idx), _stream()), "vd_step_advance")
+
+
+def block_transpose(src, nb, na, nc, out=None):
+    """dst[(a*nb + b)*nc + c] = src[(b*na + a)*nc + c] over bf16 rows."""
+    _dev(src, out)
+    width = src.shape[1]
+    if out is None:
+        out = torch.empty_like(src)
+    check(lib().vd_block_transpose(_p(src), _p(out), nb, na, nc, width, _stream()), "vd_block_transpose")
+    return out

@@ -1,0 +1,208 @@
+"""AnimateDiffPipeline-compatible denoising loop on MI355X.
+
+Mirrors the `pipe(...)` surface the reference drives at
+experiments/05_grid_search_ablation.py:121-169 (from_pretrained-like
+construction, settable `.scheduler`, enable_vae_slicing()/
+enable_model_cpu_offload() as no-ops, `pipe(prompt=, negative_prompt=,
+num_frames=, guidance_scale=, num_inference_steps=, height=, width=,
+generator=).frames[0]`) and the loop body of diffusers'
+AnimateDiffPipeline.__call__:
+
+    x_in = cat([x, x]); eps = unet(x_in, t, ehs).sample
+    eps = eps_u + g (eps_c - eps_u); x = scheduler.step(eps, t, x).prev_sample
+
+Here that body is ONE captured hipGraph (torch.cuda.CUDAGraph == hipGraph on
+ROCm): time embedding from a device timestep table indexed by a device step
+counter, the UNet on packed NHWC rows, the fused CFG+DDIM kernel that also
+writes the next step's packed input, and the counter increment — replayed
+num_inference_steps times with no host work in between.  The cross-attention
+K/V of the (constant) prompt embeddings are projected once per video, outside
+the graph.
+
+Out of scope: CLIP text encoding (a deterministic stub
+encoder stands in; real embeddings can be passed as prompt_embeds) and VAE
+decoding (output_type="latent" only).
+"""
+from __future__ import annotations
+
+import zlib
+from collections import namedtuple
+
+import torch
+
+from . import ops
+from .models.unet_motion import CIN_PAD, UNetMotionModel
+from .sched.ddim import DDIMScheduler
+from .weights import init_synthetic_
+
+AnimateDiffPipelineOutput = namedtuple("AnimateDiffPipelineOutput", ["frames"])
+
+
+class SyntheticTextEncoder:
+    """Stand-in for CLIPTextModel (out of scope): prompt -> deterministic
+    N(0,1) [77, dim] embedding seeded by crc32(prompt)."""
+
+    def __init__(self, dim: int, seq_len: int = 77):
+        self.dim, self.seq_len = dim, seq_len
+
+    def __call__(self, prompt: str) -> torch.Tensor:
+        g = torch.Generator().manual_seed(zlib.crc32(prompt.encode()))
+        return torch.randn((self.seq_len, self.dim), generator=g)
+
+
+class DenoiseLoop:
+    """Preallocated device state + the captured graph of one denoising step."""
+
+    def __init__(self, unet: UNetMotionModel, scheduler: DDIMScheduler, latents: torch.Tensor,
+                 prompt_embeds: torch.Tensor, guidance_scale: float, timesteps=None,
+                 use_graph: bool = True):
+        if not unet._prepared:
+            unet.prepare()
+        dev = unet.device
+        self.unet = unet
+        self.ncfg = 2 if guidance_scale > 1 else 1
+        self.g = float(guidance_scale)
+        self.lat = latents.to(dev, torch.float32).contiguous().clone()
+        self.B, _, self.F, self.H, self.W = self.lat.shape
+        self.Bt = self.ncfg * self.B
+        ts = scheduler.timesteps if timesteps is None else timesteps
+        self.n_steps = len(ts)
+        self.ts = torch.as_tensor(ts).to(dev, torch.float32)
+        self.coef = scheduler.coefficient_table(torch.as_tensor(ts).cpu()).to(dev)
+        self.step_idx = torch.zeros(1, device=dev, dtype=torch.int32)
+        pe = prompt_embeds.to(dev, torch.bfloat16).contiguous()
+        if pe.shape[0] != self.Bt:
+            raise ValueError(f"prompt_embeds batch {pe.shape[0]} != {self.Bt} (uncond first when CFG)")
+        self.L = pe.shape[1]
+        self.ehs_rows = pe.reshape(self.Bt * self.L, -1)
+        self.x_in = ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD)
+        self.kv_cache = {}
+        self.use_graph = use_graph
+        self.graph = None
+        self.graph_error = None
+
+    def step(self):
+        u = self.unet
+        te = ops.timestep_embed(self.ts, u.time_proj.num_channels, step_idx=self.step_idx, batch=self.Bt)
+        ctx = u.make_ctx(te, self.ehs_rows, self.Bt, self.F, self.L, kv_cache=self.kv_cache)
+        eps = u.forward_rows(self.x_in, self.H, self.W, ctx)
+        ops.ddim_cfg_step(eps, self.ncfg, self.g, self.lat, self.coef, step_idx=self.step_idx,
+                          next_in=self.x_in)
+        ops.step_advance(self.step_idx)
+
+    def reset(self, latents):
+        self.lat.copy_(latents)
+        self.step_idx.zero_()
+        ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD, out=self.x_in)
+
+    def prime(self):
+        """One eager step (loads kernels, fills the cross-attention K/V cache,
+        initialises communicators), then restore the state; capture the graph."""
+        saved = self.lat.clone()
+        self.step()
+        self.reset(saved)
+        torch.cuda.synchronize()
+        if self.use_graph and self.graph is None:
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self.step()
+                self.graph = g
+            except Exception as e:  # capture unsupported (e.g. a collective): run eagerly
+                self.graph_error = repr(e)
+                self.graph = None
+                torch.cuda.synchronize()
+                self.reset(saved)
+        return self
+
+    def run(self, n=None):
+        n = self.n_steps if n is None else n
+        for _ in range(n):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self.step()
+        return self.lat
+
+
+class AnimateDiffPipeline:
+    def __init__(self, unet: UNetMotionModel, scheduler=None, text_encoder=None, vae=None, dist=None):
+        self.unet = unet
+        self.scheduler = scheduler or DDIMScheduler()
+        self.text_encoder = text_encoder or SyntheticTextEncoder(unet.config["cross_attention_dim"])
+        self.vae = vae
+        self.dist = dist
+        self.unet.dist = dist
+
+    @classmethod
+    def from_config(cls, config="full", device="cuda", seed=0, scheduler=None, dist=None):
+        unet = UNetMotionModel(config)
+        init_synthetic_(unet, seed)
+        unet = unet.to(device=device, dtype=torch.bfloat16)
+        unet.prepare()
+        sched = scheduler or DDIMScheduler.from_config(None, beta_schedule="linear", steps_offset=1,
+                                                       clip_sample=False)
+        return cls(unet, sched, dist=dist)
+
+    @classmethod
+    def from_pretrained(cls, *args, **kwargs):
+        raise NotImplementedError("hub checkpoints are unreachable offline: build with from_config() "
+                                  "and vdiff.weights.load_diffusers_state_dict() for local safetensors")
+
+    def enable_vae_slicing(self):
+        pass
+
+    def enable_model_cpu_offload(self, *a, **k):
+        pass  # 288 GB HBM: the 12 GB-GPU workaround is unnecessary
+
+    def to(self, *a, **k):
+        return self
+
+    def encode_prompt(self, prompt, batch):
+        if isinstance(prompt, str):
+            prompt = [prompt] * batch
+        return torch.stack([self.text_encoder(p) for p in prompt])
+
+    @torch.no_grad()
+    def __call__(self, prompt=None, num_frames=16, height=None, width=None, num_inference_steps=50,
+                 guidance_scale=7.5, negative_prompt=None, num_videos_per_prompt=1, eta=0.0,
+                 generator=None, latents=None, prompt_embeds=None, negative_prompt_embeds=None,
+                 output_type="latent", return_dict=True, use_graph=True, **unused):
+        if eta != 0.0:
+            raise NotImplementedError("eta > 0")
+        if output_type != "latent":
+            raise NotImplementedError("VAE decode is out of scope for this build (SURVEY.md §8f): "
+                                      "use output_type='latent'")
+        dev = self.unet.device
+        sample = self.unet.config["sample_size"]
+        h = (height or sample * 8) // 8
+        w = (width or sample * 8) // 8
+        if prompt_embeds is None:
+            if prompt is None:
+                raise ValueError("prompt or prompt_embeds required")
+            n = 1 if isinstance(prompt, str) else len(prompt)
+            prompt_embeds = self.encode_prompt(prompt, n)
+        B = prompt_embeds.shape[0] * num_videos_per_prompt
+        prompt_embeds = prompt_embeds.repeat_interleave(num_videos_per_prompt, 0)
+        do_cfg = guidance_scale > 1
+        if do_cfg:
+            if negative_prompt_embeds is None:
+                negative_prompt_embeds = self.encode_prompt(negative_prompt or "", B)
+            ehs = torch.cat([negative_prompt_embeds.to(prompt_embeds), prompt_embeds])
+        else:
+            ehs = prompt_embeds
+        self.scheduler.set_timesteps(num_inference_steps)
+        if latents is None:
+            latents = torch.randn((B, self.unet.config["in_channels"], num_frames, h, w),
+                                  generator=generator, dtype=torch.float32)
+        latents = latents.to(dev, torch.float32) * self.scheduler.init_noise_sigma
+        local = latents
+        if self.dist is not None:
+            fl = self.dist.frames_local(num_frames)
+            local = latents[:, :, self.dist.rank * fl:(self.dist.rank + 1) * fl]
+        loop = DenoiseLoop(self.unet, self.scheduler, local, ehs, guidance_scale,
+                           use_graph=use_graph).prime()
+        out = loop.run()
+        if self.dist is not None:
+            out = self.dist.all_gather_frames(out)
+        return AnimateDiffPipelineOutput(frames=out) if return_dict else (out,)
