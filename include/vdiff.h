@@ -77,9 +77,19 @@ typedef struct vd_gemm_desc {
   const void* res; int64_t ld_res;
   int32_t act;
   void* out; int64_t ldc; int32_t out_f32;
+  /* split-K workspace (fp32 partial slabs); size from vd_gemm_ws_bytes(), may be
+   * NULL when that returns 0. */
+  void* ws; int64_t ws_bytes;
 } vd_gemm_desc;
 
 int vd_gemm(const vd_gemm_desc* d, vd_stream_t stream);
+/* Workspace bytes vd_gemm needs for this descriptor (0 = none): shapes with too
+ * few output tiles to fill 256 CUs are split along K into fp32 slabs that a
+ * second kernel reduces (deterministic, no atomics) while applying the epilogue. */
+int64_t vd_gemm_ws_bytes(const vd_gemm_desc* d);
+/* Test/benchmark hook: on != 0 forces the register-staged v1 GEMM path for every
+ * shape (default: the LDS-DMA v2 path wherever it applies). */
+int vd_gemm_force_v1(int32_t on);
 
 /* ---------------------------------------------------------------- GroupNorm
  * torch GroupNorm over NHWC rows, for ResnetBlock2D.norm1/2 (eps 1e-5, +SiLU),

@@ -16,7 +16,7 @@ HEADER = ROOT / "include" / "vdiff.h"
 
 def header_functions():
     txt = HEADER.read_text()
-    return set(re.findall(r"^\s*(?:const\s+char\s*\*|int)\s+(vd_\w+)\s*\(", txt, re.M))
+    return set(re.findall(r"^\s*(?:const\s+char\s*\*|int|int64_t)\s+(vd_\w+)\s*\(", txt, re.M))
 
 
 def test_header_declares_exactly_the_bound_symbols():
@@ -70,3 +70,12 @@ def test_ops_refuse_cpu_tensors():
 def test_error_path_raises_with_message():
     with pytest.raises(L.VdiffError, match="invalid argument"):
         L.check(1000, "probe")
+
+
+def test_gemm_workspace_policy():
+    """Split-K is requested only when the output tiles cannot fill the chip."""
+    big = L.GemmDesc(M=131072, N=320, K=2880, k0=2880, lda0=2880, ldw=2880, a_mode=0)
+    assert L.lib().vd_gemm_ws_bytes(ctypes.byref(big)) == 0
+    small = L.GemmDesc(M=2048, N=1280, K=11520, k0=11520, lda0=11520, ldw=11520, a_mode=0)
+    nbytes = L.lib().vd_gemm_ws_bytes(ctypes.byref(small))
+    assert nbytes > 0 and nbytes % (2048 * 1280 * 4) == 0

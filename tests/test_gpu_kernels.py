@@ -80,6 +80,99 @@ def test_gemm_geglu(cuda):
     close_bf16(got, h * F.gelu(g))
 
 
+# ---------------------------------------------------------------- v2 (LDS-DMA) paths
+@pytest.fixture(params=["v2", "v1"])
+def gemm_path(request, cuda):
+    from vdiff._lib import lib
+    lib().vd_gemm_force_v1(int(request.param == "v1"))
+    yield request.param
+    lib().vd_gemm_force_v1(0)
+
+
+def test_gemm_large_dense(gemm_path):
+    """Shapes large enough for the 256-row LDS-DMA kernel (v2) and the same on v1."""
+    M, N = 32768, 320
+    a, a1 = rnd(M, 256), rnd(M, 384)
+    w = rnd(N, 640, std=0.04)
+    b = torch.randn(N, device="cuda")
+    temb = torch.randn(4, N, device="cuda")
+    res = rnd(M, N)
+    got = ops.gemm(a, w, a1=a1, bias=b, rowbias=temb, rb_div=M // 4, res=res)
+    x = torch.cat([a, a1], 1).float()
+    want = x @ w.float().T + b + temb.repeat_interleave(M // 4, 0) + res.float()
+    close_bf16(got, want)
+    got = ops.gemm(a1, w[:, :384].contiguous(), bias=b, out_f32=True)
+    close_f32(got, a1.float() @ w[:, :384].float().T + b, rtol=1e-3, atol=1e-3)
+
+
+def test_gemm_large_geglu(gemm_path):
+    M, C = 32768, 64
+    n = rnd(M, 256)
+    w = rnd(8 * C, 256, std=0.06)
+    bb = torch.randn(8 * C, device="cuda") * 0.1
+    got = ops.gemm(n, pack_geglu(w), bias=pack_geglu(bb), act=ops.ACT_GEGLU)
+    hg = n.float() @ w.float().T + bb
+    h, g = hg.chunk(2, -1)
+    close_bf16(got, h * F.gelu(g))
+
+
+@pytest.mark.parametrize("case", ["s1", "s2", "up", "concat"])
+def test_conv3x3_large(gemm_path, case):
+    n, co = 8, 320
+    h = w = 128 if case == "s2" else (32 if case == "up" else 64)
+    c0, c1 = 64, (64 if case == "concat" else 0)
+    x0 = rnd(n * h * w, c0)
+    x1 = rnd(n * h * w, c1) if c1 else None
+    wt = bf(torch.randn(co, c0 + c1, 3, 3, device="cuda") * 0.04)
+    b = torch.randn(co, device="cuda")
+    stride = 2 if case == "s2" else 1
+    out, ho, wo = ops.conv3x3(x0, n, h, w, pack_conv3x3(wt), x1=x1, stride=stride, upsample=case == "up",
+                              bias=b)
+    assert ho * wo * n == 32768
+    xin = x0 if x1 is None else torch.cat([x0, x1], 1)
+    img = xin.float().reshape(n, h, w, -1).permute(0, 3, 1, 2)
+    if case == "up":
+        img = F.interpolate(img, scale_factor=2.0, mode="nearest")
+    want = F.conv2d(img, wt.float(), b, stride=stride, padding=1).permute(0, 2, 3, 1).reshape(-1, co)
+    close_bf16(out, want)
+
+
+def test_gemm_splitk_dense(cuda):
+    """Few output tiles + long K (the 8x8 level): split-K slabs + reduce epilogue."""
+    M, N, K = 2048, 1280, 2560
+    a, w = rnd(M, K), rnd(N, K, std=K ** -0.5)
+    b = torch.randn(N, device=cuda)
+    temb = torch.randn(2, N, device=cuda)
+    res = rnd(M, N)
+    got = ops.gemm(a, w, bias=b, rowbias=temb, rb_div=M // 2, res=res)
+    want = a.float() @ w.float().T + b + temb.repeat_interleave(M // 2, 0) + res.float()
+    close_bf16(got, want)
+    got = ops.gemm(a, w, bias=b, act=ops.ACT_SILU, out_f32=True)
+    close_f32(got, F.silu(a.double() @ w.double().T + b.double()), rtol=1e-3, atol=1e-3)
+
+
+def test_gemm_splitk_geglu(cuda):
+    M, C, K = 1024, 128, 1280
+    n = rnd(M, K)
+    w = rnd(8 * C, K, std=K ** -0.5)
+    bb = torch.randn(8 * C, device=cuda) * 0.1
+    got = ops.gemm(n, pack_geglu(w), bias=pack_geglu(bb), act=ops.ACT_GEGLU)
+    h, g = (n.float() @ w.float().T + bb).chunk(2, -1)
+    close_bf16(got, h * F.gelu(g))
+
+
+def test_conv3x3_splitk(cuda):
+    n, h, w, ci, co = 32, 8, 8, 256, 1280
+    x = rnd(n * h * w, ci)
+    wt = bf(torch.randn(co, ci, 3, 3, device=cuda) * 0.02)
+    b = torch.randn(co, device=cuda)
+    res = rnd(n * h * w, co)
+    out, _, _ = ops.conv3x3(x, n, h, w, pack_conv3x3(wt), bias=b, res=res)
+    img = x.float().reshape(n, h, w, ci).permute(0, 3, 1, 2)
+    want = F.conv2d(img, wt.float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, co) + res.float()
+    close_bf16(out, want)
+
+
 # ---------------------------------------------------------------- conv
 @pytest.mark.parametrize("case", ["s1", "s2", "up", "concat", "cin8", "cout4"])
 def test_conv3x3(cuda, case):

@@ -22,7 +22,7 @@ from oracle import ddim_ref, unet_ref
 from vdiff import DDIMScheduler, DenoiseLoop, UNetMotionModel, init_synthetic_, ops
 from vdiff.config import TINY
 from vdiff.models.blocks import AnimateDiffTransformer3D, Ctx, ResnetBlock2D, Transformer2DModel
-from vdiff.models.layers import Act
+from vdiff.models.layers import Act, prepare_tree
 
 pytestmark = pytest.mark.gpu
 GOLD = Path(__file__).resolve().parent / "golden"
@@ -64,7 +64,7 @@ def test_resnet_block_concat_shortcut(cuda):
     r = randomize_(ResnetBlock2D(cin_x + cin_s, cout, tdim), 0)
     sd = sd_of(r, "r")
     r = r.to("cuda", torch.bfloat16)
-    r.prepare()
+    prepare_tree(r)
     x = torch.randn(B * Fr, cin_x, H, W).to(torch.bfloat16).float()
     s = torch.randn(B * Fr, cin_s, H, W).to(torch.bfloat16).float()
     temb = torch.randn(B, tdim).to(torch.bfloat16).float()
@@ -83,7 +83,7 @@ def test_transformer2d_with_cross_attention(cuda):
     t = randomize_(Transformer2DModel(heads, C // heads, C, D), 1)
     sd = sd_of(t, "t")
     t = t.to("cuda", torch.bfloat16)
-    t.prepare()
+    prepare_tree(t)
     x = torch.randn(B * Fr, C, H, W).to(torch.bfloat16).float()
     ehs = torch.randn(B, L, D).to(torch.bfloat16).float()
     ctx = Ctx(B, Fr, None, ehs.reshape(B * L, D).to("cuda", torch.bfloat16), L)
@@ -103,7 +103,7 @@ def test_motion_module(cuda):
     m = randomize_(AnimateDiffTransformer3D(heads, C // heads, C), 2)
     sd = sd_of(m, "m")
     m = m.to("cuda", torch.bfloat16)
-    m.prepare()
+    prepare_tree(m)
     x = (torch.randn(B * Fr, C, H, W) + 0.5).to(torch.bfloat16).float()
     ctx = Ctx(B, Fr, None, None, 77)
     out = m(Act(to_rows(x), B * Fr, H, W), ctx)

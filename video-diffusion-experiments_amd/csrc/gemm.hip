@@ -30,6 +30,80 @@ __device__ __forceinline__ int lds_off(int row, int chunk) {
   return row * BK + ((chunk ^ (row & 7)) << 3);
 }
 
+template <int BM, int BN, int MB, int NB>
+__device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], int64_t m0,
+                                              int64_t n0, int wm, int wn, int lane) {
+  const int64_t M = d.M, N = d.N;
+  const int fr = lane & 15, fq = lane >> 4;
+  // acc[a][b][j] = C[m = m0 + wm*BM/WM + b*16 + fr][n = n0 + wn*BN/2 + a*16 + 4*fq + j]
+  constexpr int WROWS = MB * 16;
+  const int64_t nw = n0 + wn * (BN / 2);
+  if (d.act == VD_ACT_GEGLU) {
+    if constexpr (NB % 2 == 0) {
+#pragma unroll
+      for (int a = 0; a < NB; a += 2) {
+        const int64_t nh = nw + a * 16 + 4 * fq;        // packed hidden column
+        const int64_t ng = nh + 16;                      // packed gate column
+        if (ng >= N) continue;
+        const int64_t nout = nw / 2 + (a / 2) * 16 + 4 * fq;
+        float bh[4] = {0, 0, 0, 0}, bg[4] = {0, 0, 0, 0};
+        if (d.bias) {
+          const float4 t0 = *(const float4*)(d.bias + nh);
+          const float4 t1 = *(const float4*)(d.bias + ng);
+          bh[0] = t0.x; bh[1] = t0.y; bh[2] = t0.z; bh[3] = t0.w;
+          bg[0] = t1.x; bg[1] = t1.y; bg[2] = t1.z; bg[3] = t1.w;
+        }
+#pragma unroll
+        for (int b = 0; b < MB; ++b) {
+          const int64_t m = m0 + wm * WROWS + b * 16 + fr;
+          if (m >= M) continue;
+          float o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = (acc[a][b][j] + bh[j]) * gelu_erf(acc[a + 1][b][j] + bg[j]);
+          bf16_t* op = (bf16_t*)d.out + m * d.ldc + nout;
+          *(uint2*)op = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int a = 0; a < NB; ++a) {
+    const int64_t n = nw + a * 16 + 4 * fq;
+    if (n >= N) continue;
+    float bv[4] = {0, 0, 0, 0};
+    if (d.bias) {
+      const float4 t = *(const float4*)(d.bias + n);
+      bv[0] = t.x; bv[1] = t.y; bv[2] = t.z; bv[3] = t.w;
+    }
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      const int64_t m = m0 + wm * WROWS + b * 16 + fr;
+      if (m >= M) continue;
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = acc[a][b][j] + bv[j];
+      if (d.rowbias) {
+        const float4 t = *(const float4*)(d.rowbias + (m / d.rb_div) * d.ld_rb + n);
+        o[0] += t.x; o[1] += t.y; o[2] += t.z; o[3] += t.w;
+      }
+      if (d.act == VD_ACT_SILU) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = silu_f(o[j]);
+      }
+      if (d.res) {
+        const uint2 r = *(const uint2*)((const bf16_t*)d.res + m * d.ld_res + n);
+        o[0] += bf_lo(r.x); o[1] += bf_hi(r.x); o[2] += bf_lo(r.y); o[3] += bf_hi(r.y);
+      }
+      if (d.out_f32) {
+        *(float4*)((float*)d.out + m * d.ldc + n) = make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+        *(uint2*)((bf16_t*)d.out + m * d.ldc + n) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int MODE>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
   constexpr int RA = BM / 32;        // A chunks staged per thread
@@ -172,73 +246,288 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
     __syncthreads();
   }
 
-  // ---------------------------------------------------------------- epilogue
-  // acc[a][b][j] = C[m = m0 + wm*BM/2 + b*16 + fr][n = n0 + wn*BN/2 + a*16 + 4*fq + j]
-  const int64_t nw = n0 + wn * (BN / 2);
-  if (d.act == VD_ACT_GEGLU) {
-    if constexpr (NB % 2 == 0) {
+  gemm_epilogue<BM, BN, MB, NB>(d, acc, m0, n0, wm, wn, lane);
+}
+
+// ============================================================================ v2
+// LDS-DMA GEMM: BM = 256, BN in {128, 160}, BK = 64, 512 threads = 8 waves as
+// 4(M) x 2(N), each wave 64 x BN/2.  Operands reach LDS by `buffer_load_dwordx4
+// ... lds` (no VGPR staging, no ds_write pass) into a 3-stage ring, two tiles in
+// flight, ONE raw s_barrier per K-tile behind a counted vmcnt (guide §5
+// "Pipelining across barriers").  The LDS image is lane-linear; the (row & 7)
+// XOR swizzle is applied on the per-lane SOURCE address (rule 21).  Conv taps
+// outside the image are zero-filled by the buffer range check (voffset beyond
+// num_records returns 0).  Per-tile address work: one integer add per load.
+constexpr int G2_BM = 256, G2_NT = 512, G2_STAGES = 3;
+constexpr uint32_t G2_OOB = 0x80000000u;
+
+template <int BN>
+struct G2 {
+  static constexpr int A_BYTES = G2_BM * BK * 2;   // 32 KiB
+  static constexpr int B_BYTES = BN * BK * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int NA = 4;                     // A DMA instructions per wave per tile
+  static constexpr int NBI = BN / 8;               // B DMA instructions per tile (whole block)
+  static constexpr int NBMAX = (NBI + 7) / 8;      // per wave, upper bound
+  static constexpr int MB = 4, NB = BN / 32;
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
+}
+
+template <int BN, int MODE>
+__global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
+                                                         uint32_t a1_bytes, uint32_t w_bytes,
+                                                         int split) {
+  using C = G2<BN>;
+  __shared__ __attribute__((aligned(1024))) char smem[G2_STAGES * C::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int64_t M = d.M, N = d.N, K = d.K;
+  const int tiles_n = (int)((N + BN - 1) / BN);
+  const int tiles_m = (int)((M + G2_BM - 1) / G2_BM);
+  const int gid = xcd_remap(blockIdx.x, tiles_n * tiles_m * split);
+  const int sp = gid % split;          // split-K slice (adjacent ids share the output tile)
+  const int id = gid / split;
+  const int64_t m0 = (int64_t)(id / tiles_n) * G2_BM;
+  const int64_t n0 = (int64_t)(id % tiles_n) * BN;
+  const int nk_all = (int)(K / BK);
+  const int kt0 = (int)((int64_t)nk_all * sp / split), kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
+
+  const int rb = lane >> 3;                    // row within the 8-row DMA block
+  const uint32_t lc16 = (uint32_t)(((lane & 7) ^ rb) * 16);   // swizzled source chunk (bytes)
+
+  const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)d.a0, 0, a0_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ra1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(d.a1 ? d.a1 : d.a0), 0, d.a1 ? a1_bytes : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, w_bytes, 0x00020000);
+
+  // B (weights): this wave issues instructions bi = j*8 + wid, rows bi*8 + rb.
+  const int nbw = (C::NBI - wid + 7) / 8;
+  uint32_t boff[C::NBMAX];
 #pragma unroll
-      for (int a = 0; a < NB; a += 2) {
-        const int64_t nh = nw + a * 16 + 4 * fq;        // packed hidden column
-        const int64_t ng = nh + 16;                      // packed gate column
-        if (ng >= N) continue;
-        const int64_t nout = nw / 2 + (a / 2) * 16 + 4 * fq;
-        float bh[4] = {0, 0, 0, 0}, bg[4] = {0, 0, 0, 0};
-        if (d.bias) {
-          const float4 t0 = *(const float4*)(d.bias + nh);
-          const float4 t1 = *(const float4*)(d.bias + ng);
-          bh[0] = t0.x; bh[1] = t0.y; bh[2] = t0.z; bh[3] = t0.w;
-          bg[0] = t1.x; bg[1] = t1.y; bg[2] = t1.z; bg[3] = t1.w;
-        }
+  for (int j = 0; j < C::NBMAX; ++j) {
+    int64_t n = n0 + (j * 8 + wid) * 8 + rb;
+    n = n < N ? n : N - 1;
+    boff[j] = (uint32_t)(n * d.ldw * 2) + lc16;
+  }
+  // A: this wave issues rows (wid*4 + j)*8 + rb, j < 4.
+  uint32_t aoff0[C::NA], aoff1[C::NA];
+  int poh[C::NA], pow_[C::NA], pimg[C::NA];
+  if constexpr (MODE == VD_A_DENSE) {
 #pragma unroll
-        for (int b = 0; b < MB; ++b) {
-          const int64_t m = m0 + wm * (BM / 2) + b * 16 + fr;
-          if (m >= M) continue;
-          float o[4];
+    for (int j = 0; j < C::NA; ++j) {
+      int64_t m = m0 + (wid * 4 + j) * 8 + rb;
+      m = m < M ? m : M - 1;
+      aoff0[j] = (uint32_t)(m * d.lda0 * 2) + lc16;
+      aoff1[j] = (uint32_t)(m * d.lda1 * 2) + lc16;
+    }
+  } else {
+    const int hw = d.h_out * d.w_out;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = (acc[a][b][j] + bh[j]) * gelu_erf(acc[a + 1][b][j] + bg[j]);
-          bf16_t* op = (bf16_t*)d.out + m * d.ldc + nout;
-          *(uint2*)op = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+    for (int j = 0; j < C::NA; ++j) {
+      int64_t m = m0 + (wid * 4 + j) * 8 + rb;
+      m = m < M ? m : M - 1;
+      pimg[j] = (int)(m / hw);
+      const int p = (int)(m - (int64_t)pimg[j] * hw);
+      poh[j] = p / d.w_out;
+      pow_[j] = p - poh[j] * d.w_out;
+      aoff0[j] = aoff1[j] = G2_OOB;
+    }
+  }
+  const int cin = MODE == VD_A_CONV3X3 ? (int)(K / 9) : 0;
+  const int hgrid = d.upsample ? 2 * d.h_in : d.h_in;
+  const int wgrid = d.upsample ? 2 * d.w_in : d.w_in;
+  // conv: (tap, channel) of the next tile to issue; offsets recomputed on a tap change
+  int c_tap = 0, c_ci = 0;
+  bool c_new = true;
+  if constexpr (MODE == VD_A_CONV3X3) {
+    c_tap = kt0 * BK / cin;
+    c_ci = kt0 * BK - c_tap * cin;
+  }
+
+  auto issue = [&](int kt, int stage) {
+    char* la = smem + stage * C::STAGE;
+    char* lb = la + C::A_BYTES;
+    const int kb = kt * BK;
+    if constexpr (MODE == VD_A_DENSE) {
+      const bool s0 = kb < d.k0;
+      const uint32_t koff = (uint32_t)(s0 ? kb : kb - (int)d.k0) * 2;
+#pragma unroll
+      for (int j = 0; j < C::NA; ++j)
+        dma16(s0 ? ra0 : ra1, la + (wid * 4 + j) * 1024, (s0 ? aoff0[j] : aoff1[j]) + koff);
+    } else {
+      if (c_new) {  // new tap: recompute the rows' pixel offsets
+        c_new = false;
+        const int dy = c_tap / 3, dx = c_tap - 3 * dy;
+#pragma unroll
+        for (int j = 0; j < C::NA; ++j) {
+          int ih = poh[j] * d.stride + dy - 1, iw = pow_[j] * d.stride + dx - 1;
+          const bool ok = ih >= 0 && ih < hgrid && iw >= 0 && iw < wgrid;
+          ih >>= d.upsample;
+          iw >>= d.upsample;
+          const uint32_t pix = (uint32_t)((pimg[j] * d.h_in + ih) * d.w_in + iw);
+          aoff0[j] = ok ? pix * (uint32_t)(d.lda0 * 2) + lc16 : G2_OOB;
+          aoff1[j] = ok ? pix * (uint32_t)(d.lda1 * 2) + lc16 : G2_OOB;
         }
       }
+      const bool s0 = c_ci < d.k0;
+      const uint32_t coff = (uint32_t)(s0 ? c_ci : c_ci - (int)d.k0) * 2;
+#pragma unroll
+      for (int j = 0; j < C::NA; ++j) {
+        const uint32_t o = s0 ? aoff0[j] : aoff1[j];
+        dma16(s0 ? ra0 : ra1, la + (wid * 4 + j) * 1024, o == G2_OOB ? G2_OOB : o + coff);
+      }
+      c_ci += BK;
+      if (c_ci == cin) { c_ci = 0; ++c_tap; c_new = true; }
     }
+#pragma unroll
+    for (int j = 0; j < C::NBMAX; ++j)
+      if (j < nbw) dma16(rw, lb + (j * 8 + wid) * 1024, boff[j] + (uint32_t)kb * 2);
+  };
+
+  f32x4 acc[C::NB][C::MB];
+#pragma unroll
+  for (int a = 0; a < C::NB; ++a)
+#pragma unroll
+    for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kt1 - kt0;  // tiles of this split; issue() takes absolute tile indices
+  issue(kt0, 0);
+  if (nk > 1) issue(kt0 + 1, 1);
+  const int fr = lane & 15, fq = lane >> 4;
+  int stage = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's DMA for tile kt has landed once at most tile kt+1's remain outstanding
+    if (kt + 1 < nk) {
+      if (nbw == C::NBMAX) wait_vm<C::NA + C::NBMAX>();
+      else wait_vm<C::NA + C::NBMAX - 1>();
+    } else {
+      wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for kt landed; stage (kt-1)%3 fully read
+    if (kt + 2 < nk) issue(kt0 + kt + 2, stage == 0 ? 2 : stage - 1);
+    const bf16_t* as = (const bf16_t*)(smem + stage * C::STAGE);
+    const bf16_t* ws = (const bf16_t*)(smem + stage * C::STAGE + C::A_BYTES);
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 wf[C::NB], xf[C::MB];
+#pragma unroll
+      for (int a = 0; a < C::NB; ++a)
+        wf[a] = *(const bf16x8*)(ws + lds_off(wn * (BN / 2) + a * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int b = 0; b < C::MB; ++b)
+        xf[b] = *(const bf16x8*)(as + lds_off(wm * 64 + b * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int a = 0; a < C::NB; ++a)
+#pragma unroll
+        for (int b = 0; b < C::MB; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][b], 0, 0, 0);
+    }
+    stage = stage == 2 ? 0 : stage + 1;
+  }
+  if (split == 1) {
+    gemm_epilogue<G2_BM, BN, C::MB, C::NB>(d, acc, m0, n0, wm, wn, lane);
     return;
   }
+  // split-K: raw fp32 partial slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
+  float* slab = (float*)d.ws + (int64_t)sp * M * N;
 #pragma unroll
-  for (int a = 0; a < NB; ++a) {
-    const int64_t n = nw + a * 16 + 4 * fq;
+  for (int a = 0; a < C::NB; ++a) {
+    const int64_t n = n0 + wn * (BN / 2) + a * 16 + 4 * fq;
     if (n >= N) continue;
-    float bv[4] = {0, 0, 0, 0};
-    if (d.bias) {
-      const float4 t = *(const float4*)(d.bias + n);
-      bv[0] = t.x; bv[1] = t.y; bv[2] = t.z; bv[3] = t.w;
-    }
 #pragma unroll
-    for (int b = 0; b < MB; ++b) {
-      const int64_t m = m0 + wm * (BM / 2) + b * 16 + fr;
-      if (m >= M) continue;
-      float o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = acc[a][b][j] + bv[j];
-      if (d.rowbias) {
-        const float4 t = *(const float4*)(d.rowbias + (m / d.rb_div) * d.ld_rb + n);
-        o[0] += t.x; o[1] += t.y; o[2] += t.z; o[3] += t.w;
-      }
-      if (d.act == VD_ACT_SILU) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = silu_f(o[j]);
-      }
-      if (d.res) {
-        const uint2 r = *(const uint2*)((const bf16_t*)d.res + m * d.ld_res + n);
-        o[0] += bf_lo(r.x); o[1] += bf_hi(r.x); o[2] += bf_lo(r.y); o[3] += bf_hi(r.y);
-      }
-      if (d.out_f32) {
-        *(float4*)((float*)d.out + m * d.ldc + n) = make_float4(o[0], o[1], o[2], o[3]);
-      } else {
-        *(uint2*)((bf16_t*)d.out + m * d.ldc + n) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
-      }
+    for (int b = 0; b < C::MB; ++b) {
+      const int64_t m = m0 + wm * 64 + b * 16 + fr;
+      if (m < M) *(float4*)(slab + m * N + n) = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
     }
   }
+}
+
+// Sum the split-K slabs and apply the GEMM epilogue (4 output columns per thread).
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, int split) {
+  const int64_t M = d.M, N = d.N;
+  const bool geglu = d.act == VD_ACT_GEGLU;
+  const int64_t nout = geglu ? N / 2 : N;
+  const int64_t total = M * (nout / 4);
+  const float* ws = (const float*)d.ws;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / (nout / 4);
+    const int64_t o = (i - m * (nout / 4)) * 4;
+    float o4[4];
+    if (geglu) {
+      const int64_t nh = (o / 16) * 32 + (o % 16), ng = nh + 16;
+      float h[4] = {0, 0, 0, 0}, g[4] = {0, 0, 0, 0};
+      for (int sp = 0; sp < split; ++sp) {
+        const float4 a = *(const float4*)(ws + (sp * M + m) * N + nh);
+        const float4 b = *(const float4*)(ws + (sp * M + m) * N + ng);
+        h[0] += a.x; h[1] += a.y; h[2] += a.z; h[3] += a.w;
+        g[0] += b.x; g[1] += b.y; g[2] += b.z; g[3] += b.w;
+      }
+      if (d.bias) {
+        const float4 a = *(const float4*)(d.bias + nh);
+        const float4 b = *(const float4*)(d.bias + ng);
+        h[0] += a.x; h[1] += a.y; h[2] += a.z; h[3] += a.w;
+        g[0] += b.x; g[1] += b.y; g[2] += b.z; g[3] += b.w;
+      }
+      for (int j = 0; j < 4; ++j) o4[j] = h[j] * gelu_erf(g[j]);
+    } else {
+      float v[4] = {0, 0, 0, 0};
+      for (int sp = 0; sp < split; ++sp) {
+        const float4 a = *(const float4*)(ws + (sp * M + m) * N + o);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      }
+      if (d.bias) {
+        const float4 a = *(const float4*)(d.bias + o);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      }
+      if (d.rowbias) {
+        const float4 a = *(const float4*)(d.rowbias + (m / d.rb_div) * d.ld_rb + o);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      }
+      if (d.act == VD_ACT_SILU)
+        for (int j = 0; j < 4; ++j) v[j] = silu_f(v[j]);
+      if (d.res) {
+        const uint2 r = *(const uint2*)((const bf16_t*)d.res + m * d.ld_res + o);
+        v[0] += bf_lo(r.x); v[1] += bf_hi(r.x); v[2] += bf_lo(r.y); v[3] += bf_hi(r.y);
+      }
+      for (int j = 0; j < 4; ++j) o4[j] = v[j];
+    }
+    if (d.out_f32)
+      *(float4*)((float*)d.out + m * d.ldc + o) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+    else
+      *(uint2*)((bf16_t*)d.out + m * d.ldc + o) = make_uint2(pack2(o4[0], o4[1]), pack2(o4[2], o4[3]));
+  }
+}
+
+template <int BN>
+int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
+  const int64_t tiles = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + BN - 1) / BN) * split;
+  if (d.a_mode == VD_A_CONV3X3)
+    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3>), dim3((unsigned)tiles), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
+  else
+    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)tiles), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
+  int rc = vd_launch_status();
+  if (rc != VD_OK || split == 1) return rc;
+  const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
+  const int64_t blocks = (work + 255) / 256;
+  hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, d, split);
+  return vd_launch_status();
 }
 
 template <int BM, int BN>
@@ -254,8 +543,47 @@ int launch(const vd_gemm_desc& d, hipStream_t s) {
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
+int g_force_v1 = 0;
+
+struct Plan {
+  bool v2 = false;
+  int bn = 128, split = 1;
+  uint32_t a0b = 0, a1b = 0, wb = 0;
+  int64_t ws_bytes = 0;
+};
+
+// v2 (LDS-DMA, 256-row tiles) wherever the operands fit 32-bit buffer offsets;
+// split K when the output tiles cannot fill the 256 CUs.
+Plan plan(const vd_gemm_desc& d) {
+  Plan p;
+  if (g_force_v1 || d.K % BK || d.k0 % BK || d.M < G2_BM || d.N < 64) return p;
+  const int64_t a_rows = d.a_mode == VD_A_CONV3X3 ? (int64_t)d.n_img * d.h_in * d.w_in : d.M;
+  const int64_t a0b = a_rows * d.lda0 * 2, a1b = d.a1 ? a_rows * d.lda1 * 2 : 0, wb = d.N * d.ldw * 2;
+  if (a0b >= (int64_t)G2_OOB || a1b >= (int64_t)G2_OOB || wb >= (int64_t)G2_OOB) return p;
+  const int64_t p128 = (d.N + 127) / 128 * 128, p160 = (d.N + 159) / 160 * 160;
+  p.bn = d.act != VD_ACT_GEGLU && (p160 < p128 || (p160 == p128 && d.N % 160 == 0)) ? 160 : 128;
+  const int64_t tiles = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + p.bn - 1) / p.bn);
+  const int64_t nk = d.K / BK;
+  if (tiles < 192 && nk >= 16) {
+    int64_t sp = (256 + tiles - 1) / tiles;
+    sp = sp < nk / 8 ? sp : nk / 8;
+    p.split = (int)(sp < 8 ? sp : 8);
+  }
+  p.v2 = true;
+  p.a0b = (uint32_t)a0b; p.a1b = (uint32_t)a1b; p.wb = (uint32_t)wb;
+  p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 : 0;
+  return p;
+}
 
 }  // namespace
+
+extern "C" int64_t vd_gemm_ws_bytes(const vd_gemm_desc* d) { return d ? plan(*d).ws_bytes : 0; }
+
+// Test/benchmark hook: force the v1 (register-staged) GEMM path.
+extern "C" int vd_gemm_force_v1(int32_t on) {
+  g_force_v1 = on;
+  return VD_OK;
+}
 
 extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   if (!dp) return VD_EINVAL;
@@ -289,10 +617,14 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
     VD_CHECK_ARG(d.a_mode == VD_A_DENSE);
     if (d.k0 < d.K) VD_CHECK_ARG(d.a1 != nullptr);
   }
-  if (d.act == VD_ACT_GEGLU) {
-    VD_CHECK_ARG(d.N % 32 == 0 && !d.res && !d.rowbias && !d.out_f32);
-    return launch<128, 128>(d, s);
+  if (d.act == VD_ACT_GEGLU) VD_CHECK_ARG(d.N % 32 == 0 && !d.res && !d.rowbias && !d.out_f32);
+  const Plan p = plan(d);
+  if (p.v2) {
+    if (p.split > 1) VD_CHECK_ARG(d.ws && al16(d.ws) && d.ws_bytes >= p.ws_bytes);
+    return p.bn == 160 ? launch2<160>(d, s, p.a0b, p.a1b, p.wb, p.split)
+                       : launch2<128>(d, s, p.a0b, p.a1b, p.wb, p.split);
   }
+  if (d.act == VD_ACT_GEGLU) return launch<128, 128>(d, s);
   // N tile: least padding, then fewer tiles.
   if (d.N <= 64) return launch<128, 64>(d, s);
   const int64_t p128 = (d.N + 127) / 128 * 128, p160 = (d.N + 159) / 160 * 160;

@@ -102,47 +102,51 @@ __global__ __launch_bounds__(NT) void gn_partial_kernel(const bf16_t* x0, int64_
   }
 }
 
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float n2, float mean2,
+                                           float m22) {
+  if (n2 == 0.f) return;
+  const float nn = n + n2;
+  const float delta = mean2 - mean;
+  mean += delta * (n2 / nn);
+  m2 += m22 + delta * delta * (n * n2 / nn);
+  n = nn;
+}
+
+// One block per (instance, group): Chan-combine the n_split x (C/groups) records
+// of the group in parallel (per-thread, then an LDS tree), then write {a, b}.
 __global__ __launch_bounds__(NT) void gn_finalize_kernel(const float4* ws, int n_split, int64_t C,
                                                          int groups, float eps, const float* gamma,
                                                          const float* beta, float2* ss) {
-  extern __shared__ float4 chs[];  // [C] {n, mean, M2}; then [groups] {mean, rstd}
-  const int inst = blockIdx.x;
-  const float4* src = ws + (int64_t)inst * n_split * C;
-  for (int64_t c = threadIdx.x; c < C; c += NT) {
-    float n = 0.f, mean = 0.f, m2 = 0.f;
-    for (int s = 0; s < n_split; ++s) {
-      const float4 r = src[(int64_t)s * C + c];
-      if (r.x == 0.f) continue;
-      const float nn = n + r.x;
-      const float delta = r.y - mean;
-      mean += delta * (r.x / nn);
-      m2 += r.z + delta * delta * (n * r.x / nn);
-      n = nn;
-    }
-    chs[c] = make_float4(n, mean, m2, 0.f);
-  }
-  __syncthreads();
+  __shared__ float3 red[NT];
+  const int inst = blockIdx.x / groups;
+  const int g = blockIdx.x % groups;
   const int cpg = (int)(C / groups);
-  float4* gst = chs + C;
-  for (int g = threadIdx.x; g < groups; g += NT) {
-    float n = 0.f, mean = 0.f, m2 = 0.f;
-    for (int q = 0; q < cpg; ++q) {
-      const float4 r = chs[g * cpg + q];
-      if (r.x == 0.f) continue;
-      const float nn = n + r.x;
-      const float delta = r.y - mean;
-      mean += delta * (r.x / nn);
-      m2 += r.z + delta * delta * (n * r.x / nn);
-      n = nn;
-    }
-    const float var = n > 0.f ? m2 / n : 0.f;
-    gst[g] = make_float4(mean, rsqrtf(var + eps), 0.f, 0.f);
+  const int nrec = n_split * cpg;
+  const float4* src = ws + (int64_t)inst * n_split * C + (int64_t)g * cpg;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int r = threadIdx.x; r < nrec; r += NT) {
+    const int s = r / cpg, q = r - s * cpg;
+    const float4 v = src[(int64_t)s * C + q];
+    chan_merge(n, mean, m2, v.x, v.y, v.z);
   }
+  red[threadIdx.x] = make_float3(n, mean, m2);
   __syncthreads();
-  for (int64_t c = threadIdx.x; c < C; c += NT) {
-    const float4 st = gst[c / cpg];
-    const float a = st.y * gamma[c];
-    ss[(int64_t)inst * C + c] = make_float2(a, beta[c] - st.x * a);
+  for (int off = NT / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      float3 a = red[threadIdx.x];
+      const float3 b = red[threadIdx.x + off];
+      chan_merge(a.x, a.y, a.z, b.x, b.y, b.z);
+      red[threadIdx.x] = a;
+    }
+    __syncthreads();
+  }
+  const float3 t = red[0];
+  const float var = t.x > 0.f ? t.z / t.x : 0.f;
+  const float rstd = rsqrtf(var + eps);
+  for (int q = threadIdx.x; q < cpg; q += NT) {
+    const int64_t c = (int64_t)g * cpg + q;
+    const float a = rstd * gamma[c];
+    ss[(int64_t)inst * C + c] = make_float2(a, beta[c] - t.y * a);
   }
 }
 
@@ -253,9 +257,8 @@ extern "C" int vd_gn_finalize(const float* ws, int64_t n_inst, int32_t n_split_t
                               int32_t groups, float eps, const float* gamma, const float* beta,
                               float* scale_shift, vd_stream_t stream) {
   VD_CHECK_ARG(ws && gamma && beta && scale_shift && n_inst > 0 && n_split_total > 0);
-  VD_CHECK_ARG(groups > 0 && C % groups == 0 && C <= 8192);
-  const size_t lds = (size_t)(C + groups) * sizeof(float4);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)n_inst), dim3(NT), lds,
+  VD_CHECK_ARG(groups > 0 && C % groups == 0 && n_inst * groups < 0x7fffffff);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)(n_inst * groups)), dim3(NT), 0,
                      (hipStream_t)stream, (const float4*)ws, n_split_total, C, groups, eps, gamma,
                      beta, (float2*)scale_shift);
   return vd_launch_status();

@@ -23,6 +23,8 @@ SIGNATURES = {
     "vd_strerror": ([c_i32], C.c_char_p),
     "vd_version": ([], c_i32),
     "vd_gemm": ([c_vp, c_vp], c_i32),
+    "vd_gemm_force_v1": ([c_i32], c_i32),
+    "vd_gemm_ws_bytes": ([c_vp], c_i64),
     "vd_gn_partial": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp], c_i32),
     "vd_gn_finalize": ([c_vp, c_i64, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp], c_i32),
     "vd_gn_apply": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_i64, c_vp], c_i32),
@@ -54,6 +56,7 @@ class GemmDesc(C.Structure):
         ("res", c_vp), ("ld_res", c_i64),
         ("act", c_i32),
         ("out", c_vp), ("ldc", c_i64), ("out_f32", c_i32),
+        ("ws", c_vp), ("ws_bytes", c_i64),
     ]
 
 

@@ -43,6 +43,16 @@ def bf(p):
     return p.detach().to(torch.bfloat16).contiguous()
 
 
+def prepare_tree(module: nn.Module) -> nn.Module:
+    """Run prepare() on every submodule that defines one (children first)."""
+    for m in reversed(list(module.modules())):
+        if m is not module and hasattr(m, "prepare") and not hasattr(m, "_prepared"):
+            m.prepare()
+    if hasattr(module, "prepare"):
+        module.prepare()
+    return module
+
+
 def pack_conv3x3(wt: torch.Tensor, cin_pad: Optional[int] = None) -> torch.Tensor:
     """[Cout, Cin, 3, 3] -> [Cout, 9*Cin'] with K = tap*Cin' + ci (tap = 3*dy + dx)."""
     co, ci = wt.shape[:2]

@@ -96,7 +96,7 @@ class UNetMotionModel(nn.Module):
             raise RuntimeError("UNetMotionModel.prepare(): move the model to the GPU first (no CPU path)")
         for m in self.modules():
             if m is not self and hasattr(m, "prepare"):
-                m.prepare()
+                m.prepare()  # every block packs only its own operands
         self._w_in = pack_conv3x3(self.conv_in.weight, cin_pad=CIN_PAD)
         self._b_in = f32(self.conv_in.bias)
         self._w_out, self._b_out = pack_conv3x3(self.conv_out.weight), f32(self.conv_out.bias)

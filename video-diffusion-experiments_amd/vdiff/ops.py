@@ -42,6 +42,17 @@ def _rows(t, dtype=BF16):
 
 
 # ---------------------------------------------------------------- GEMM / conv
+def _run_gemm(d, device, what):
+    """Attach the split-K workspace the C side asks for (if any), then launch."""
+    nbytes = lib().vd_gemm_ws_bytes(C.byref(d))
+    ws = None
+    if nbytes > 0:
+        ws = torch.empty(nbytes // 4, device=device, dtype=torch.float32)
+        d.ws, d.ws_bytes = ws.data_ptr(), nbytes
+    check(lib().vd_gemm(C.byref(d), _stream()), what)
+    return ws  # keep alive until the launch is enqueued (stream-ordered reuse is safe)
+
+
 def gemm(a, w, *, a1=None, bias=None, rowbias=None, rb_div=1, res=None, act=ACT_NONE,
          out=None, out_f32=False):
     """out[m, n] = epi(sum_k cat(a, a1)[m, k] * w[n, k]); a/a1/w bf16, bias/rowbias fp32."""
@@ -65,7 +76,7 @@ def gemm(a, w, *, a1=None, bias=None, rowbias=None, rb_div=1, res=None, act=ACT_
                  res=_p(res), ld_res=_rows(res) if res is not None else 0, act=act,
                  out=_p(out), ldc=_rows(out, torch.float32 if out_f32 else BF16),
                  out_f32=int(out_f32))
-    check(lib().vd_gemm(C.byref(d), _stream()), "vd_gemm")
+    _run_gemm(d, a.device, "vd_gemm")
     return out
 
 
@@ -96,7 +107,7 @@ def conv3x3(x, n_img, h_in, w_in, w, *, x1=None, stride=1, upsample=False, bias=
                  res=_p(res), ld_res=_rows(res) if res is not None else 0, act=act,
                  out=_p(out), ldc=_rows(out, torch.float32 if out_f32 else BF16),
                  out_f32=int(out_f32))
-    check(lib().vd_gemm(C.byref(d), _stream()), "vd_gemm(conv3x3)")
+    _run_gemm(d, x.device, "vd_gemm(conv3x3)")
     return out, h_out, w_out
 
 
