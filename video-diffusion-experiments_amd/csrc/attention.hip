@@ -13,10 +13,15 @@
 //                    cdna_hip_programming.md §3 "accumulator as next operand"),
 //                    and V^T comes out of LDS with ds_read_b64_tr_b16 (T10) in
 //                    the same permuted key order.  No LDS round trip for P.
-// Workgroup: 4 waves x 32 queries; K/V tiles of 64 keys double-buffered in LDS
-// with the next tile's global loads issued before the current tile's MFMAs
-// (T14).  Row strides are padded so 16-B K-row reads and the transposed V reads
-// are bank-conflict free (guide §2 / T10).
+// Softmax VALU per score kept minimal: the scale is folded into the exp2
+// argument (one FMA), the row max crosses lanes with v_permlane32/16_swap, the
+// O rescale is skipped when no row max moved (wave-uniform), only a ragged
+// last key tile is masked, and when PV is padded (d = 40 -> 48) column d of V
+// holds 1.0 so the PV MFMA also produces the softmax row sum.
+// Workgroup: 4 waves x 16*QBLK queries (QBLK = 4 for long sequences); K/V
+// tiles of 64 keys double-buffered in LDS with the next tile's global loads
+// issued before the current tile's MFMAs (T14).  Row strides are padded so
+// 16-B K-row reads and the transposed V reads are bank-conflict free (§2/T10).
 //
 // temporal_attn_kernel — the motion-module attention over F <= 32 frames
 // (a9).  Tiny per item (16x16 scores), so VALU with one wave per (position,
@@ -26,8 +31,6 @@
 namespace {
 
 constexpr int NT = 256;
-constexpr int QW = 32;   // queries per wave
-constexpr int QBLK = 2;  // 16-query blocks per wave
 constexpr int KT = 64;   // keys per tile
 
 template <int D>
@@ -42,24 +45,36 @@ struct AttnCfg {
   static constexpr int VREG = (KT * VCH + NT - 1) / NT;
 };
 
-template <int D>
+// Cross-lane max over the 4 lanes holding one query (l, l^16, l^32, l^48):
+// v_permlane32_swap / v_permlane16_swap + max, no LDS traffic (T12).
+__device__ __forceinline__ float max_over_query_lanes(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(t[0]), __uint_as_float(t[1]));
+}
+
+template <int D, int QBLK>
 __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
-    int64_t sq, int64_t skv, int64_t kv_div, float scale_log2) {
+    int64_t sq, int64_t skv, int64_t kv_div, float c) {
   using C = AttnCfg<D>;
+  // When PV is padded (DV > D) column D of V is set to 1.0, so the PV MFMA also
+  // produces the softmax row sum (no per-score adds).
+  constexpr bool ONES = C::DV > D;
+  constexpr int QWV = 16 * QBLK;  // queries per wave
   __shared__ __attribute__((aligned(16))) bf16_t ks_lds[2][KT * C::KS];
   __shared__ __attribute__((aligned(16))) bf16_t vs_lds[2][KT * C::VS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = blockIdx.y;
   const int64_t b = blockIdx.z;
-  const int64_t q0 = (int64_t)blockIdx.x * (4 * QW) + wave * QW;
+  const int64_t q0 = (int64_t)blockIdx.x * (4 * QWV) + wave * QWV;
   const int64_t bkv = b / kv_div;
   const bf16_t* qb_ptr = q + b * sq * ldq + (int64_t)h * D;
   const bf16_t* kb_ptr = k + bkv * skv * ldk + (int64_t)h * D;
   const bf16_t* vb_ptr = v + bkv * skv * ldv + (int64_t)h * D;
-
   const int fr = lane & 15, fg = lane >> 4;
 
   // Q^T fragments (B operand): lane holds Q[q0 + qb*16 + fr][dc*32 + 8*fg .. +7].
@@ -82,17 +97,18 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
 #pragma unroll
     for (int i = 0; i < C::KREG; ++i) {
       const int idx = tid + i * NT;
-      const int r = idx / C::KCH, c = idx - r * C::KCH;
+      const int r = idx / C::KCH, cc = idx - r * C::KCH;
       uint4 u = make_uint4(0, 0, 0, 0);
-      if (r < KT && key0 + r < skv && c * 8 < D) u = *(const uint4*)(kb_ptr + (key0 + r) * ldk + c * 8);
+      if (r < KT && key0 + r < skv && cc * 8 < D) u = *(const uint4*)(kb_ptr + (key0 + r) * ldk + cc * 8);
       kreg[i] = u;
     }
 #pragma unroll
     for (int i = 0; i < C::VREG; ++i) {
       const int idx = tid + i * NT;
-      const int r = idx / C::VCH, c = idx - r * C::VCH;
+      const int r = idx / C::VCH, cc = idx - r * C::VCH;
       uint4 u = make_uint4(0, 0, 0, 0);
-      if (r < KT && key0 + r < skv && c * 8 < D) u = *(const uint4*)(vb_ptr + (key0 + r) * ldv + c * 8);
+      if (r < KT && key0 + r < skv && cc * 8 < D) u = *(const uint4*)(vb_ptr + (key0 + r) * ldv + cc * 8);
+      if (ONES && cc == D / 8) u.x = 0x3F80u;  // bf16 1.0 in column D
       vreg[i] = u;
     }
   };
@@ -100,14 +116,14 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
 #pragma unroll
     for (int i = 0; i < C::KREG; ++i) {
       const int idx = tid + i * NT;
-      const int r = idx / C::KCH, c = idx - r * C::KCH;
-      if (r < KT) *(uint4*)(&ks_lds[buf][r * C::KS + c * 8]) = kreg[i];
+      const int r = idx / C::KCH, cc = idx - r * C::KCH;
+      if (r < KT) *(uint4*)(&ks_lds[buf][r * C::KS + cc * 8]) = kreg[i];
     }
 #pragma unroll
     for (int i = 0; i < C::VREG; ++i) {
       const int idx = tid + i * NT;
-      const int r = idx / C::VCH, c = idx - r * C::VCH;
-      if (r < KT) *(uint4*)(&vs_lds[buf][r * C::VS + c * 8]) = vreg[i];
+      const int r = idx / C::VCH, cc = idx - r * C::VCH;
+      if (r < KT) *(uint4*)(&vs_lds[buf][r * C::VS + cc * 8]) = vreg[i];
     }
   };
 
@@ -116,17 +132,16 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
   for (int a = 0; a < C::DV / 16; ++a)
 #pragma unroll
     for (int qb = 0; qb < QBLK; ++qb) oacc[a][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float mrow[QBLK], lrow[QBLK];
+  float mrow[QBLK], lrow[QBLK];  // running max (scaled, log2 units) / lane-partial row sum
 #pragma unroll
   for (int qb = 0; qb < QBLK; ++qb) { mrow[qb] = -INFINITY; lrow[qb] = 0.f; }
 
   const int ntiles = (int)((skv + KT - 1) / KT);
+  const bool ragged = (skv % KT) != 0;
   load_kv(0);
   store_kv(0);
   __syncthreads();
-
-  // tr-read lane geometry: lane 4*qq + pp of its 16-lane group addresses row qq, cols 4*pp..
-  const int qq = fr >> 2, pp = fr & 3;
+  const int qq = fr >> 2, pp = fr & 3;  // tr-read geometry: lane 4*qq+pp -> row qq, cols 4*pp..
 
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
@@ -150,40 +165,43 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
           s[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qb][dc], s[kb][qb], 0, 0, 0);
       }
     }
-    // ---- mask + online softmax (scores kept in log2 units)
-    const int64_t kbase = (int64_t)t * KT + 4 * fg;
-    bf16x8 pf[2][QBLK];
-#pragma unroll
-    for (int qb = 0; qb < QBLK; ++qb) {
-      float mx = -INFINITY;
+    if (ragged && t == ntiles - 1) {  // only the last tile of a ragged key range is masked
+      const int64_t kbase = (int64_t)t * KT + 4 * fg;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float x = s[kb][qb][j] * scale_log2;
-          if (kbase + kb * 16 + j >= skv) x = -INFINITY;
-          s[kb][qb][j] = x;
-          mx = fmaxf(mx, x);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        for (int j = 0; j < 4; ++j)
+          if (kbase + kb * 16 + j >= skv) {
+#pragma unroll
+            for (int qb = 0; qb < QBLK; ++qb) s[kb][qb][j] = -INFINITY;
+          }
+    }
+    // ---- online softmax in log2 units: p = exp2(s*c - m)
+    bf16x8 pf[2][QBLK];
+    bool any_rescale = false;
+    float alpha[QBLK];
+#pragma unroll
+    for (int qb = 0; qb < QBLK; ++qb) {
+      float mx = s[0][qb][0];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mx = fmaxf(mx, s[kb][qb][j]);
+      mx = max_over_query_lanes(mx) * c;
       const float mnew = fmaxf(mrow[qb], mx);
-      const float alpha = exp2f(mrow[qb] - mnew);
+      alpha[qb] = __builtin_amdgcn_exp2f(mrow[qb] - mnew);
+      any_rescale |= mnew != mrow[qb];
       mrow[qb] = mnew;
       float ls = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float p = exp2f(s[kb][qb][j] - mnew);
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][qb][j], c, -mnew));
           s[kb][qb][j] = p;
-          ls += p;
+          if (!ONES) ls += p;
         }
-      lrow[qb] = lrow[qb] * alpha + ls;
-#pragma unroll
-      for (int a = 0; a < C::DV / 16; ++a)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) oacc[a][qb][j] *= alpha;
+      if (!ONES) lrow[qb] = lrow[qb] * alpha[qb] + ls;
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         bf16x8 f;
@@ -194,6 +212,14 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
         }
         pf[st][qb] = f;
       }
+    }
+    if (__any(any_rescale)) {  // wave-uniform: skip the O-wide multiply when no max moved
+#pragma unroll
+      for (int a = 0; a < C::DV / 16; ++a)
+#pragma unroll
+        for (int qb = 0; qb < QBLK; ++qb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) oacc[a][qb][j] *= alpha[qb];
     }
     // ---- O^T += V^T . P^T
 #pragma unroll
@@ -218,9 +244,15 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
   // ---- epilogue: O[q][d] = O^T[d][q] / l
 #pragma unroll
   for (int qb = 0; qb < QBLK; ++qb) {
-    float l = lrow[qb];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    float l;
+    if constexpr (ONES) {
+      constexpr int a1 = D / 16, r1 = D % 16;
+      l = __shfl(oacc[a1][qb][r1 % 4], (r1 / 4) * 16 + fr, 64);
+    } else {
+      l = lrow[qb];
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+    }
     const float inv = 1.0f / l;
     const int64_t qi = q0 + qb * 16 + fr;
     if (qi >= sq) continue;
@@ -240,10 +272,18 @@ template <int D>
 int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                  void* o, int64_t ldo, int64_t batch, int heads, int64_t sq, int64_t skv,
                  int64_t kv_div, float scale, hipStream_t s) {
-  const dim3 grid((unsigned)((sq + 4 * QW - 1) / (4 * QW)), (unsigned)heads, (unsigned)batch);
-  hipLaunchKernelGGL(flash_attn_kernel<D>, grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                     (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv,
-                     kv_div, scale * 1.4426950408889634f);
+  const float c = scale * 1.4426950408889634f;
+  if (sq >= 1024 && D <= 64) {
+    const dim3 grid((unsigned)((sq + 255) / 256), (unsigned)heads, (unsigned)batch);
+    hipLaunchKernelGGL((flash_attn_kernel<D, 4>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                       (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv,
+                       kv_div, c);
+  } else {
+    const dim3 grid((unsigned)((sq + 127) / 128), (unsigned)heads, (unsigned)batch);
+    hipLaunchKernelGGL((flash_attn_kernel<D, 2>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                       (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv,
+                       kv_div, c);
+  }
   return vd_launch_status();
 }
 
