@@ -1,0 +1,95 @@
+"""Kernel microbenchmark over the UNet's real shapes (full config, 1 GPU).
+
+python tools/kbench.py [filter]  -> one line per shape: us, TFLOP/s, effective GB/s
+"""
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "video-diffusion-experiments_amd")]
+import torch  # noqa: E402
+
+from vdiff import ops  # noqa: E402
+from vdiff._lib import lib  # noqa: E402
+
+flt = sys.argv[1] if len(sys.argv) > 1 else ""
+dev = "cuda"
+g = torch.Generator(device=dev).manual_seed(0)
+
+
+def rnd(*s, std=1.0):
+    return (torch.randn(*s, device=dev, generator=g) * std).to(torch.bfloat16)
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def report(name, us, flop, byts):
+    print(f"{name:58s} {us:9.1f} us {flop / us / 1e6:8.1f} TF/s {byts / us / 1e3:8.1f} GB/s", flush=True)
+
+
+cases = []
+# dense GEMMs (M, N, K, extra)
+for lvl, (hw, C) in enumerate([(4096, 320), (1024, 640), (256, 1280), (64, 1280)]):
+    M = 32 * hw
+    cases += [(f"L{lvl+1} dense proj   M={M} N={C} K={C} +res", "dense", M, C, C, True),
+              (f"L{lvl+1} dense qkv    M={M} N={3*C} K={C}", "dense", M, 3 * C, C, False),
+              (f"L{lvl+1} dense ff2    M={M} N={C} K={4*C} +res", "dense", M, C, 4 * C, True),
+              (f"L{lvl+1} geglu        M={M} N={8*C} K={C}", "geglu", M, 8 * C, C, False)]
+convs = [("L1 conv 320->320", 32, 64, 320, 320), ("L2 conv 640->640", 32, 32, 640, 640),
+         ("L3 conv 1280->1280", 32, 16, 1280, 1280), ("L4 conv 1280->1280", 32, 8, 1280, 1280),
+         ("L4 conv 2560->1280", 32, 8, 2560, 1280), ("L1 conv 640->320", 32, 64, 640, 320)]
+
+for name, kind, M, N, K, res in cases:
+    if flt not in name:
+        continue
+    a = rnd(M, K)
+    w = rnd(N, K, std=K ** -0.5)
+    b = torch.zeros(N, device=dev)
+    r = rnd(M, N) if res else None
+    for path in __import__("os").environ.get("KB_PATHS", "v2,v1").split(","):
+        lib().vd_gemm_force_v1(int(path == "v1"))
+        act = ops.ACT_GEGLU if kind == "geglu" else ops.ACT_NONE
+        nout = N // 2 if kind == "geglu" else N
+        out = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
+        us = timeit(lambda: ops.gemm(a, w, bias=b, res=r, act=act, out=out))
+        byts = 2 * (M * K + N * K + M * nout + (M * N if res else 0))
+        report(f"{name} [{path}]", us, 2.0 * M * N * K, byts)
+    lib().vd_gemm_force_v1(0)
+
+for name, n, hw, ci, co in convs:
+    if flt not in name:
+        continue
+    x = rnd(n * hw * hw, ci)
+    w = rnd(co, 9 * ci, std=(9 * ci) ** -0.5)
+    out = torch.empty(n * hw * hw, co, device=dev, dtype=torch.bfloat16)
+    for path in __import__("os").environ.get("KB_PATHS", "v2,v1").split(","):
+        lib().vd_gemm_force_v1(int(path == "v1"))
+        us = timeit(lambda: ops.conv3x3(x, n, hw, hw, w, out=out))
+        report(f"{name} M={n*hw*hw} K={9*ci} [{path}]", us, 2.0 * n * hw * hw * co * 9 * ci,
+               2 * (n * hw * hw * (ci + co) + co * 9 * ci))
+    lib().vd_gemm_force_v1(0)
+
+for name, n_img, S, d, skv in [("attn L1 self", 32, 4096, 40, 4096), ("attn L2 self", 32, 1024, 80, 1024),
+                               ("attn L3 self", 32, 256, 160, 256), ("attn L1 cross", 32, 4096, 40, 77)]:
+    if flt not in name:
+        continue
+    C = 8 * d
+    qkv = rnd(n_img * S, 3 * C, std=1.5)
+    kv = rnd(2 * skv, 2 * C, std=1.5)
+    out = torch.empty(n_img * S, C, device=dev, dtype=torch.bfloat16)
+    if skv == S:
+        fn = lambda: ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], n_img, 8, S, S, d, out=out)
+    else:
+        fn = lambda: ops.attention(qkv[:, :C], kv[:, :C], kv[:, C:], n_img, 8, S, skv, d, kv_div=16, out=out)
+    us = timeit(fn)
+    report(f"{name} S={S} d={d} skv={skv}", us, 4.0 * n_img * 8 * S * skv * d, 2 * n_img * S * C * 4)

@@ -33,19 +33,30 @@ __device__ __forceinline__ int lds_off(int row, int chunk) {
 template <int BM, int BN, int MB, int NB>
 __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], int64_t m0,
                                               int64_t n0, int wm, int wn, int lane) {
-  const int64_t M = d.M, N = d.N;
+  // acc[a][b][j] = C[m = m0 + wm*MB*16 + b*16 + fr][n = n0 + wn*BN/2 + a*16 + 4*fq + j]
+  // All offsets fit 32 bits (M*ldc < 2^31 is checked on the host).
+  const int M = (int)d.M, N = (int)d.N;
   const int fr = lane & 15, fq = lane >> 4;
-  // acc[a][b][j] = C[m = m0 + wm*BM/WM + b*16 + fr][n = n0 + wn*BN/2 + a*16 + 4*fq + j]
-  constexpr int WROWS = MB * 16;
-  const int64_t nw = n0 + wn * (BN / 2);
+  const int nw = (int)n0 + wn * (BN / 2);
+  int mrow[MB];
+  bool mok[MB];
+  const float* rbrow[MB];
+#pragma unroll
+  for (int b = 0; b < MB; ++b) {
+    const int m = (int)m0 + wm * MB * 16 + b * 16 + fr;
+    mok[b] = m < M;
+    mrow[b] = mok[b] ? m : 0;
+    rbrow[b] = d.rowbias ? d.rowbias + (int64_t)(mrow[b] / (int)d.rb_div) * d.ld_rb : nullptr;
+  }
   if (d.act == VD_ACT_GEGLU) {
     if constexpr (NB % 2 == 0) {
+      bf16_t* out = (bf16_t*)d.out;
 #pragma unroll
       for (int a = 0; a < NB; a += 2) {
-        const int64_t nh = nw + a * 16 + 4 * fq;        // packed hidden column
-        const int64_t ng = nh + 16;                      // packed gate column
+        const int nh = nw + a * 16 + 4 * fq;  // packed hidden column
+        const int ng = nh + 16;                // packed gate column
         if (ng >= N) continue;
-        const int64_t nout = nw / 2 + (a / 2) * 16 + 4 * fq;
+        const int nout = nw / 2 + (a / 2) * 16 + 4 * fq;
         float bh[4] = {0, 0, 0, 0}, bg[4] = {0, 0, 0, 0};
         if (d.bias) {
           const float4 t0 = *(const float4*)(d.bias + nh);
@@ -55,13 +66,11 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
         }
 #pragma unroll
         for (int b = 0; b < MB; ++b) {
-          const int64_t m = m0 + wm * WROWS + b * 16 + fr;
-          if (m >= M) continue;
+          if (!mok[b]) continue;
           float o[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) o[j] = (acc[a][b][j] + bh[j]) * gelu_erf(acc[a + 1][b][j] + bg[j]);
-          bf16_t* op = (bf16_t*)d.out + m * d.ldc + nout;
-          *(uint2*)op = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          *(uint2*)(out + (uint32_t)(mrow[b] * (int)d.ldc + nout)) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
         }
       }
     }
@@ -69,7 +78,7 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
   }
 #pragma unroll
   for (int a = 0; a < NB; ++a) {
-    const int64_t n = nw + a * 16 + 4 * fq;
+    const int n = nw + a * 16 + 4 * fq;
     if (n >= N) continue;
     float bv[4] = {0, 0, 0, 0};
     if (d.bias) {
@@ -78,13 +87,12 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
     }
 #pragma unroll
     for (int b = 0; b < MB; ++b) {
-      const int64_t m = m0 + wm * WROWS + b * 16 + fr;
-      if (m >= M) continue;
+      if (!mok[b]) continue;
       float o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = acc[a][b][j] + bv[j];
       if (d.rowbias) {
-        const float4 t = *(const float4*)(d.rowbias + (m / d.rb_div) * d.ld_rb + n);
+        const float4 t = *(const float4*)(rbrow[b] + n);
         o[0] += t.x; o[1] += t.y; o[2] += t.z; o[3] += t.w;
       }
       if (d.act == VD_ACT_SILU) {
@@ -92,13 +100,14 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
         for (int j = 0; j < 4; ++j) o[j] = silu_f(o[j]);
       }
       if (d.res) {
-        const uint2 r = *(const uint2*)((const bf16_t*)d.res + m * d.ld_res + n);
+        const uint2 r = *(const uint2*)((const bf16_t*)d.res + (uint32_t)(mrow[b] * (int)d.ld_res + n));
         o[0] += bf_lo(r.x); o[1] += bf_hi(r.x); o[2] += bf_lo(r.y); o[3] += bf_hi(r.y);
       }
+      const uint32_t off = (uint32_t)(mrow[b] * (int)d.ldc + n);
       if (d.out_f32) {
-        *(float4*)((float*)d.out + m * d.ldc + n) = make_float4(o[0], o[1], o[2], o[3]);
+        *(float4*)((float*)d.out + off) = make_float4(o[0], o[1], o[2], o[3]);
       } else {
-        *(uint2*)((bf16_t*)d.out + m * d.ldc + n) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+        *(uint2*)((bf16_t*)d.out + off) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
       }
     }
   }
@@ -259,6 +268,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
 // outside the image are zero-filled by the buffer range check (voffset beyond
 // num_records returns 0).  Per-tile address work: one integer add per load.
 constexpr int G2_BM = 256, G2_NT = 512, G2_STAGES = 3;
+int g_num_cus = 256;  // MI355X; refreshed from the device on first use
 constexpr uint32_t G2_OOB = 0x80000000u;
 
 template <int BN>
@@ -291,7 +301,7 @@ __device__ __forceinline__ void wait_vm() {
 template <int BN, int MODE>
 __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                          uint32_t a1_bytes, uint32_t w_bytes,
-                                                         int split) {
+                                                         int split, int per_wg) {
   using C = G2<BN>;
   __shared__ __attribute__((aligned(1024))) char smem[G2_STAGES * C::STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -300,70 +310,77 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
   const int64_t M = d.M, N = d.N, K = d.K;
   const int tiles_n = (int)((N + BN - 1) / BN);
   const int tiles_m = (int)((M + G2_BM - 1) / G2_BM);
-  const int gid = xcd_remap(blockIdx.x, tiles_n * tiles_m * split);
-  const int sp = gid % split;          // split-K slice (adjacent ids share the output tile)
-  const int id = gid / split;
-  const int64_t m0 = (int64_t)(id / tiles_n) * G2_BM;
-  const int64_t n0 = (int64_t)(id % tiles_n) * BN;
+  const int units = tiles_n * tiles_m * split;
+  // Persistent: this workgroup owns the contiguous unit range [u_begin, u_end);
+  // a unit is (output tile, split-K slice), slices adjacent.  XCD-aware so the
+  // workgroups sharing an L2 walk neighbouring tiles.
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int u_begin = lid * per_wg;
+  const int u_end = u_begin + per_wg < units ? u_begin + per_wg : units;
   const int nk_all = (int)(K / BK);
-  const int kt0 = (int)((int64_t)nk_all * sp / split), kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
 
-  const int rb = lane >> 3;                    // row within the 8-row DMA block
-  const uint32_t lc16 = (uint32_t)(((lane & 7) ^ rb) * 16);   // swizzled source chunk (bytes)
-
+  const int rb = lane >> 3;                                  // row within the 8-row DMA block
+  const uint32_t lc16 = (uint32_t)(((lane & 7) ^ rb) * 16);  // swizzled source chunk (bytes)
   const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)d.a0, 0, a0_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ra1 =
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.a1 ? d.a1 : d.a0), 0, d.a1 ? a1_bytes : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, w_bytes, 0x00020000);
-
-  // B (weights): this wave issues instructions bi = j*8 + wid, rows bi*8 + rb.
-  const int nbw = (C::NBI - wid + 7) / 8;
-  uint32_t boff[C::NBMAX];
-#pragma unroll
-  for (int j = 0; j < C::NBMAX; ++j) {
-    int64_t n = n0 + (j * 8 + wid) * 8 + rb;
-    n = n < N ? n : N - 1;
-    boff[j] = (uint32_t)(n * d.ldw * 2) + lc16;
-  }
-  // A: this wave issues rows (wid*4 + j)*8 + rb, j < 4.
-  uint32_t aoff0[C::NA], aoff1[C::NA];
-  int poh[C::NA], pow_[C::NA], pimg[C::NA];
-  if constexpr (MODE == VD_A_DENSE) {
-#pragma unroll
-    for (int j = 0; j < C::NA; ++j) {
-      int64_t m = m0 + (wid * 4 + j) * 8 + rb;
-      m = m < M ? m : M - 1;
-      aoff0[j] = (uint32_t)(m * d.lda0 * 2) + lc16;
-      aoff1[j] = (uint32_t)(m * d.lda1 * 2) + lc16;
-    }
-  } else {
-    const int hw = d.h_out * d.w_out;
-#pragma unroll
-    for (int j = 0; j < C::NA; ++j) {
-      int64_t m = m0 + (wid * 4 + j) * 8 + rb;
-      m = m < M ? m : M - 1;
-      pimg[j] = (int)(m / hw);
-      const int p = (int)(m - (int64_t)pimg[j] * hw);
-      poh[j] = p / d.w_out;
-      pow_[j] = p - poh[j] * d.w_out;
-      aoff0[j] = aoff1[j] = G2_OOB;
-    }
-  }
+  const int nbw = (C::NBI - wid + 7) / 8;  // this wave's B DMA instructions per K-tile
   const int cin = MODE == VD_A_CONV3X3 ? (int)(K / 9) : 0;
   const int hgrid = d.upsample ? 2 * d.h_in : d.h_in;
   const int wgrid = d.upsample ? 2 * d.w_in : d.w_in;
-  // conv: (tap, channel) of the next tile to issue; offsets recomputed on a tap change
+
+  // ---- issue cursor: the (unit, k-tile) whose DMA goes out next
+  int iu = u_begin, ikt = 0, ikt1 = 0;
+  uint32_t boff[C::NBMAX], aoff0[C::NA], aoff1[C::NA];
+  int poh[C::NA], pow_[C::NA], pimg[C::NA];
   int c_tap = 0, c_ci = 0;
   bool c_new = true;
-  if constexpr (MODE == VD_A_CONV3X3) {
-    c_tap = kt0 * BK / cin;
-    c_ci = kt0 * BK - c_tap * cin;
-  }
-
-  auto issue = [&](int kt, int stage) {
+  auto unit_kr = [&](int u, int& kt0, int& kt1) {
+    const int sp = u % split;
+    kt0 = (int)((int64_t)nk_all * sp / split);
+    kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
+  };
+  auto setup_unit = [&](int u) {  // per-unit row offsets for the issue cursor
+    const int tile = u / split;
+    const int64_t m0 = (int64_t)(tile / tiles_n) * G2_BM, n0 = (int64_t)(tile % tiles_n) * BN;
+    int kt0;
+    unit_kr(u, kt0, ikt1);
+    ikt = kt0;
+#pragma unroll
+    for (int j = 0; j < C::NBMAX; ++j) {
+      int64_t n = n0 + (j * 8 + wid) * 8 + rb;
+      n = n < N ? n : N - 1;
+      boff[j] = (uint32_t)(n * d.ldw * 2) + lc16;
+    }
+    if constexpr (MODE == VD_A_DENSE) {
+#pragma unroll
+      for (int j = 0; j < C::NA; ++j) {
+        int64_t m = m0 + (wid * 4 + j) * 8 + rb;
+        m = m < M ? m : M - 1;
+        aoff0[j] = (uint32_t)(m * d.lda0 * 2) + lc16;
+        aoff1[j] = (uint32_t)(m * d.lda1 * 2) + lc16;
+      }
+    } else {
+      const int hw = d.h_out * d.w_out;
+#pragma unroll
+      for (int j = 0; j < C::NA; ++j) {
+        int64_t m = m0 + (wid * 4 + j) * 8 + rb;
+        m = m < M ? m : M - 1;
+        pimg[j] = (int)(m / hw);
+        const int p = (int)(m - (int64_t)pimg[j] * hw);
+        poh[j] = p / d.w_out;
+        pow_[j] = p - poh[j] * d.w_out;
+      }
+      c_tap = kt0 * BK / cin;
+      c_ci = kt0 * BK - c_tap * cin;
+      c_new = true;
+    }
+  };
+  auto issue = [&](int stage) {  // DMA of the cursor's k-tile into `stage`, then advance it
     char* la = smem + stage * C::STAGE;
     char* lb = la + C::A_BYTES;
-    const int kb = kt * BK;
+    const int kb = ikt * BK;
     if constexpr (MODE == VD_A_DENSE) {
       const bool s0 = kb < d.k0;
       const uint32_t koff = (uint32_t)(s0 ? kb : kb - (int)d.k0) * 2;
@@ -398,6 +415,7 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
 #pragma unroll
     for (int j = 0; j < C::NBMAX; ++j)
       if (j < nbw) dma16(rw, lb + (j * 8 + wid) * 1024, boff[j] + (uint32_t)kb * 2);
+    if (++ikt == ikt1 && ++iu < u_end) setup_unit(iu);
   };
 
   f32x4 acc[C::NB][C::MB];
@@ -406,56 +424,85 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
 #pragma unroll
     for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = kt1 - kt0;  // tiles of this split; issue() takes absolute tile indices
-  issue(kt0, 0);
-  if (nk > 1) issue(kt0 + 1, 1);
+  // total k-tiles this workgroup streams
+  int n_it = 0;
+  for (int u = u_begin; u < u_end; ++u) {
+    int a0_, a1_;
+    unit_kr(u, a0_, a1_);
+    n_it += a1_ - a0_;
+  }
+  if (n_it == 0) return;
+  setup_unit(u_begin);
+  issue(0);
+  if (n_it > 1) issue(1);
+  // per-lane LDS byte offsets of the first fragment of each operand for k-step
+  // ks (rows differ by multiples of 16 between fragments, so the (row & 7) XOR
+  // swizzle is the same and fragment a/b adds a constant)
+  uint32_t wlane[BK / 32], xlane[BK / 32];
+#pragma unroll
+  for (int ks = 0; ks < BK / 32; ++ks) {
+    wlane[ks] = C::A_BYTES + 2 * lds_off(wn * (BN / 2) + (lane & 15), ks * 4 + (lane >> 4));
+    xlane[ks] = 2 * lds_off(wm * 64 + (lane & 15), ks * 4 + (lane >> 4));
+  }
+  // ---- compute cursor
+  int cu = u_begin, ckt, ckt1;
+  unit_kr(cu, ckt, ckt1);
   const int fr = lane & 15, fq = lane >> 4;
   int stage = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    // this wave's DMA for tile kt has landed once at most tile kt+1's remain outstanding
-    if (kt + 1 < nk) {
+  for (int it = 0; it < n_it; ++it) {
+    // this wave's DMA for k-tile `it` has landed once at most k-tile it+1's remain
+    // outstanding (everything issued before that, epilogue stores included, is done)
+    if (it + 1 < n_it) {
       if (nbw == C::NBMAX) wait_vm<C::NA + C::NBMAX>();
       else wait_vm<C::NA + C::NBMAX - 1>();
     } else {
       wait_vm<0>();
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's DMA for kt landed; stage (kt-1)%3 fully read
-    if (kt + 2 < nk) issue(kt0 + kt + 2, stage == 0 ? 2 : stage - 1);
-    const bf16_t* as = (const bf16_t*)(smem + stage * C::STAGE);
-    const bf16_t* ws = (const bf16_t*)(smem + stage * C::STAGE + C::A_BYTES);
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for `it` landed; stage (it-1)%3 fully read
+    const char* sbase = smem + stage * C::STAGE;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 wf[C::NB], xf[C::MB];
+      const char* wp = sbase + wlane[ks];
+      const char* xp = sbase + xlane[ks];
 #pragma unroll
-      for (int a = 0; a < C::NB; ++a)
-        wf[a] = *(const bf16x8*)(ws + lds_off(wn * (BN / 2) + a * 16 + fr, ks * 4 + fq));
+      for (int a = 0; a < C::NB; ++a) wf[a] = *(const bf16x8*)(wp + a * 16 * BK * 2);
 #pragma unroll
-      for (int b = 0; b < C::MB; ++b)
-        xf[b] = *(const bf16x8*)(as + lds_off(wm * 64 + b * 16 + fr, ks * 4 + fq));
+      for (int b = 0; b < C::MB; ++b) xf[b] = *(const bf16x8*)(xp + b * 16 * BK * 2);
 #pragma unroll
       for (int a = 0; a < C::NB; ++a)
 #pragma unroll
         for (int b = 0; b < C::MB; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][b], 0, 0, 0);
     }
-    stage = stage == 2 ? 0 : stage + 1;
-  }
-  if (split == 1) {
-    gemm_epilogue<G2_BM, BN, C::MB, C::NB>(d, acc, m0, n0, wm, wn, lane);
-    return;
-  }
-  // split-K: raw fp32 partial slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
-  float* slab = (float*)d.ws + (int64_t)sp * M * N;
+    if (++ckt == ckt1) {  // unit finished: epilogue (its memory ops precede the next DMA)
+      const int tile = cu / split, sp = cu % split;
+      const int64_t m0 = (int64_t)(tile / tiles_n) * G2_BM, n0 = (int64_t)(tile % tiles_n) * BN;
+      if (split == 1) {
+        gemm_epilogue<G2_BM, BN, C::MB, C::NB>(d, acc, m0, n0, wm, wn, lane);
+      } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
+        float* slab = (float*)d.ws + (int64_t)sp * M * N;
 #pragma unroll
-  for (int a = 0; a < C::NB; ++a) {
-    const int64_t n = n0 + wn * (BN / 2) + a * 16 + 4 * fq;
-    if (n >= N) continue;
+        for (int a = 0; a < C::NB; ++a) {
+          const int64_t n = n0 + wn * (BN / 2) + a * 16 + 4 * fq;
+          if (n >= N) continue;
 #pragma unroll
-    for (int b = 0; b < C::MB; ++b) {
-      const int64_t m = m0 + wm * 64 + b * 16 + fr;
-      if (m < M) *(float4*)(slab + m * N + n) = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+          for (int b = 0; b < C::MB; ++b) {
+            const int64_t m = m0 + wm * 64 + b * 16 + fr;
+            if (m < M)
+              *(float4*)(slab + m * N + n) = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+          }
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < C::NB; ++a)
+#pragma unroll
+        for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (++cu < u_end) unit_kr(cu, ckt, ckt1);
     }
+    if (it + 2 < n_it) issue(stage == 0 ? 2 : stage - 1);
+    stage = stage == 2 ? 0 : stage + 1;
   }
 }
 
@@ -517,11 +564,15 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
 
 template <int BN>
 int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
-  const int64_t tiles = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + BN - 1) / BN) * split;
+  const int64_t units = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + BN - 1) / BN) * split;
+  const int64_t per = (units + g_num_cus - 1) / g_num_cus;   // persistent: one workgroup per CU
+  const int64_t grid = (units + per - 1) / per;
   if (d.a_mode == VD_A_CONV3X3)
-    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3>), dim3((unsigned)tiles), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
+    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb,
+                       split, (int)per);
   else
-    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)tiles), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
+    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb,
+                       split, (int)per);
   int rc = vd_launch_status();
   if (rc != VD_OK || split == 1) return rc;
   const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
@@ -596,6 +647,7 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   VD_CHECK_ARG(d.lda0 % 8 == 0 && d.k0 % 8 == 0 && d.k0 > 0);
   if (d.a1) VD_CHECK_ARG(al16(d.a1) && d.lda1 % 8 == 0);
   VD_CHECK_ARG(d.ldc % 4 == 0);
+  VD_CHECK_ARG(d.M * d.ldc < 0x7fffffff && (!d.res || d.M * d.ld_res < 0x7fffffff) && d.N < 0x7fffffff);
   VD_CHECK_ARG(d.out_f32 ? al16(d.out) : al8(d.out));
   if (d.bias) VD_CHECK_ARG(al16(d.bias));
   if (d.rowbias) VD_CHECK_ARG(al16(d.rowbias) && d.ld_rb % 4 == 0 && d.rb_div > 0);
@@ -618,6 +670,14 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
     if (d.k0 < d.K) VD_CHECK_ARG(d.a1 != nullptr);
   }
   if (d.act == VD_ACT_GEGLU) VD_CHECK_ARG(d.N % 32 == 0 && !d.res && !d.rowbias && !d.out_f32);
+  static bool cus_read = false;
+  if (!cus_read) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_num_cus = n;
+    cus_read = true;
+  }
   const Plan p = plan(d);
   if (p.v2) {
     if (p.split > 1) VD_CHECK_ARG(d.ws && al16(d.ws) && d.ws_bytes >= p.ws_bytes);
