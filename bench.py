@@ -77,6 +77,20 @@ def time_attention(n_img, reps, stream):
             "algorithmic_bytes_per_launch": byts}
 
 
+def pmc_traffic(n_img):
+    """HBM bytes per launch of the roofline kernel from the newest committed PMC
+    summary (profiles/rNN_traffic.json, written by tools/traffic.sh from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes over the same kernel at 32 images;
+    scaled linearly to this rank's image count).  None when absent."""
+    files = sorted((ROOT / "profiles").glob("r*_traffic.json"))
+    if not files:
+        return None, None
+    t = json.loads(files[-1].read_text())
+    if "flash_attn_kernel<40" not in (t.get("kernel") or ""):
+        return None, None
+    return t["traffic_bytes_per_launch"] * n_img / 32.0, files[-1].name
+
+
 def cpu_baseline(unet_gpu, cfg_name, frames_sample, frames_full):
     """Oracle (oracle/unet_ref.py, fp32 PyTorch-CPU) on `frames_sample` frames of the
     same CFG-batch step; scaled to steps/s of the full `frames_full`-frame video."""
@@ -170,6 +184,7 @@ def main():
     ms = 1e3 * elapsed / args.steps
 
     roof = time_attention(2 * fl, args.attn_reps, torch.cuda.current_stream())
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(2 * fl)
     step_tf = STEP_TFLOP[cfg_name] * (frames / (16 if cfg_name == "full" else 4)) / (ms * 1e-3) / world
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

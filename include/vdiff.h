@@ -135,6 +135,9 @@ int vd_layernorm(const void* x, int64_t ldx, int64_t rows, int64_t C, const floa
 int vd_attention(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                  int64_t ldv, void* o, int64_t ldo, int64_t batch, int32_t heads, int64_t sq,
                  int64_t skv, int32_t d, int64_t kv_div, float scale, vd_stream_t stream);
+/* Test/benchmark hook: on != 0 routes d = 40 to the 16x16x32 flash kernel instead of
+ * the 32x32x16 one (default). */
+int vd_attention_force_v1(int32_t on);
 
 /* Temporal (motion-module) self-attention over frames (a9): token (b, f, p) is
  * row (b*frames + f)*positions + p of q/k/v/o (the NHWC layout, no permute);

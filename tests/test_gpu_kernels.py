@@ -69,6 +69,23 @@ def test_gemm_epilogues(cuda):
     close_bf16(got, F.silu(x @ w.double().T + b.double()))
 
 
+@pytest.mark.parametrize("N,out_view", [(100, False), (328, False), (488, True), (1288, False)])
+def test_gemm_epilogue_widths(cuda, gemm_path, N, out_view):
+    """16-B (permlane16-paired) epilogue vs its 8-B fallback: N % 8 == 4 and an output /
+    residual whose row stride is not a multiple of 8 take the narrow path; N = 328 / 1288
+    leave a partial last column tile on the wide one."""
+    M, K = 700, 320
+    a, w = rnd(M, K), rnd(N, K, std=K ** -0.5)
+    b = torch.randn(N, device=cuda)
+    if out_view:
+        out = torch.empty(M, N + 4, device=cuda, dtype=torch.bfloat16)[:, :N]
+        res = rnd(M, N + 4)[:, :N]
+    else:
+        out, res = None, rnd(M, N)
+    got = ops.gemm(a, w, bias=b, res=res, out=out)
+    close_bf16(got, a.double() @ w.double().T + b.double() + res.double())
+
+
 def test_gemm_geglu(cuda):
     M, C = 333, 64
     n = rnd(M, C)
@@ -247,6 +264,15 @@ def sdpa_ref(q, k, v, batch, heads, sq, skv, d, kv_div=1):
     return (w @ vb).transpose(1, 2).reshape(batch * sq, heads * d)
 
 
+@pytest.fixture(params=["flash32", "v1"])
+def attn_path(request, cuda):
+    """d = 40 runs on the 32x32x16 kernel by default; "v1" forces the 16x16x32 one."""
+    from vdiff._lib import lib
+    lib().vd_attention_force_v1(int(request.param == "v1"))
+    yield request.param
+    lib().vd_attention_force_v1(0)
+
+
 @pytest.mark.parametrize("d", [32, 40, 64, 80, 128, 160])
 @pytest.mark.parametrize("sq", [64, 300, 1024])
 def test_flash_attention_self(cuda, d, sq):
@@ -279,6 +305,66 @@ def test_flash_attention_rescale_spike(cuda):
     k[100] = bf(q[5].float() * 4)   # spike for query 5 at key 100 (tile 1)
     got = ops.attention(q, k, v, batch, heads, sq, sq, d)
     close_bf16(got, sdpa_ref(q, k, v, batch, heads, sq, sq, d))
+
+
+@pytest.mark.parametrize("sq,skv", [(256, 256), (300, 77), (1000, 333), (64, 1)])
+def test_flash_attention_d40_paths(attn_path, sq, skv):
+    """Both d = 40 kernels over aligned, ragged and single-key shapes (queries past sq,
+    keys past skv), fused-QKV strides for self and separate K/V otherwise."""
+    torch.manual_seed(11)
+    batch, heads, d = 2, 8, 40
+    C = heads * d
+    q = rnd(batch * sq, 3 * C, std=1.5)[:, :C]
+    kv = rnd(batch * skv, 2 * C, std=1.5)
+    got = ops.attention(q, kv[:, :C], kv[:, C:], batch, heads, sq, skv, d)
+    close_bf16(got, sdpa_ref(q, kv[:, :C], kv[:, C:], batch, heads, sq, skv, d))
+
+
+def _deferred_max_case(kind, sq=256, skv=640, d=40):
+    """Score patterns that drive the deferred-max branch (§5.4 rule 26): the branch
+    is data-dependent, so each case forces a different decision sequence.  Scores run
+    along a fixed unit direction u: s*log2(e)/sqrt(d) grows by about 2.7*alpha per
+    64-key tile for q = 12u, k = alpha*tile*u (threshold THR = 6 in those units)."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    q = torch.randn(sq, d, device="cuda", generator=g)
+    k = torch.randn(skv, d, device="cuda", generator=g)
+    v = torch.randn(skv, d, device="cuda", generator=g)
+    u = torch.randn(d, device="cuda", generator=g)
+    u = u / u.norm()
+    tile = (torch.arange(skv, device="cuda") // 64).float()[:, None]
+    if kind == "ramp":          # each tile's max beats the last by ~8 > THR: rescale every tile
+        q, k = 12 * u + 0.3 * q, 3.0 * tile * u + 0.1 * k
+    elif kind == "creep":       # growth ~3 < THR per tile: deferred, P accumulates up to 2^THR
+        q, k = 12 * u + 0.3 * q, 1.1 * tile * u + 0.1 * k
+    elif kind == "late_spike":  # one query's max jumps in the last tile only (mixed lanes)
+        k = 0.1 * k
+        k[skv - 3] = q[37] * 6
+    elif kind == "offset":      # all scores ~ +70 (mu far from 0: bf16 rounding of mu)
+        q, k = 8 * u + 0.3 * q, 40 * u + 0.1 * k
+    elif kind == "negative":    # all scores ~ -70: the first tile's mu must come from the data
+        q, k = 8 * u + 0.3 * q, -40 * u + 0.1 * k
+    return bf(q), bf(k), bf(v)
+
+
+@pytest.mark.parametrize("kind", ["ramp", "creep", "late_spike", "offset", "negative"])
+def test_flash_attention_deferred_max(attn_path, kind):
+    q, k, v = _deferred_max_case(kind)
+    sq, skv, d = q.shape[0], k.shape[0], q.shape[1]
+    got = ops.attention(q, k, v, 1, 1, sq, skv, d)
+    assert torch.isfinite(got.float()).all()
+    close_bf16(got, sdpa_ref(q, k, v, 1, 1, sq, skv, d))
+
+
+def test_flash_attention_unit_scale(cuda):
+    """c = scale*log2(e) == 1 exactly skips the in-kernel Q prescale (callers that fold
+    the softmax scale into the Q projection); must equal the prescaled path's math."""
+    torch.manual_seed(2)
+    sq, d = 512, 40
+    q, k, v = rnd(sq, d, std=3.0), rnd(sq, d), rnd(sq, d)
+    got = ops.attention(q, k, v, 1, 1, sq, sq, d, scale=1.0 / math.log2(math.e))
+    qd, kd, vd = q.double(), k.double(), v.double()
+    want = torch.softmax(qd @ kd.T / math.log2(math.e), -1) @ vd
+    close_bf16(got, want)
 
 
 @pytest.mark.parametrize("frames,d", [(16, 40), (16, 160), (4, 32), (32, 80), (5, 64)])

@@ -57,6 +57,10 @@ for name, kind, M, N, K, res in cases:
     b = torch.zeros(N, device=dev)
     r = rnd(M, N) if res else None
     for path in __import__("os").environ.get("KB_PATHS", "v2,v1").split(","):
+        if path == "torch":  # vendor comparator: hipBLASLt through F.linear (no epilogue fusion)
+            us = timeit(lambda: torch.nn.functional.linear(a, w))
+            report(f"{name} [hipblaslt]", us, 2.0 * M * N * K, 2 * (M * K + N * K + M * N))
+            continue
         lib().vd_gemm_force_v1(int(path == "v1"))
         act = ops.ACT_GEGLU if kind == "geglu" else ops.ACT_NONE
         nout = N // 2 if kind == "geglu" else N
@@ -73,6 +77,13 @@ for name, n, hw, ci, co in convs:
     w = rnd(co, 9 * ci, std=(9 * ci) ** -0.5)
     out = torch.empty(n * hw * hw, co, device=dev, dtype=torch.bfloat16)
     for path in __import__("os").environ.get("KB_PATHS", "v2,v1").split(","):
+        if path == "torch":  # vendor comparator: MIOpen NCHW-channels_last conv
+            xc = x.view(n, hw, hw, ci).permute(0, 3, 1, 2)
+            wc = w.view(co, 3, 3, ci).permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+            us = timeit(lambda: torch.nn.functional.conv2d(xc, wc, padding=1))
+            report(f"{name} M={n*hw*hw} K={9*ci} [miopen]", us, 2.0 * n * hw * hw * co * 9 * ci,
+                   2 * (n * hw * hw * (ci + co) + co * 9 * ci))
+            continue
         lib().vd_gemm_force_v1(int(path == "v1"))
         us = timeit(lambda: ops.conv3x3(x, n, hw, hw, w, out=out))
         report(f"{name} M={n*hw*hw} K={9*ci} [{path}]", us, 2.0 * n * hw * hw * co * 9 * ci,
@@ -93,3 +104,15 @@ for name, n_img, S, d, skv in [("attn L1 self", 32, 4096, 40, 4096), ("attn L2 s
         fn = lambda: ops.attention(qkv[:, :C], kv[:, :C], kv[:, C:], n_img, 8, S, skv, d, kv_div=16, out=out)
     us = timeit(fn)
     report(f"{name} S={S} d={d} skv={skv}", us, 4.0 * n_img * 8 * S * skv * d, 2 * n_img * S * C * 4)
+    if "torch" in __import__("os").environ.get("KB_PATHS", ""):  # vendor comparator: SDPA
+        q4 = qkv[:, :C].reshape(n_img, S, 8, d).transpose(1, 2)
+        src = qkv if skv == S else kv
+        k4 = src[: n_img * skv if skv == S else skv, C:2 * C].reshape(-1, skv, 8, d).transpose(1, 2)
+        v4 = (qkv[:, 2 * C:] if skv == S else kv[:skv, C:]).reshape(-1, skv, 8, d).transpose(1, 2)
+        if skv != S:
+            k4, v4 = k4.expand(n_img, -1, -1, -1), v4.expand(n_img, -1, -1, -1)
+        try:
+            us = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q4, k4, v4))
+            report(f"{name} S={S} d={d} skv={skv} [sdpa]", us, 4.0 * n_img * 8 * S * skv * d, 2 * n_img * S * C * 4)
+        except Exception as e:  # noqa: BLE001
+            print(f"{name} [sdpa] failed: {e}")

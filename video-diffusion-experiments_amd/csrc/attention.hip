@@ -32,17 +32,19 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int KT = 64;   // keys per tile
+int g_flash32 = 1;       // d = 40 on the 32x32x16 kernel (vd_attention_force_v1 turns it off)
 
 template <int D>
 struct AttnCfg {
   static constexpr int DQK = (D + 31) / 32 * 32;          // QK^T contraction, padded
   static constexpr int DV = (D + 15) / 16 * 16;           // PV output columns, padded
-  static constexpr int KS = DQK + 8;                      // K LDS row (elements): odd # of 16B
+  static constexpr int KS = DQK + 16;                     // K LDS row (elements): +32 B pad, conflict-free
+                                                          // b128 fragment reads (tools/lds_banks.py)
   static constexpr int VS = ((DV * 2 + 31) / 64 * 64 + 32) / 2;  // V LDS row: 32B * odd
   static constexpr int KCH = DQK / 8;                     // K 16-byte chunks per row
   static constexpr int VCH = DV / 8;
-  static constexpr int KREG = (KT * KCH + NT - 1) / NT;   // staged chunks per thread
-  static constexpr int VREG = (KT * VCH + NT - 1) / NT;
+  static constexpr int DCH = D / 8;                       // valid 16-byte chunks per K/V row
+  static constexpr int LREG = (KT * DCH + NT - 1) / NT;   // staged K (and V) chunks per thread
 };
 
 // Cross-lane max over the 4 lanes holding one query (l, l^16, l^32, l^48):
@@ -52,6 +54,43 @@ __device__ __forceinline__ float max_over_query_lanes(float x) {
   x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
   auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(t[0]), __uint_as_float(t[1]));
+}
+
+// K/V tile staging: the in-flight tile lives in one ext_vector register block
+// (4 dwords per 16-byte chunk) with compile-time element indices — arrays of
+// uint4 passed around were left as a scratch stack object by the compiler.
+template <int L>
+using stage_t = __attribute__((ext_vector_type(8 * L))) uint32_t;  // K chunks then V chunks
+
+template <int L>
+__device__ __forceinline__ stage_t<L> kv_load(const bf16_t* kb_ptr, const bf16_t* vb_ptr, int ldk,
+                                              int ldv, int t, int64_t skv, const int (&krow)[L],
+                                              const uint32_t (&kcol)[L]) {
+  const int64_t key0 = (int64_t)t * KT;
+  const bf16_t* kp = kb_ptr + key0 * ldk;
+  const bf16_t* vp = vb_ptr + key0 * ldv;
+  const int kmax = (int)(skv - 1 - key0);  // >= KT-1 except on a ragged last tile
+  stage_t<L> st;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int r = krow[i] < kmax ? krow[i] : kmax;
+    const uint4 a = *(const uint4*)(kp + (uint32_t)(r * ldk) + kcol[i]);
+    const uint4 b = *(const uint4*)(vp + (uint32_t)(r * ldv) + kcol[i]);
+    st[4 * i + 0] = a.x; st[4 * i + 1] = a.y; st[4 * i + 2] = a.z; st[4 * i + 3] = a.w;
+    st[4 * L + 4 * i + 0] = b.x; st[4 * L + 4 * i + 1] = b.y;
+    st[4 * L + 4 * i + 2] = b.z; st[4 * L + 4 * i + 3] = b.w;
+  }
+  return st;
+}
+template <int L>
+__device__ __forceinline__ void kv_store(const stage_t<L>& st, bf16_t* kl, bf16_t* vl,
+                                         const uint32_t (&ldsk)[L], const uint32_t (&ldsv)[L]) {
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    *(uint4*)(kl + ldsk[i]) = make_uint4(st[4 * i], st[4 * i + 1], st[4 * i + 2], st[4 * i + 3]);
+    *(uint4*)(vl + ldsv[i]) = make_uint4(st[4 * L + 4 * i], st[4 * L + 4 * i + 1], st[4 * L + 4 * i + 2],
+                                         st[4 * L + 4 * i + 3]);
+  }
 }
 
 template <int D, int QBLK>
@@ -91,41 +130,35 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
     }
   }
 
-  uint4 kreg[C::KREG], vreg[C::VREG];
-  auto load_kv = [&](int t) {
-    const int64_t key0 = (int64_t)t * KT;
+  // K/V tile staging: only the D/8 valid chunks of each row are loaded; the
+  // padding columns of both LDS buffers (zeros for K and V, and the 1.0 column
+  // of V when ONES) are written once here and never overwritten.  Per-thread
+  // (row, chunk) slots and their offsets are fixed for the whole kernel, so the
+  // per-tile cost is one add per load; bounds are checked only on a ragged last tile.
+  for (int idx = tid; idx < 2 * KT; idx += NT) {
+    const int buf = idx / KT, r = idx % KT;
+    for (int cc = C::DCH; cc < C::KCH; ++cc)
+      *(uint4*)(&ks_lds[buf][r * C::KS + cc * 8]) = make_uint4(0, 0, 0, 0);
+    for (int cc = C::DCH; cc < C::VCH; ++cc)
+      *(uint4*)(&vs_lds[buf][r * C::VS + cc * 8]) = make_uint4(ONES && cc == C::DCH ? 0x3F80u : 0u, 0, 0, 0);
+  }
+  // Branch-free staging: every thread loads LREG (row, chunk) slots per tile;
+  // slots past the tile's valid chunk count duplicate a valid one (same bytes to
+  // the same LDS address), and rows past the last key are clamped to it (their
+  // scores are masked to -inf, so P = 0 multiplies finite V).
+  int krow[C::LREG];
+  uint32_t kcol[C::LREG], ldsk[C::LREG], ldsv[C::LREG];
 #pragma unroll
-    for (int i = 0; i < C::KREG; ++i) {
-      const int idx = tid + i * NT;
-      const int r = idx / C::KCH, cc = idx - r * C::KCH;
-      uint4 u = make_uint4(0, 0, 0, 0);
-      if (r < KT && key0 + r < skv && cc * 8 < D) u = *(const uint4*)(kb_ptr + (key0 + r) * ldk + cc * 8);
-      kreg[i] = u;
-    }
-#pragma unroll
-    for (int i = 0; i < C::VREG; ++i) {
-      const int idx = tid + i * NT;
-      const int r = idx / C::VCH, cc = idx - r * C::VCH;
-      uint4 u = make_uint4(0, 0, 0, 0);
-      if (r < KT && key0 + r < skv && cc * 8 < D) u = *(const uint4*)(vb_ptr + (key0 + r) * ldv + cc * 8);
-      if (ONES && cc == D / 8) u.x = 0x3F80u;  // bf16 1.0 in column D
-      vreg[i] = u;
-    }
-  };
-  auto store_kv = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < C::KREG; ++i) {
-      const int idx = tid + i * NT;
-      const int r = idx / C::KCH, cc = idx - r * C::KCH;
-      if (r < KT) *(uint4*)(&ks_lds[buf][r * C::KS + cc * 8]) = kreg[i];
-    }
-#pragma unroll
-    for (int i = 0; i < C::VREG; ++i) {
-      const int idx = tid + i * NT;
-      const int r = idx / C::VCH, cc = idx - r * C::VCH;
-      if (r < KT) *(uint4*)(&vs_lds[buf][r * C::VS + cc * 8]) = vreg[i];
-    }
-  };
+  for (int i = 0; i < C::LREG; ++i) {
+    const int idx = (tid + i * NT) % (KT * C::DCH);
+    const int r = idx / C::DCH, cc = idx % C::DCH;
+    krow[i] = r;
+    kcol[i] = (uint32_t)(cc * 8);
+    ldsk[i] = (uint32_t)(r * C::KS + cc * 8);
+    ldsv[i] = (uint32_t)(r * C::VS + cc * 8);
+  }
+  const int ldk32 = (int)ldk, ldv32 = (int)ldv;
+  stage_t<C::LREG> kvst;
 
   f32x4 oacc[C::DV / 16][QBLK];
 #pragma unroll
@@ -138,14 +171,14 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
 
   const int ntiles = (int)((skv + KT - 1) / KT);
   const bool ragged = (skv % KT) != 0;
-  load_kv(0);
-  store_kv(0);
+  kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, 0, skv, krow, kcol);
+  kv_store<C::LREG>(kvst, ks_lds[0], vs_lds[0], ldsk, ldsv);
   __syncthreads();
   const int qq = fr >> 2, pp = fr & 3;  // tr-read geometry: lane 4*qq+pp -> row qq, cols 4*pp..
 
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
-    if (t + 1 < ntiles) load_kv(t + 1);
+    if (t + 1 < ntiles) kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, t + 1, skv, krow, kcol);
     const bf16_t* kl = ks_lds[buf];
     const bf16_t* vl = vs_lds[buf];
 
@@ -237,7 +270,7 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
           oacc[a][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[st][qb], oacc[a][qb], 0, 0, 0);
       }
     }
-    if (t + 1 < ntiles) store_kv(buf ^ 1);
+    if (t + 1 < ntiles) kv_store<C::LREG>(kvst, ks_lds[buf ^ 1], vs_lds[buf ^ 1], ldsk, ldsv);
     __syncthreads();
   }
 
@@ -268,12 +301,337 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
   }
 }
 
+// ============================================================ flash32
+// Small-head flash attention on v_mfma_f32_32x32x16_bf16 (d = 40: SD-1.5's
+// level-1 spatial self-attention, the hottest attention of the step).
+//
+//   S^T = K'.Q'^T   A = K rows (32 keys x 16 d, ds_read_b128), B = Q'^T from
+//                   registers; contraction over d padded to DK = 48 (3 MFMAs
+//                   per 32x32 tile instead of 4 with 16x16x32 at 64).  Column D
+//                   of K' holds 1.0 and column D of Q' holds -mu (mu = this
+//                   query's running max, bf16-representable), so the MFMA emits
+//                   u = c*s - mu directly: no per-score FMA.
+//   O^T += V^T.P^T  the S^T accumulator, packed to bf16, IS the P^T B operand
+//                   (cdna_hip_programming.md §3 "accumulator tile as the next
+//                   MFMA's operand"; permuted key order within each 16-key
+//                   step), V^T comes from ds_read_b64_tr_b16 in that order; V's
+//                   column D holds 1.0 so the same MFMA yields the row sum.
+// Deferred max (T13): while every u of the tile is <= THR, p = exp2(u) (one
+// v_exp + 1/2 v_max3 + 1/2 v_cvt_pk per score); otherwise (first tile, or a
+// row max that grew by > THR) mu is raised for those rows, the tile's u and
+// the O rows are rescaled and Q''s -mu entry is rewritten — the decision covers
+// the whole tile before any of its P is formed, so nothing is half-scaled.
+// P <= 2^THR stays exact in the fp32 O/l accumulators; P's bf16 rounding is
+// relative, so the normalised result does not depend on THR.
+// Layout: 4 waves x 64 queries (2 query blocks of 32); K/V tiles of 64 keys
+// double-buffered in ONE LDS array (K rows padded to 56 elements, V as
+// [2][64 keys][32 d] images): both the K b128 reads and the V transposed reads
+// are bank-conflict free (tools/lds_banks.py).  Register staging (T14): the
+// next tile's global loads issue before this tile's MFMAs, their LDS writes
+// after the PV, one barrier per tile.  Epilogue: permlane32_swap pairs give
+// 16-byte stores of 8 consecutive output channels.
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+template <int D>
+struct F32Cfg {
+  static_assert(D % 8 == 0 && D <= 48, "flash32: d must be a multiple of 8, <= 48");
+  static constexpr int DK = (D + 1 + 15) / 16 * 16;   // contraction incl. the -mu column
+  static constexpr int KSTEPS = DK / 16;
+  static constexpr int DVP = (D + 1 + 31) / 32 * 32;  // PV rows incl. the ones column
+  static constexpr int NDB = DVP / 32;
+  static constexpr int KS = DK + 8;                   // K LDS row (elements), conflict-free
+  static constexpr int DCH = D / 8;                   // 16-B chunks per K/V row
+  static constexpr int K_ELEMS = KT * KS;
+  static constexpr int V_ELEMS = NDB * KT * 32;
+  static constexpr int STAGE = K_ELEMS + V_ELEMS;     // elements per buffer
+  static constexpr int LREG = (KT * DCH + NT - 1) / NT;
+  // position of d = D in the Q'^T fragment (k-step, lane half, element)
+  static constexpr int MU_KS = D / 16, MU_H = (D % 16) / 8, MU_J = D % 8;
+  // position of the ones column in the O^T accumulator (d-block, lane half, register)
+  static constexpr int L_DB = D / 32, L_H = ((D % 32) / 4) & 1, L_I = (D % 4) + 4 * ((D % 32) / 8);
+};
+
+constexpr float F32_THR = 6.0f;  // deferred-max threshold (log2 units): P <= 64
+
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  // plain v_max3_f32: fmaxf would add IEEE canonicalising maxes on MFMA results
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmax2(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// max over the 32 scores a lane holds for its query in one 64-key tile
+__device__ __forceinline__ float tile_max(const f32x16& a, const f32x16& b) {
+  float m0 = vmax3(a[0], a[1], a[2]), m1 = vmax3(a[3], a[4], a[5]), m2 = vmax3(a[6], a[7], a[8]);
+  float m3 = vmax3(a[9], a[10], a[11]), m4 = vmax3(a[12], a[13], a[14]), m5 = vmax3(a[15], b[0], b[1]);
+  float m6 = vmax3(b[2], b[3], b[4]), m7 = vmax3(b[5], b[6], b[7]), m8 = vmax3(b[8], b[9], b[10]);
+  float m9 = vmax3(b[11], b[12], b[13]), m10 = vmax2(b[14], b[15]);
+  m0 = vmax3(m0, m1, m2);
+  m3 = vmax3(m3, m4, m5);
+  m6 = vmax3(m6, m7, m8);
+  m9 = vmax2(m9, m10);
+  return vmax2(vmax3(m0, m3, m6), m9);
+}
+// value of lane l ^ 32 (v_permlane32_swap)
+__device__ __forceinline__ float partner32(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  // r[0] = new vdst (lanes 32-63 <- src of lanes 0-31), r[1] = new src (lanes 0-31 <- vdst of lanes 32-63)
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
+
+template <int D>
+__global__ __launch_bounds__(NT, 2) void flash32_kernel(
+    const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
+    const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
+    int64_t sq, int64_t skv, int64_t kv_div, float c) {
+  using C = F32Cfg<D>;
+  constexpr int QB = 2;  // 32-query blocks per wave
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * C::STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int h = blockIdx.y;
+  const int64_t b = blockIdx.z;
+  const int64_t q0 = (int64_t)blockIdx.x * (4 * 32 * QB) + wave * (32 * QB);
+  const int64_t bkv = b / kv_div;
+  const bf16_t* qb_ptr = q + b * sq * ldq + (int64_t)h * D;
+  const bf16_t* kb_ptr = k + bkv * skv * ldk + (int64_t)h * D;
+  const bf16_t* vb_ptr = v + bkv * skv * ldv + (int64_t)h * D;
+
+  // Q'^T fragments: lane holds Q'[q0 + qb*32 + r32][16*ks + 8*hh .. +7], times c
+  // when c != 1 (callers that fold c into the Q projection pass c = 1 exactly).
+  const bool prescale = c != 1.0f;
+  bf16x8 qf[QB][C::KSTEPS];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    const int64_t qi = q0 + qb * 32 + r32;
+#pragma unroll
+    for (int ks = 0; ks < C::KSTEPS; ++ks) {
+      const int dd = ks * 16 + 8 * hh;
+      uint4 u = make_uint4(0, 0, 0, 0);
+      if (qi < sq && dd < D) u = *(const uint4*)(qb_ptr + qi * ldq + dd);
+      if (prescale) {
+        float f[8];
+        unpack8(u, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= c;
+        u = pack8(f);
+      }
+      qf[qb][ks] = __builtin_bit_cast(bf16x8, u);  // d = D entry starts at 0 (mu = 0)
+    }
+  }
+
+  // LDS padding, written once: K' column D = 1.0 (the -mu column), V column D =
+  // 1.0 (the row-sum column), every other padding element 0.
+  for (int idx = tid; idx < 2 * KT; idx += NT) {
+    const int buf = idx / KT, r = idx % KT;
+    bf16_t* kl = lds + buf * C::STAGE;
+    bf16_t* vl = kl + C::K_ELEMS;
+    for (int cc = C::DCH; cc < C::DK / 8; ++cc)
+      *(uint4*)(kl + r * C::KS + cc * 8) = make_uint4(cc == C::DCH ? 0x3F80u : 0u, 0, 0, 0);
+    for (int cc = C::DCH; cc < C::DVP / 8; ++cc)
+      *(uint4*)(vl + ((cc >> 2) * KT + r) * 32 + (cc & 3) * 8) = make_uint4(cc == C::DCH ? 0x3F80u : 0u, 0, 0, 0);
+  }
+  // staging slots (row, chunk) per thread, fixed for the kernel
+  int krow[C::LREG];
+  uint32_t kcol[C::LREG], ldsk[C::LREG], ldsv[C::LREG];
+#pragma unroll
+  for (int i = 0; i < C::LREG; ++i) {
+    const int idx = (tid + i * NT) % (KT * C::DCH);
+    const int r = idx / C::DCH, cc = idx % C::DCH;
+    krow[i] = r;
+    kcol[i] = (uint32_t)(cc * 8);
+    ldsk[i] = (uint32_t)(r * C::KS + cc * 8);
+    ldsv[i] = (uint32_t)(C::K_ELEMS + ((cc >> 2) * KT + r) * 32 + (cc & 3) * 8);
+  }
+  const int ldk32 = (int)ldk, ldv32 = (int)ldv;
+  stage_t<C::LREG> kvst;
+
+  f32x16 oacc[C::NDB][QB];
+#pragma unroll
+  for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[db][qb][i] = 0.f;
+  float mu[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) mu[qb] = 0.f;
+
+  const int ntiles = (int)((skv + KT - 1) / KT);
+  const bool ragged = (skv % KT) != 0;
+  kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, 0, skv, krow, kcol);
+  {
+    bf16_t* b0 = lds;
+#pragma unroll
+    for (int i = 0; i < C::LREG; ++i) {
+      *(uint4*)(b0 + ldsk[i]) = make_uint4(kvst[4 * i], kvst[4 * i + 1], kvst[4 * i + 2], kvst[4 * i + 3]);
+      *(uint4*)(b0 + ldsv[i]) = make_uint4(kvst[4 * C::LREG + 4 * i], kvst[4 * C::LREG + 4 * i + 1],
+                                           kvst[4 * C::LREG + 4 * i + 2], kvst[4 * C::LREG + 4 * i + 3]);
+    }
+  }
+  __syncthreads();
+  const int g16 = lane >> 4, i16 = lane & 15;
+  // V^T tr-read lane offset inside a [32 d] image row block (elements)
+  const int vtr = ((4 * hh + (i16 >> 2)) * 32) + 16 * (g16 & 1) + 4 * (i16 & 3);
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, t + 1, skv, krow, kcol);
+    const bf16_t* kl = lds + buf * C::STAGE;
+    const bf16_t* vl = kl + C::K_ELEMS;
+
+    // ---- u^T = K'.Q'^T  (= c*s - mu)
+    f32x16 s[2][QB];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int ks = 0; ks < C::KSTEPS; ++ks) {
+        const bf16x8 kf = *(const bf16x8*)(kl + (kb * 32 + r32) * C::KS + ks * 16 + 8 * hh);
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          if (ks == 0) {
+            f32x16 z;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) z[i] = 0.f;
+            s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][ks], z, 0, 0, 0);
+          } else {
+            s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][ks], s[kb][qb], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (ragged && t == ntiles - 1) {  // keys past skv: u = -inf (rows are clamped duplicates)
+      const int kvalid = (int)(skv - (int64_t)t * KT);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (key >= kvalid) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) s[kb][qb][i] = -INFINITY;
+          }
+        }
+    }
+    // ---- deferred max
+    float tm[QB];
+    bool need = t == 0;
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      const float m = tile_max(s[0][qb], s[1][qb]);
+      tm[qb] = vmax2(m, partner32(m));
+      need |= tm[qb] > F32_THR;
+    }
+    if (__any(need)) {  // wave-uniform: first tile or a row max moved by > THR
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const bool up = t == 0 || tm[qb] > F32_THR;
+        const float nmu = up ? (float)(__bf16)(mu[qb] + tm[qb]) : mu[qb];
+        const float delta = nmu - mu[qb];  // exact: both bf16 values
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        mu[qb] = nmu;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) s[kb][qb][i] -= delta;
+#pragma unroll
+        for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
+        if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
+      }
+    }
+    // ---- P = exp2(u), packed: registers 8*s2 .. 8*s2+7 of tile kb = k-step (kb, s2)
+    bf16x8 pf[2][2][QB];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = (__bf16)__builtin_amdgcn_exp2f(s[kb][qb][8 * s2 + j]);
+          pf[kb][s2][qb] = f;
+        }
+    // ---- O^T += V^T.P^T (key order of each step: 16*s2 + 8*(j>>2) + 4*hh + (j&3))
+#pragma unroll
+    for (int db = 0; db < C::NDB; ++db) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16_t* p0 = vl + (db * KT + kb * 32 + 16 * s2) * 32 + vtr;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (bf16x4 __attribute__((address_space(3)))*)(p0));
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (bf16x4 __attribute__((address_space(3)))*)(p0 + 8 * 32));
+          const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb)
+            oacc[db][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kb][s2][qb], oacc[db][qb], 0, 0, 0);
+        }
+      }
+    }
+    if (t + 1 < ntiles) {
+      bf16_t* nb = lds + (buf ^ 1) * C::STAGE;
+#pragma unroll
+      for (int i = 0; i < C::LREG; ++i) {
+        *(uint4*)(nb + ldsk[i]) = make_uint4(kvst[4 * i], kvst[4 * i + 1], kvst[4 * i + 2], kvst[4 * i + 3]);
+        *(uint4*)(nb + ldsv[i]) = make_uint4(kvst[4 * C::LREG + 4 * i], kvst[4 * C::LREG + 4 * i + 1],
+                                             kvst[4 * C::LREG + 4 * i + 2], kvst[4 * C::LREG + 4 * i + 3]);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: O[q][d] = O^T[d][q] / l; register i of d-block db holds
+  // d = 32*db + 8*(i>>2) + 4*hh + (i&3); swap 4-channel groups across lane halves
+  // so each lane stores 8 consecutive channels (16 B).
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    const float lown = oacc[C::L_DB][qb][C::L_I];
+    const float lp = partner32(lown);
+    const float l = hh == C::L_H ? lown : lp;
+    const float inv = __builtin_amdgcn_rcpf(l);
+    const int64_t qi = q0 + qb * 32 + r32;
+    bf16_t* orow = o + (b * sq + (qi < sq ? qi : 0)) * ldo + (int64_t)h * D;
+#pragma unroll
+    for (int db = 0; db < C::NDB; ++db) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const f32x16& a = oacc[db][qb];
+        uint32_t x0 = pack2(a[8 * m + 0] * inv, a[8 * m + 1] * inv), x1 = pack2(a[8 * m + 2] * inv, a[8 * m + 3] * inv);
+        uint32_t y0 = pack2(a[8 * m + 4] * inv, a[8 * m + 5] * inv), y1 = pack2(a[8 * m + 6] * inv, a[8 * m + 7] * inv);
+        auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+        auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+        // lanes < 32: (x, y) = channels 16m + 0..7; lanes >= 32: channels 16m + 8..15
+        const int dd = 32 * db + 16 * m + 8 * hh;
+        if (qi < sq && dd + 8 <= D) *(uint4*)(orow + dd) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+    }
+  }
+}
+
 template <int D>
 int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                  void* o, int64_t ldo, int64_t batch, int heads, int64_t sq, int64_t skv,
                  int64_t kv_div, float scale, hipStream_t s) {
   const float c = scale * 1.4426950408889634f;
-  if (sq >= 1024 && D <= 64) {
+  if constexpr (D == 40) {
+    if (g_flash32 && ((uintptr_t)o & 15) == 0 && ldo % 8 == 0) {
+      const dim3 grid((unsigned)((sq + 255) / 256), (unsigned)heads, (unsigned)batch);
+      hipLaunchKernelGGL((flash32_kernel<D>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k, ldk,
+                         (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
+      return vd_launch_status();
+    }
+  }
+  if (sq >= 1024 && D <= 40) {
     const dim3 grid((unsigned)((sq + 255) / 256), (unsigned)heads, (unsigned)batch);
     hipLaunchKernelGGL((flash_attn_kernel<D, 4>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                        (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv,
@@ -382,6 +740,12 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
+// Test/benchmark hook: route d = 40 to the 16x16x32 kernel instead of flash32.
+extern "C" int vd_attention_force_v1(int32_t on) {
+  g_flash32 = !on;
+  return VD_OK;
+}
+
 extern "C" int vd_attention(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                             int64_t ldv, void* o, int64_t ldo, int64_t batch, int32_t heads,
                             int64_t sq, int64_t skv, int32_t d, int64_t kv_div, float scale,
@@ -390,6 +754,7 @@ extern "C" int vd_attention(const void* q, int64_t ldq, const void* k, int64_t l
   VD_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0);
   VD_CHECK_ARG(batch > 0 && heads > 0 && sq > 0 && skv > 0 && kv_div > 0 && batch % kv_div == 0);
   VD_CHECK_ARG(batch <= 65535 && heads <= 65535);
+  VD_CHECK_ARG(skv * ldk < 0x7fffffff && skv * ldv < 0x7fffffff);
   hipStream_t s = (hipStream_t)stream;
   switch (d) {
     case 32: return launch_flash<32>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s);

@@ -48,7 +48,55 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
     mrow[b] = mok[b] ? m : 0;
     rbrow[b] = d.rowbias ? d.rowbias + (int64_t)(mrow[b] / (int)d.rb_div) * d.ld_rb : nullptr;
   }
+  // Wide path (T21 for the 16x16 layout): v_permlane16_swap of 16-column blocks
+  // (a, a+1) leaves each lane 8 CONSECUTIVE channels — lane group g of the pair
+  // holds columns 16a + 16(g&1) + 8(g>>1) .. +7 — so residual loads and bf16
+  // stores are 16 B and each store instruction writes 64 contiguous bytes per row
+  // (full 64-B write granules) instead of 32.
+  const bool wide = (N % 8) == 0 && !d.out_f32 && (d.ldc % 8) == 0 && (((uintptr_t)d.out) & 15) == 0 &&
+                    (!d.res || ((d.ld_res % 8) == 0 && (((uintptr_t)d.res) & 15) == 0));
+  const int wcol = 16 * (fq & 1) + 8 * (fq >> 1);  // lane's column offset inside a swapped pair
   if (d.act == VD_ACT_GEGLU) {
+    if constexpr (NB % 4 == 0) {
+      if (wide) {
+        bf16_t* out = (bf16_t*)d.out;
+#pragma unroll
+        for (int a = 0; a < NB; a += 4) {  // hidden/gate blocks (a, a+1) and (a+2, a+3)
+          const int nh0 = nw + a * 16 + 4 * fq, nh1 = nh0 + 32;
+          float bh0[4] = {0, 0, 0, 0}, bg0[4] = {0, 0, 0, 0}, bh1[4] = {0, 0, 0, 0}, bg1[4] = {0, 0, 0, 0};
+          if (d.bias) {
+            const float4 t0 = *(const float4*)(d.bias + (nh0 < N ? nh0 : 0));
+            const float4 t1 = *(const float4*)(d.bias + (nh0 + 16 < N ? nh0 + 16 : 0));
+            const float4 t2 = *(const float4*)(d.bias + (nh1 < N ? nh1 : 0));
+            const float4 t3 = *(const float4*)(d.bias + (nh1 + 16 < N ? nh1 + 16 : 0));
+            bh0[0] = t0.x; bh0[1] = t0.y; bh0[2] = t0.z; bh0[3] = t0.w;
+            bg0[0] = t1.x; bg0[1] = t1.y; bg0[2] = t1.z; bg0[3] = t1.w;
+            bh1[0] = t2.x; bh1[1] = t2.y; bh1[2] = t2.z; bh1[3] = t2.w;
+            bg1[0] = t3.x; bg1[1] = t3.y; bg1[2] = t3.z; bg1[3] = t3.w;
+          }
+          const int nout = nw / 2 + (a / 2) * 16 + wcol;
+#pragma unroll
+          for (int b = 0; b < MB; ++b) {
+            uint32_t x[2], y[2];
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+              const float o0 = (acc[a][b][2 * h2] + bh0[2 * h2]) * gelu_erf(acc[a + 1][b][2 * h2] + bg0[2 * h2]);
+              const float o1 = (acc[a][b][2 * h2 + 1] + bh0[2 * h2 + 1]) *
+                               gelu_erf(acc[a + 1][b][2 * h2 + 1] + bg0[2 * h2 + 1]);
+              const float p0 = (acc[a + 2][b][2 * h2] + bh1[2 * h2]) * gelu_erf(acc[a + 3][b][2 * h2] + bg1[2 * h2]);
+              const float p1 = (acc[a + 2][b][2 * h2 + 1] + bh1[2 * h2 + 1]) *
+                               gelu_erf(acc[a + 3][b][2 * h2 + 1] + bg1[2 * h2 + 1]);
+              auto r = __builtin_amdgcn_permlane16_swap(pack2(o0, o1), pack2(p0, p1), false, false);
+              x[h2] = r[0];
+              y[h2] = r[1];
+            }
+            if (mok[b] && 2 * nout < N)
+              *(uint4*)(out + (uint32_t)(mrow[b] * (int)d.ldc + nout)) = make_uint4(x[0], x[1], y[0], y[1]);
+          }
+        }
+        return;
+      }
+    }
     if constexpr (NB % 2 == 0) {
       bf16_t* out = (bf16_t*)d.out;
 #pragma unroll
@@ -76,8 +124,53 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
     }
     return;
   }
+  if (wide) {
+    bf16_t* out = (bf16_t*)d.out;
 #pragma unroll
-  for (int a = 0; a < NB; ++a) {
+    for (int a = 0; a + 1 < NB; a += 2) {
+      const int n = nw + a * 16 + wcol;  // first of this lane's 8 columns after the swap
+      const bool nok = n < N;
+      const int nn = nok ? n : 0;
+      float bv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (d.bias) {
+        const float4 t0 = *(const float4*)(d.bias + nn), t1 = *(const float4*)(d.bias + nn + 4);
+        bv[0] = t0.x; bv[1] = t0.y; bv[2] = t0.z; bv[3] = t0.w;
+        bv[4] = t1.x; bv[5] = t1.y; bv[6] = t1.z; bv[7] = t1.w;
+      }
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[a][b][j]), __float_as_uint(acc[a + 1][b][j]),
+                                                    false, false);
+          o[j] = __uint_as_float(r[0]) + bv[j];
+          o[4 + j] = __uint_as_float(r[1]) + bv[4 + j];
+        }
+        if (!mok[b] || !nok) continue;
+        if (d.rowbias) {
+          const float4 t0 = *(const float4*)(rbrow[b] + n), t1 = *(const float4*)(rbrow[b] + n + 4);
+          o[0] += t0.x; o[1] += t0.y; o[2] += t0.z; o[3] += t0.w;
+          o[4] += t1.x; o[5] += t1.y; o[6] += t1.z; o[7] += t1.w;
+        }
+        if (d.act == VD_ACT_SILU) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = silu_f(o[j]);
+        }
+        if (d.res) {
+          float rf[8];
+          unpack8(*(const uint4*)((const bf16_t*)d.res + (uint32_t)(mrow[b] * (int)d.ld_res + n)), rf);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += rf[j];
+        }
+        *(uint4*)(out + (uint32_t)(mrow[b] * (int)d.ldc + n)) = pack8(o);
+      }
+    }
+    if constexpr (NB % 2 == 0) return;
+  }
+#pragma unroll
+  for (int a = 0; a < NB; ++a) {  // narrow path (or, when wide, the odd last block)
+    if (wide && a + 1 < NB) continue;
     const int n = nw + a * 16 + 4 * fq;
     if (n >= N) continue;
     float bv[4] = {0, 0, 0, 0};
@@ -301,7 +394,7 @@ __device__ __forceinline__ void wait_vm() {
 template <int BN, int MODE>
 __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                          uint32_t a1_bytes, uint32_t w_bytes,
-                                                         int split, int per_wg) {
+                                                         int split) {
   using C = G2<BN>;
   __shared__ __attribute__((aligned(1024))) char smem[G2_STAGES * C::STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -311,12 +404,17 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
   const int tiles_n = (int)((N + BN - 1) / BN);
   const int tiles_m = (int)((M + G2_BM - 1) / G2_BM);
   const int units = tiles_n * tiles_m * split;
-  // Persistent: this workgroup owns the contiguous unit range [u_begin, u_end);
-  // a unit is (output tile, split-K slice), slices adjacent.  XCD-aware so the
-  // workgroups sharing an L2 walk neighbouring tiles.
+  // Persistent, strided: this workgroup owns units lid, lid + G, lid + 2G, ...
+  // (G = gridDim.x <= #CUs, all resident).  A unit is (output tile, split-K
+  // slice), tiles N-fastest.  lid is XCD-contiguous (xcd_remap), so at every
+  // round the ~32 workgroups of one XCD run ~32 CONSECUTIVE units — the N-tiles
+  // of the same few A row-panels — and each A panel comes from HBM once and is
+  // shared through that XCD's L2 (a contiguous per-workgroup range instead puts
+  // 32 different panels in flight per XCD, thrashes L2 and re-reads A from HBM
+  // once per N-tile).
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int u_begin = lid * per_wg;
-  const int u_end = u_begin + per_wg < units ? u_begin + per_wg : units;
+  const int G = gridDim.x;
+  const int u_begin = lid;
   const int nk_all = (int)(K / BK);
 
   const int rb = lane >> 3;                                  // row within the 8-row DMA block
@@ -415,7 +513,7 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
 #pragma unroll
     for (int j = 0; j < C::NBMAX; ++j)
       if (j < nbw) dma16(rw, lb + (j * 8 + wid) * 1024, boff[j] + (uint32_t)kb * 2);
-    if (++ikt == ikt1 && ++iu < u_end) setup_unit(iu);
+    if (++ikt == ikt1 && (iu += G) < units) setup_unit(iu);
   };
 
   f32x4 acc[C::NB][C::MB];
@@ -426,7 +524,7 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
 
   // total k-tiles this workgroup streams
   int n_it = 0;
-  for (int u = u_begin; u < u_end; ++u) {
+  for (int u = u_begin; u < units; u += G) {
     int a0_, a1_;
     unit_kr(u, a0_, a1_);
     n_it += a1_ - a0_;
@@ -499,7 +597,7 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
       for (int a = 0; a < C::NB; ++a)
 #pragma unroll
         for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (++cu < u_end) unit_kr(cu, ckt, ckt1);
+      if ((cu += G) < units) unit_kr(cu, ckt, ckt1);
     }
     if (it + 2 < n_it) issue(stage == 0 ? 2 : stage - 1);
     stage = stage == 2 ? 0 : stage + 1;
@@ -565,14 +663,15 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
 template <int BN>
 int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
   const int64_t units = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + BN - 1) / BN) * split;
-  const int64_t per = (units + g_num_cus - 1) / g_num_cus;   // persistent: one workgroup per CU
-  const int64_t grid = (units + per - 1) / per;
+  // persistent: one workgroup per CU, ceil(units / grid) rounds, balanced grid
+  const int64_t rounds = (units + g_num_cus - 1) / g_num_cus;
+  const int64_t grid = (units + rounds - 1) / rounds;
   if (d.a_mode == VD_A_CONV3X3)
     hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb,
-                       split, (int)per);
+                       split);
   else
     hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb,
-                       split, (int)per);
+                       split);
   int rc = vd_launch_status();
   if (rc != VD_OK || split == 1) return rc;
   const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
