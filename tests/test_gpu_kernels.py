@@ -352,7 +352,11 @@ def test_flash_attention_deferred_max(attn_path, kind):
     sq, skv, d = q.shape[0], k.shape[0], q.shape[1]
     got = ops.attention(q, k, v, 1, 1, sq, skv, d)
     assert torch.isfinite(got.float()).all()
-    close_bf16(got, sdpa_ref(q, k, v, 1, 1, sq, skv, d))
+    # O is a convex combination of V rows and P is rounded to bf16 (relative 2^-9) before
+    # PV, so the absolute error scales with |V|, not |O| (these cases concentrate the
+    # weights on a few keys and |O| << |V|); a mis-scaled tile shows up as errors >= 0.1.
+    close_bf16(got, sdpa_ref(q, k, v, 1, 1, sq, skv, d), abs_frac=2e-3 * v.float().abs().max().item()
+               / sdpa_ref(q, k, v, 1, 1, sq, skv, d).abs().max().item())
 
 
 def test_flash_attention_unit_scale(cuda):

@@ -2,6 +2,7 @@
 
 python tools/kbench.py [filter]  -> one line per shape: us, TFLOP/s, effective GB/s
 """
+import math
 import sys
 from pathlib import Path
 
@@ -42,6 +43,7 @@ cases = []
 for lvl, (hw, C) in enumerate([(4096, 320), (1024, 640), (256, 1280), (64, 1280)]):
     M = 32 * hw
     cases += [(f"L{lvl+1} dense proj   M={M} N={C} K={C} +res", "dense", M, C, C, True),
+              (f"L{lvl+1} dense proj   M={M} N={C} K={C} nores", "dense", M, C, C, False),
               (f"L{lvl+1} dense qkv    M={M} N={3*C} K={C}", "dense", M, 3 * C, C, False),
               (f"L{lvl+1} dense ff2    M={M} N={C} K={4*C} +res", "dense", M, C, 4 * C, True),
               (f"L{lvl+1} geglu        M={M} N={8*C} K={C}", "geglu", M, 8 * C, C, False)]
@@ -104,6 +106,10 @@ for name, n_img, S, d, skv in [("attn L1 self", 32, 4096, 40, 4096), ("attn L2 s
         fn = lambda: ops.attention(qkv[:, :C], kv[:, :C], kv[:, C:], n_img, 8, S, skv, d, kv_div=16, out=out)
     us = timeit(fn)
     report(f"{name} S={S} d={d} skv={skv}", us, 4.0 * n_img * 8 * S * skv * d, 2 * n_img * S * C * 4)
+    if skv == S:  # the model path: softmax scale folded into the Q projection (c == 1)
+        us = timeit(lambda: ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], n_img, 8, S, S, d, out=out,
+                                          scale=1.0 / math.log2(math.e)))
+        report(f"{name} S={S} d={d} skv={skv} [unit c]", us, 4.0 * n_img * 8 * S * skv * d, 2 * n_img * S * C * 4)
     if "torch" in __import__("os").environ.get("KB_PATHS", ""):  # vendor comparator: SDPA
         q4 = qkv[:, :C].reshape(n_img, S, 8, d).transpose(1, 2)
         src = qkv if skv == S else kv
@@ -116,3 +122,12 @@ for name, n_img, S, d, skv in [("attn L1 self", 32, 4096, 40, 4096), ("attn L2 s
             report(f"{name} S={S} d={d} skv={skv} [sdpa]", us, 4.0 * n_img * 8 * S * skv * d, 2 * n_img * S * C * 4)
         except Exception as e:  # noqa: BLE001
             print(f"{name} [sdpa] failed: {e}")
+
+for name, hw, d in [("temporal L1", 4096, 40), ("temporal L2", 1024, 80), ("temporal L3", 256, 160)]:
+    if flt not in name:
+        continue
+    C, F_, B = 8 * d, 16, 2
+    qkv = rnd(B * F_ * hw, 3 * C, std=1.5)
+    out = torch.empty(B * F_ * hw, C, device=dev, dtype=torch.bfloat16)
+    us = timeit(lambda: ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, F_, hw, 8, d, out=out))
+    report(f"{name} F=16 pos={hw} d={d}", us, 4.0 * B * hw * 8 * F_ * F_ * d, 2 * B * F_ * hw * C * 4)

@@ -310,7 +310,10 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
 //                   per 32x32 tile instead of 4 with 16x16x32 at 64).  Column D
 //                   of K' holds 1.0 and column D of Q' holds -mu (mu = this
 //                   query's running max, bf16-representable), so the MFMA emits
-//                   u = c*s - mu directly: no per-score FMA.
+//                   x = s - mu directly.  When the caller folded the softmax
+//                   scale and log2(e) into its Q projection (c == 1, the model
+//                   path: vdiff Attention.prepare) p = exp2(x) needs no per-score
+//                   FMA; otherwise p = exp2(c*x) (one multiply).
 //   O^T += V^T.P^T  the S^T accumulator, packed to bf16, IS the P^T B operand
 //                   (cdna_hip_programming.md §3 "accumulator tile as the next
 //                   MFMA's operand"; permuted key order within each 16-key
@@ -383,7 +386,7 @@ __device__ __forceinline__ float partner32(float x) {
   return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
 }
 
-template <int D>
+template <int D, bool UNITC>
 __global__ __launch_bounds__(NT, 2) void flash32_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
@@ -394,17 +397,24 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
-  const int h = blockIdx.y;
-  const int64_t b = blockIdx.z;
-  const int64_t q0 = (int64_t)blockIdx.x * (4 * 32 * QB) + wave * (32 * QB);
+  // 1-D grid, XCD-aware (T1): the query blocks of one (image, head) get
+  // consecutive logical ids and xcd_remap keeps consecutive ids on one XCD, so
+  // that head's K/V is fetched into one L2 instead of eight.
+  const int nqb = (int)((sq + 4 * 32 * QB - 1) / (4 * 32 * QB));
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qblk = lid % nqb;
+  const int h = (lid / nqb) % heads;
+  const int64_t b = (lid / nqb) / heads;
+  const int64_t q0 = (int64_t)qblk * (4 * 32 * QB) + wave * (32 * QB);
   const int64_t bkv = b / kv_div;
   const bf16_t* qb_ptr = q + b * sq * ldq + (int64_t)h * D;
   const bf16_t* kb_ptr = k + bkv * skv * ldk + (int64_t)h * D;
   const bf16_t* vb_ptr = v + bkv * skv * ldv + (int64_t)h * D;
 
-  // Q'^T fragments: lane holds Q'[q0 + qb*32 + r32][16*ks + 8*hh .. +7], times c
-  // when c != 1 (callers that fold c into the Q projection pass c = 1 exactly).
-  const bool prescale = c != 1.0f;
+  // Q'^T fragments: lane holds Q'[q0 + qb*32 + r32][16*ks + 8*hh .. +7].  Q is
+  // used as given (no bf16 prescale: that second rounding costs ~0.4% in P); with
+  // UNITC the caller folded c into its Q projection (c == 1 exactly) and mu lives
+  // in log2 units, otherwise mu is in raw score units and p = exp2(c * x).
   bf16x8 qf[QB][C::KSTEPS];
 #pragma unroll
   for (int qb = 0; qb < QB; ++qb) {
@@ -414,13 +424,6 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
       const int dd = ks * 16 + 8 * hh;
       uint4 u = make_uint4(0, 0, 0, 0);
       if (qi < sq && dd < D) u = *(const uint4*)(qb_ptr + qi * ldq + dd);
-      if (prescale) {
-        float f[8];
-        unpack8(u, f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] *= c;
-        u = pack8(f);
-      }
       qf[qb][ks] = __builtin_bit_cast(bf16x8, u);  // d = D entry starts at 0 (mu = 0)
     }
   }
@@ -485,13 +488,20 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
     const bf16_t* kl = lds + buf * C::STAGE;
     const bf16_t* vl = kl + C::K_ELEMS;
 
-    // ---- u^T = K'.Q'^T  (= c*s - mu)
+    // ---- x^T = K'.Q'^T  (= s - mu)
     f32x16 s[2][QB];
+    bf16x8 kfr[2][C::KSTEPS];  // all K fragments of the tile first: one LDS latency, not six
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < C::KSTEPS; ++ks)
+        kfr[kb][ks] = *(const bf16x8*)(kl + (kb * 32 + r32) * C::KS + ks * 16 + 8 * hh);
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them to their MFMAs)
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
       for (int ks = 0; ks < C::KSTEPS; ++ks) {
-        const bf16x8 kf = *(const bf16x8*)(kl + (kb * 32 + r32) * C::KS + ks * 16 + 8 * hh);
+        const bf16x8 kf = kfr[kb][ks];
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb) {
           if (ks == 0) {
@@ -518,6 +528,23 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
           }
         }
     }
+    // V^T fragments for this tile's PV, issued now so their LDS latency hides
+    // under the softmax VALU work (key order of each step: 16*s2 + 8*(j>>2) + 4*hh + (j&3))
+    bf16x8 vfr[C::NDB][2][2];
+#pragma unroll
+    for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16_t* p0 = vl + (db * KT + kb * 32 + 16 * s2) * 32 + vtr;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (bf16x4 __attribute__((address_space(3)))*)(p0));
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (bf16x4 __attribute__((address_space(3)))*)(p0 + 8 * 32));
+          vfr[db][kb][s2] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+    __builtin_amdgcn_sched_barrier(0);
     // ---- deferred max
     float tm[QB];
     bool need = t == 0;
@@ -525,15 +552,15 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
     for (int qb = 0; qb < QB; ++qb) {
       const float m = tile_max(s[0][qb], s[1][qb]);
       tm[qb] = vmax2(m, partner32(m));
-      need |= tm[qb] > F32_THR;
+      need |= (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
     }
     if (__any(need)) {  // wave-uniform: first tile or a row max moved by > THR
 #pragma unroll
       for (int qb = 0; qb < QB; ++qb) {
-        const bool up = t == 0 || tm[qb] > F32_THR;
+        const bool up = t == 0 || (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
         const float nmu = up ? (float)(__bf16)(mu[qb] + tm[qb]) : mu[qb];
         const float delta = nmu - mu[qb];  // exact: both bf16 values
-        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
         mu[qb] = nmu;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
@@ -556,28 +583,21 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
         for (int s2 = 0; s2 < 2; ++s2) {
           bf16x8 f;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = (__bf16)__builtin_amdgcn_exp2f(s[kb][qb][8 * s2 + j]);
+          for (int j = 0; j < 8; ++j)
+            f[j] = (__bf16)__builtin_amdgcn_exp2f(UNITC ? s[kb][qb][8 * s2 + j] : s[kb][qb][8 * s2 + j] * c);
           pf[kb][s2][qb] = f;
         }
-    // ---- O^T += V^T.P^T (key order of each step: 16*s2 + 8*(j>>2) + 4*hh + (j&3))
+    // ---- O^T += V^T.P^T
 #pragma unroll
-    for (int db = 0; db < C::NDB; ++db) {
+    for (int db = 0; db < C::NDB; ++db)
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16_t* p0 = vl + (db * KT + kb * 32 + 16 * s2) * 32 + vtr;
-          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-              (bf16x4 __attribute__((address_space(3)))*)(p0));
-          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-              (bf16x4 __attribute__((address_space(3)))*)(p0 + 8 * 32));
-          const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
           for (int qb = 0; qb < QB; ++qb)
-            oacc[db][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kb][s2][qb], oacc[db][qb], 0, 0, 0);
-        }
-      }
-    }
+            oacc[db][qb] =
+                __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[db][kb][s2], pf[kb][s2][qb], oacc[db][qb], 0, 0, 0);
     if (t + 1 < ntiles) {
       bf16_t* nb = lds + (buf ^ 1) * C::STAGE;
 #pragma unroll
@@ -625,9 +645,15 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
   const float c = scale * 1.4426950408889634f;
   if constexpr (D == 40) {
     if (g_flash32 && ((uintptr_t)o & 15) == 0 && ldo % 8 == 0) {
-      const dim3 grid((unsigned)((sq + 255) / 256), (unsigned)heads, (unsigned)batch);
-      hipLaunchKernelGGL((flash32_kernel<D>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k, ldk,
-                         (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
+      const int64_t nblk = (sq + 255) / 256 * heads * batch;
+      if (nblk > 0x7fffffff) return VD_EINVAL;
+      const dim3 grid((unsigned)nblk);
+      if (c == 1.0f)
+        hipLaunchKernelGGL((flash32_kernel<D, true>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
+      else
+        hipLaunchKernelGGL((flash32_kernel<D, false>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
       return vd_launch_status();
     }
   }

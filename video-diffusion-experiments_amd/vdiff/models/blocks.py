@@ -107,7 +107,8 @@ class BasicTransformerBlock(nn.Module):
         d = self.dim_head
         n = ops.layer_norm(h, *self._norm1)
         qkv = ops.gemm(n, self.attn1._wqkv)
-        a = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], n_img, self.heads, hw, hw, d)
+        a = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], n_img, self.heads, hw, hw, d,
+                          scale=self.attn1.attn_scale)
         h = ops.gemm(a, self.attn1._wo, bias=self.attn1._bo, res=h)
         n = ops.layer_norm(h, *self._norm2)
         q = ops.gemm(n, self.attn2._wq)
@@ -117,7 +118,7 @@ class BasicTransformerBlock(nn.Module):
             if ctx.kv_cache is not None:
                 ctx.kv_cache[id(self.attn2)] = kv
         a = ops.attention(q, kv[:, :C], kv[:, C:], n_img, self.heads, hw, ctx.ctx_len, d,
-                          kv_div=ctx.frames)
+                          kv_div=ctx.frames, scale=self.attn2.attn_scale)
         h = ops.gemm(a, self.attn2._wo, bias=self.attn2._bo, res=h)
         n = ops.layer_norm(h, *self._norm3)
         return self.ff.forward_rows(n, h)
@@ -130,7 +131,7 @@ class BasicTransformerBlock(nn.Module):
             n = ops.layer_norm(h, *nrm, pe=self._pe, pe_div=positions, pe_period=frames)
             qkv = ops.gemm(n, attn._wqkv)
             a = ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch, frames,
-                                       positions, self.heads, d)
+                                       positions, self.heads, d, scale=attn.attn_scale)
             h = ops.gemm(a, attn._wo, bias=attn._bo, res=h)
         n = ops.layer_norm(h, *self._norm3)
         return self.ff.forward_rows(n, h)

@@ -134,12 +134,20 @@ class Attention(nn.Module):
         self.to_v = nn.Linear(kv_dim, inner, bias=False)
         self.to_out = nn.ModuleList([nn.Linear(inner, query_dim), nn.Dropout(0.0)])
 
+    # The softmax scale dim_head^-0.5 (and the log2(e) of the kernels' exp2) is
+    # folded into the packed to_q rows: the projection GEMM rounds c*q to bf16 ONCE
+    # and the attention kernels run with c = scale*log2(e) == 1 exactly (their
+    # exp-only path).  `attn_scale` is the scale to hand them.
+    attn_scale = 1.0 / math.log2(math.e)
+
     def prepare(self):
+        c = self.dim_head ** -0.5 * math.log2(math.e)
+        wq = self.to_q.weight.float() * c
         if self.is_cross:
-            self._wq = bf(self.to_q.weight)
+            self._wq = bf(wq)
             self._wkv = bf(torch.cat([self.to_k.weight, self.to_v.weight], 0))
         else:
-            self._wqkv = bf(torch.cat([self.to_q.weight, self.to_k.weight, self.to_v.weight], 0))
+            self._wqkv = bf(torch.cat([wq, self.to_k.weight.float(), self.to_v.weight.float()], 0))
         self._wo, self._bo = bf(self.to_out[0].weight), f32(self.to_out[0].bias)
 
     def project_kv(self, ctx_rows):
