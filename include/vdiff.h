@@ -90,6 +90,10 @@ int64_t vd_gemm_ws_bytes(const vd_gemm_desc* d);
 /* Test/benchmark hook: on != 0 forces the register-staged v1 GEMM path for every
  * shape (default: the LDS-DMA v2 path wherever it applies). */
 int vd_gemm_force_v1(int32_t on);
+/* Test/benchmark hook: 0 = automatic (default), 1 = v1 (register-staged, any shape),
+ * 2 = v2 (256 x {128,160} persistent LDS-DMA), 3 = v3 (256 x 256 8-phase, dense A only;
+ * shapes it cannot take fall back to the automatic choice). */
+int vd_gemm_select_path(int32_t path);
 
 /* ---------------------------------------------------------------- GroupNorm
  * torch GroupNorm over NHWC rows, for ResnetBlock2D.norm1/2 (eps 1e-5, +SiLU),

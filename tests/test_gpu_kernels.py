@@ -98,12 +98,13 @@ def test_gemm_geglu(cuda):
 
 
 # ---------------------------------------------------------------- v2 (LDS-DMA) paths
-@pytest.fixture(params=["v2", "v1"])
+@pytest.fixture(params=["v3", "v2", "v1"])
 def gemm_path(request, cuda):
+    """Force one GEMM kernel (v3 only takes dense A; other shapes fall back to auto)."""
     from vdiff._lib import lib
-    lib().vd_gemm_force_v1(int(request.param == "v1"))
+    lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3}[request.param])
     yield request.param
-    lib().vd_gemm_force_v1(0)
+    lib().vd_gemm_select_path(0)
 
 
 def test_gemm_large_dense(gemm_path):
@@ -120,6 +121,26 @@ def test_gemm_large_dense(gemm_path):
     close_bf16(got, want)
     got = ops.gemm(a1, w[:, :384].contiguous(), bias=b, out_f32=True)
     close_f32(got, a1.float() @ w[:, :384].float().T + b, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K,k0", [(256, 256, 64, 64), (300, 512, 128, 64), (513, 1000, 192, 192),
+                                      (2048, 1280, 2560, 2560), (8192, 768, 640, 320), (1024, 256, 5120, 5120)])
+def test_gemm_v3_shapes(cuda, M, N, K, k0):
+    """v3 pipeline edges: 1-3 K-tiles (prologue / drain), ragged M and N, the a0|a1 channel
+    concat split at k0, few tiles (split-K), bias + residual epilogue."""
+    from vdiff._lib import lib
+    lib().vd_gemm_select_path(3)
+    try:
+        a = rnd(M, k0)
+        a1 = rnd(M, K - k0) if K > k0 else None
+        w = rnd(N, K, std=K ** -0.5)
+        b = torch.randn(N, device=cuda)
+        res = rnd(M, N)
+        got = ops.gemm(a, w, a1=a1, bias=b, res=res)
+        x = a if a1 is None else torch.cat([a, a1], 1)
+        close_bf16(got, x.float() @ w.float().T + b + res.float())
+    finally:
+        lib().vd_gemm_select_path(0)
 
 
 def test_gemm_large_geglu(gemm_path):

@@ -47,6 +47,8 @@ for lvl, (hw, C) in enumerate([(4096, 320), (1024, 640), (256, 1280), (64, 1280)
               (f"L{lvl+1} dense qkv    M={M} N={3*C} K={C}", "dense", M, 3 * C, C, False),
               (f"L{lvl+1} dense ff2    M={M} N={C} K={4*C} +res", "dense", M, C, 4 * C, True),
               (f"L{lvl+1} geglu        M={M} N={8*C} K={C}", "geglu", M, 8 * C, C, False)]
+cases += [("big 4096^3", "dense", 4096, 4096, 4096, False), ("big 8192^3", "dense", 8192, 8192, 8192, False),
+          ("big M=32768 N=4096 K=1280", "dense", 32768, 4096, 1280, False)]
 convs = [("L1 conv 320->320", 32, 64, 320, 320), ("L2 conv 640->640", 32, 32, 640, 640),
          ("L3 conv 1280->1280", 32, 16, 1280, 1280), ("L4 conv 1280->1280", 32, 8, 1280, 1280),
          ("L4 conv 2560->1280", 32, 8, 2560, 1280), ("L1 conv 640->320", 32, 64, 640, 320)]
@@ -63,14 +65,14 @@ for name, kind, M, N, K, res in cases:
             us = timeit(lambda: torch.nn.functional.linear(a, w))
             report(f"{name} [hipblaslt]", us, 2.0 * M * N * K, 2 * (M * K + N * K + M * N))
             continue
-        lib().vd_gemm_force_v1(int(path == "v1"))
+        lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3}[path])
         act = ops.ACT_GEGLU if kind == "geglu" else ops.ACT_NONE
         nout = N // 2 if kind == "geglu" else N
         out = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
         us = timeit(lambda: ops.gemm(a, w, bias=b, res=r, act=act, out=out))
         byts = 2 * (M * K + N * K + M * nout + (M * N if res else 0))
         report(f"{name} [{path}]", us, 2.0 * M * N * K, byts)
-    lib().vd_gemm_force_v1(0)
+    lib().vd_gemm_select_path(0)
 
 for name, n, hw, ci, co in convs:
     if flt not in name:
@@ -86,11 +88,11 @@ for name, n, hw, ci, co in convs:
             report(f"{name} M={n*hw*hw} K={9*ci} [miopen]", us, 2.0 * n * hw * hw * co * 9 * ci,
                    2 * (n * hw * hw * (ci + co) + co * 9 * ci))
             continue
-        lib().vd_gemm_force_v1(int(path == "v1"))
+        lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3}[path])
         us = timeit(lambda: ops.conv3x3(x, n, hw, hw, w, out=out))
         report(f"{name} M={n*hw*hw} K={9*ci} [{path}]", us, 2.0 * n * hw * hw * co * 9 * ci,
                2 * (n * hw * hw * (ci + co) + co * 9 * ci))
-    lib().vd_gemm_force_v1(0)
+    lib().vd_gemm_select_path(0)
 
 for name, n_img, S, d, skv in [("attn L1 self", 32, 4096, 40, 4096), ("attn L2 self", 32, 1024, 80, 1024),
                                ("attn L3 self", 32, 256, 160, 256), ("attn L1 cross", 32, 4096, 40, 77)]:

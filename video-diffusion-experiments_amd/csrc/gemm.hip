@@ -30,20 +30,20 @@ __device__ __forceinline__ int lds_off(int row, int chunk) {
   return row * BK + ((chunk ^ (row & 7)) << 3);
 }
 
-template <int BM, int BN, int MB, int NB>
-__device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], int64_t m0,
-                                              int64_t n0, int wm, int wn, int lane) {
-  // acc[a][b][j] = C[m = m0 + wm*MB*16 + b*16 + fr][n = n0 + wn*BN/2 + a*16 + 4*fq + j]
+template <int MB, int NB>
+__device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], int mbase,
+                                              int nbase, int lane) {
+  // acc[a][b][j] = C[m = mbase + b*16 + fr][n = nbase + a*16 + 4*fq + j]  (the wave's sub-tile)
   // All offsets fit 32 bits (M*ldc < 2^31 is checked on the host).
   const int M = (int)d.M, N = (int)d.N;
   const int fr = lane & 15, fq = lane >> 4;
-  const int nw = (int)n0 + wn * (BN / 2);
+  const int nw = nbase;
   int mrow[MB];
   bool mok[MB];
   const float* rbrow[MB];
 #pragma unroll
   for (int b = 0; b < MB; ++b) {
-    const int m = (int)m0 + wm * MB * 16 + b * 16 + fr;
+    const int m = mbase + b * 16 + fr;
     mok[b] = m < M;
     mrow[b] = mok[b] ? m : 0;
     rbrow[b] = d.rowbias ? d.rowbias + (int64_t)(mrow[b] / (int)d.rb_div) * d.ld_rb : nullptr;
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
     __syncthreads();
   }
 
-  gemm_epilogue<BM, BN, MB, NB>(d, acc, m0, n0, wm, wn, lane);
+  gemm_epilogue<MB, NB>(d, acc, (int)m0 + wm * MB * 16, (int)n0 + wn * (BN / 2), lane);
 }
 
 // ============================================================================ v2
@@ -388,6 +388,7 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
@@ -578,7 +579,7 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
       const int tile = cu / split, sp = cu % split;
       const int64_t m0 = (int64_t)(tile / tiles_n) * G2_BM, n0 = (int64_t)(tile % tiles_n) * BN;
       if (split == 1) {
-        gemm_epilogue<G2_BM, BN, C::MB, C::NB>(d, acc, m0, n0, wm, wn, lane);
+        gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::MB * 16, (int)n0 + wn * (BN / 2), lane);
       } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
         float* slab = (float*)d.ws + (int64_t)sp * M * N;
 #pragma unroll
@@ -601,6 +602,193 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     }
     if (it + 2 < n_it) issue(stage == 0 ? 2 : stage - 1);
     stage = stage == 2 ? 0 : stage + 1;
+  }
+}
+
+// ============================================================================ v3
+// 256x256 tile, 8 waves as 2(M) x 4(N) (128 x 64 per wave: 0.375 LDS fragment
+// reads per MFMA vs 0.45 for v2's 64 x 80), after the 8-phase template of
+// cdna_hip_programming.md §5 "The 256² 8-phase template":
+//  * a K-tile (BK = 64) is 4 phases, each one quadrant of the wave's C
+//    (64 m x 32 n x K 64 = 16 MFMAs): Q(x0,w0) Q(x0,w1) Q(x1,w1) Q(x1,w0), so
+//    the phases read 12 / 4 / 8 / 0 fragments (W0+X0, W1, X1, -);
+//  * each K-tile's operands are four 16-KiB parts — X0 = A rows with
+//    (r & 127) < 64, X1 the other A rows, W0 = W rows with (n & 63) < 32, W1 the
+//    rest — one part DMA'd (buffer_load ... lds, 2 instructions per wave) per
+//    phase, 6-7 phases before its first read, into the stage of the K-tile two
+//    back (2 x 64 KiB); every part is restaged >= 1 phase after its last read
+//    (lgkmcnt(0) retired the reads before the phase's MFMAs) and waited for by
+//    a uniform counted vmcnt(10) (5 parts in flight) before the barrier ahead of
+//    its first read;
+//  * phase = [ds_reads | DMA | vmcnt] barrier lgkmcnt(0) setprio(1) MFMAs
+//    setprio(0) barrier, and the wr = 1 wave group runs ONE BARRIER BEHIND the
+//    wr = 0 group: on every SIMD (one wave of each group) one wave issues MFMAs
+//    while the other reads LDS and issues DMA (ping-pong);
+//  * the A (X) parts a wave group reads are DMA'd by that group only, so the
+//    stagger never lets one group overwrite rows the other has yet to read; the
+//    W parts, read by both groups, are restaged >= 2 phases after their reads.
+// Non-persistent (one output tile, or one split-K slice of it, per workgroup),
+// XCD-aware order with the N tiles of an A row-panel adjacent.
+constexpr int G3_BM = 256, G3_BN = 256, G3_NT = 512;
+constexpr int G3_A_BYTES = G3_BM * BK * 2;     // 32 KiB
+constexpr int G3_STAGE = 2 * G3_A_BYTES;       // A + W: 64 KiB
+
+template <int MODE>
+__global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
+                                                         uint32_t a1_bytes, uint32_t w_bytes, int split) {
+  static_assert(MODE == VD_A_DENSE, "gemm3: dense A only");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * G3_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int64_t M = d.M, N = d.N, K = d.K;
+  const int tiles_n = (int)((N + G3_BN - 1) / G3_BN);
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = lid / split, sp = lid % split;
+  const int64_t m0 = (int64_t)(tile / tiles_n) * G3_BM, n0 = (int64_t)(tile % tiles_n) * G3_BN;
+  const int nk_all = (int)(K / BK);
+  const int kt0 = (int)((int64_t)nk_all * sp / split), kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
+  const int nk = kt1 - kt0;
+
+  const int rb = lane >> 3;
+  const uint32_t lc16 = (uint32_t)(((lane & 7) ^ rb) * 16);
+  const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)d.a0, 0, a0_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ra1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(d.a1 ? d.a1 : d.a0), 0, d.a1 ? a1_bytes : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, w_bytes, 0x00020000);
+
+  // DMA slots (wave-uniform LDS bases, per-lane source offsets): X part q, slot j covers
+  // A rows 128*wr + 64*q + 8*(2*wc + j) + 0..7; W part q, slot j covers W rows
+  // 64*c + 32*q + rr + 0..7 with (c, rr) from g = 2*wid + j.
+  uint32_t xsrc0[2][2], xsrc1[2][2], xdst[2][2], wsrc[2][2], wdst[2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int xr = 128 * wr + 64 * q + 8 * (2 * wc + j);
+      xdst[q][j] = (uint32_t)(xr * 128);
+      int64_t m = m0 + xr + rb;
+      m = m < M ? m : M - 1;
+      xsrc0[q][j] = (uint32_t)(m * d.lda0 * 2) + lc16;
+      xsrc1[q][j] = (uint32_t)(m * d.lda1 * 2) + lc16;
+      const int g = 2 * wid + j;
+      const int wrow = 64 * (g >> 2) + 32 * q + 8 * (g & 3);
+      wdst[q][j] = (uint32_t)(G3_A_BYTES + wrow * 128);
+      int64_t n = n0 + wrow + rb;
+      n = n < N ? n : N - 1;
+      wsrc[q][j] = (uint32_t)(n * d.ldw * 2) + lc16;
+    }
+  auto dma_x = [&](int q, int tk) {  // X part q of local K-tile tk
+    char* st = smem + (tk & 1) * G3_STAGE;
+    const int kb = (kt0 + tk) * BK;
+    const bool s0 = kb < d.k0;
+    const uint32_t koff = (uint32_t)(s0 ? kb : kb - (int)d.k0) * 2;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16(s0 ? ra0 : ra1, st + xdst[q][j], (s0 ? xsrc0[q][j] : xsrc1[q][j]) + koff);
+  };
+  auto dma_w = [&](int q, int tk) {
+    char* st = smem + (tk & 1) * G3_STAGE;
+    const uint32_t koff = (uint32_t)((kt0 + tk) * BK) * 2;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16(rw, st + wdst[q][j], wsrc[q][j] + koff);
+  };
+
+  // fragment LDS offsets (bytes within a stage): rows differ by multiples of 16
+  // between the blocks of one operand, so the (row & 7) XOR is shared
+  const int fr = lane & 15, fq = lane >> 4;
+  uint32_t xl[2][2], wl[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      xl[h][ks] = 2 * lds_off(128 * wr + 64 * h + fr, ks * 4 + fq);
+      wl[h][ks] = G3_A_BYTES + 2 * lds_off(64 * wc + 32 * h + fr, ks * 4 + fq);
+    }
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- prologue: K-tile 0 complete, K-tile 1's X0/W0/W1 in flight
+  if (nk > 0) {
+    dma_x(0, 0); dma_w(0, 0); dma_w(1, 0); dma_x(1, 0);
+    if (nk > 1) {
+      dma_x(0, 1); dma_w(0, 1); dma_w(1, 1);
+      wait_vm<10>();
+    } else {
+      wait_vm<0>();
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger
+
+  bf16x8 w0f[2][2], w1f[2][2], xf[4][2];
+  for (int t = 0; t < nk; ++t) {
+    const char* st = smem + (t & 1) * G3_STAGE;
+    const bool deep = t + 2 < nk;
+#define G3_SYNC_MFMA(H, G, WF)                                                                     \
+    if (deep) wait_vm<10>(); else wait_vm<0>();                                                     \
+    __builtin_amdgcn_s_barrier();                                                                   \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                              \
+    __builtin_amdgcn_s_setprio(1);                                                                  \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                \
+      _Pragma("unroll") for (int a = 0; a < 2; ++a)                                                 \
+        _Pragma("unroll") for (int b = 0; b < 4; ++b)                                               \
+          acc[2 * (G) + a][4 * (H) + b] =                                                           \
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(WF[a][ks], xf[b][ks], acc[2 * (G) + a][4 * (H) + b], 0, 0, 0); \
+    __builtin_amdgcn_s_setprio(0);                                                                  \
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 0: read W0, X0; DMA X1 of t+1; Q(x0, w0)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) w0f[a][ks] = *(const bf16x8*)(st + wl[0][ks] + a * 16 * BK * 2);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) xf[b][ks] = *(const bf16x8*)(st + xl[0][ks] + b * 16 * BK * 2);
+    if (t + 1 < nk) dma_x(1, t + 1);
+    G3_SYNC_MFMA(0, 0, w0f)
+    // ---- phase 1: read W1; DMA X0 of t+2; Q(x0, w1)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) w1f[a][ks] = *(const bf16x8*)(st + wl[1][ks] + a * 16 * BK * 2);
+    if (deep) dma_x(0, t + 2);
+    G3_SYNC_MFMA(0, 1, w1f)
+    // ---- phase 2: read X1; DMA W0 of t+2; Q(x1, w1)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) xf[b][ks] = *(const bf16x8*)(st + xl[1][ks] + b * 16 * BK * 2);
+    if (deep) dma_w(0, t + 2);
+    G3_SYNC_MFMA(1, 1, w1f)
+    // ---- phase 3: DMA W1 of t+2; Q(x1, w0)
+    if (deep) dma_w(1, t + 2);
+    G3_SYNC_MFMA(1, 0, w0f)
+#undef G3_SYNC_MFMA
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+
+  const int mbase = (int)m0 + 128 * wr, nbase = (int)n0 + 64 * wc;
+  if (split == 1) {
+    gemm_epilogue<8, 4>(d, acc, mbase, nbase, lane);
+  } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
+    float* slab = (float*)d.ws + (int64_t)sp * M * N;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int64_t n = nbase + a * 16 + 4 * fq;
+      if (n >= N) continue;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int64_t m = mbase + b * 16 + fr;
+        if (m < M) *(float4*)(slab + m * N + n) = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+      }
+    }
   }
 }
 
@@ -691,36 +879,65 @@ int launch(const vd_gemm_desc& d, hipStream_t s) {
   return vd_launch_status();
 }
 
+int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
+  const int64_t units = ((d.M + G3_BM - 1) / G3_BM) * ((d.N + G3_BN - 1) / G3_BN) * split;
+  if (units > 0x7fffffff) return VD_EINVAL;
+  hipLaunchKernelGGL((gemm3_kernel<VD_A_DENSE>), dim3((unsigned)units), dim3(G3_NT), 0, s, d, a0b, a1b, wb, split);
+  int rc = vd_launch_status();
+  if (rc != VD_OK || split == 1) return rc;
+  const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
+  const int64_t blocks = (work + 255) / 256;
+  hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, d, split);
+  return vd_launch_status();
+}
+
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
-int g_force_v1 = 0;
+int g_path = 0;  // 0 auto, 1 v1, 2 v2, 3 v3 (tests / benchmarks)
 
 struct Plan {
-  bool v2 = false;
+  int ver = 1;
   int bn = 128, split = 1;
   uint32_t a0b = 0, a1b = 0, wb = 0;
   int64_t ws_bytes = 0;
 };
 
-// v2 (LDS-DMA, 256-row tiles) wherever the operands fit 32-bit buffer offsets;
-// split K when the output tiles cannot fill the 256 CUs.
+inline int split_for(int64_t tiles, int64_t nk) {
+  if (tiles >= 192 || nk < 16) return 1;
+  int64_t sp = (256 + tiles - 1) / tiles;
+  sp = sp < nk / 8 ? sp : nk / 8;
+  return (int)(sp < 8 ? sp : 8);
+}
+
+// LDS-DMA kernels wherever the operands fit 32-bit buffer offsets: v3 (256x256,
+// 8-phase ping-pong) for wide dense shapes that fill the chip, v2 (256 x
+// {128,160}, persistent) otherwise; split K when the output tiles cannot fill
+// the 256 CUs.
 Plan plan(const vd_gemm_desc& d) {
   Plan p;
-  if (g_force_v1 || d.K % BK || d.k0 % BK || d.M < G2_BM || d.N < 64) return p;
+  if (g_path == 1 || d.K % BK || d.k0 % BK || d.M < G2_BM || d.N < 64) return p;
   const int64_t a_rows = d.a_mode == VD_A_CONV3X3 ? (int64_t)d.n_img * d.h_in * d.w_in : d.M;
   const int64_t a0b = a_rows * d.lda0 * 2, a1b = d.a1 ? a_rows * d.lda1 * 2 : 0, wb = d.N * d.ldw * 2;
   if (a0b >= (int64_t)G2_OOB || a1b >= (int64_t)G2_OOB || wb >= (int64_t)G2_OOB) return p;
-  const int64_t p128 = (d.N + 127) / 128 * 128, p160 = (d.N + 159) / 160 * 160;
-  p.bn = d.act != VD_ACT_GEGLU && (p160 < p128 || (p160 == p128 && d.N % 160 == 0)) ? 160 : 128;
-  const int64_t tiles = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + p.bn - 1) / p.bn);
-  const int64_t nk = d.K / BK;
-  if (tiles < 192 && nk >= 16) {
-    int64_t sp = (256 + tiles - 1) / tiles;
-    sp = sp < nk / 8 ? sp : nk / 8;
-    p.split = (int)(sp < 8 ? sp : 8);
-  }
-  p.v2 = true;
   p.a0b = (uint32_t)a0b; p.a1b = (uint32_t)a1b; p.wb = (uint32_t)wb;
+  const int64_t nk = d.K / BK;
+  const bool v3ok = d.a_mode == VD_A_DENSE && d.N >= 256 && g_path != 2;
+  const int64_t p256 = (d.N + 255) / 256 * 256;
+  // measured (tools/kbench.py): v3 wins on the wide projections (qkv, GEGLU) once the
+  // grid fills the chip without split-K; v2's persistent stream wins on N <= 640 and
+  // on few-tile shapes
+  const bool v3auto = v3ok && d.N >= 768 && (p256 - d.N) * 16 <= d.N &&
+                      ((d.M + G3_BM - 1) / G3_BM) * (p256 / 256) >= 256;
+  if (g_path == 3 ? v3ok : v3auto) {
+    p.ver = 3;
+    p.bn = 256;
+    p.split = split_for(((d.M + G3_BM - 1) / G3_BM) * (p256 / 256), nk);
+  } else {
+    p.ver = 2;
+    const int64_t p128 = (d.N + 127) / 128 * 128, p160 = (d.N + 159) / 160 * 160;
+    p.bn = d.act != VD_ACT_GEGLU && (p160 < p128 || (p160 == p128 && d.N % 160 == 0)) ? 160 : 128;
+    p.split = split_for(((d.M + G2_BM - 1) / G2_BM) * ((d.N + p.bn - 1) / p.bn), nk);
+  }
   p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 : 0;
   return p;
 }
@@ -729,9 +946,14 @@ Plan plan(const vd_gemm_desc& d) {
 
 extern "C" int64_t vd_gemm_ws_bytes(const vd_gemm_desc* d) { return d ? plan(*d).ws_bytes : 0; }
 
-// Test/benchmark hook: force the v1 (register-staged) GEMM path.
+// Test/benchmark hooks: force the v1 (register-staged) GEMM path / pick a path.
 extern "C" int vd_gemm_force_v1(int32_t on) {
-  g_force_v1 = on;
+  g_path = on ? 1 : 0;
+  return VD_OK;
+}
+extern "C" int vd_gemm_select_path(int32_t path) {
+  if (path < 0 || path > 3) return VD_EINVAL;
+  g_path = path;
   return VD_OK;
 }
 
@@ -778,11 +1000,11 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
     cus_read = true;
   }
   const Plan p = plan(d);
-  if (p.v2) {
-    if (p.split > 1) VD_CHECK_ARG(d.ws && al16(d.ws) && d.ws_bytes >= p.ws_bytes);
+  if (p.ver >= 2 && p.split > 1) VD_CHECK_ARG(d.ws && al16(d.ws) && d.ws_bytes >= p.ws_bytes);
+  if (p.ver == 3) return launch3(d, s, p.a0b, p.a1b, p.wb, p.split);
+  if (p.ver == 2)
     return p.bn == 160 ? launch2<160>(d, s, p.a0b, p.a1b, p.wb, p.split)
                        : launch2<128>(d, s, p.a0b, p.a1b, p.wb, p.split);
-  }
   if (d.act == VD_ACT_GEGLU) return launch<128, 128>(d, s);
   // N tile: least padding, then fewer tiles.
   if (d.N <= 64) return launch<128, 64>(d, s);
