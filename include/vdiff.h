@@ -150,6 +150,9 @@ int vd_temporal_attention(const void* q, const void* k, const void* v, int64_t l
                           void* o, int64_t ldo, int64_t batch, int32_t frames,
                           int64_t positions, int32_t heads, int32_t d, float scale,
                           vd_stream_t stream);
+/* Test/benchmark hook: on != 0 forces the VALU temporal kernel (default: the MFMA kernel
+ * for frames <= 16 and d in {40, 80, 160}). */
+int vd_temporal_force_valu(int32_t on);
 
 /* ---------------------------------------------------------------- step glue
  * vd_timestep_embed: diffusers Timesteps(dim, flip_sin_to_cos=True, shift 0)

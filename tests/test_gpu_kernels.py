@@ -392,13 +392,27 @@ def test_flash_attention_unit_scale(cuda):
     close_bf16(got, want)
 
 
-@pytest.mark.parametrize("frames,d", [(16, 40), (16, 160), (4, 32), (32, 80), (5, 64)])
-def test_temporal_attention(cuda, frames, d):
+@pytest.fixture(params=["mfma", "valu"])
+def temporal_path(request, cuda):
+    """frames <= 16 with d in {40, 80, 160} run on the MFMA kernel unless forced to VALU."""
+    from vdiff._lib import lib
+    lib().vd_temporal_force_valu(int(request.param == "valu"))
+    yield request.param
+    lib().vd_temporal_force_valu(0)
+
+
+@pytest.mark.parametrize("frames,d,scale", [(16, 40, None), (16, 80, None), (16, 160, None), (5, 40, None),
+                                            (1, 80, None), (12, 160, None), (16, 40, "unit"), (4, 32, None),
+                                            (32, 80, None), (5, 64, None)])
+def test_temporal_attention(temporal_path, frames, d, scale):
     batch, pos, heads = 2, 37, 3
     C = heads * d
     qkv = rnd(batch * frames * pos, 3 * C, std=1.5)
     q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
-    got = ops.temporal_attention(q, k, v, batch, frames, pos, heads, d)
+    sc = 1.0 / math.log2(math.e) if scale == "unit" else None   # the model's call (scale folded into to_q)
+    got = ops.temporal_attention(q, k, v, batch, frames, pos, heads, d, scale=sc)
+    if sc is not None:
+        q = q.double() * (sc * math.sqrt(d))   # sdpa_ref applies d^-0.5
 
     def tok(t):  # rows (b, f, p) -> (b*p, f, C)
         return t.double().reshape(batch, frames, pos, C).permute(0, 2, 1, 3).reshape(batch * pos, frames, C)

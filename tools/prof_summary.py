@@ -1,25 +1,33 @@
-"""Summarise a rocprofv3 kernel trace: per-kernel-shape time per denoising step.
-usage: python tools/prof_summary.py gpurun_out/prof/run_kernel_trace.csv [steps]"""
+"""Summarise a rocprofv3 kernel trace of bench.py: time per denoising step by kernel family and shape.
+
+usage: python tools/prof_summary.py gpurun_out/prof/.../run_kernel_trace.csv
+
+The step count is the number of ddim_cfg_kernel launches in the trace (one per step,
+priming and warmup included); kernel groups launched fewer times than that (weight
+init, graph-capture probes) are one-off work and are left out of the per-step table.
+"""
 import collections
 import csv
 import sys
 
-path = sys.argv[1]
-steps = float(sys.argv[2]) if len(sys.argv) > 2 else 8.0
-rows = list(csv.DictReader(open(path)))
+rows = list(csv.DictReader(open(sys.argv[1])))
 agg = collections.defaultdict(list)
 for r in rows:
-    n = r["Kernel_Name"]
-    short = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
-    key = (short[:48], r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"])
+    n = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+    key = (n[:44], r["Grid_Size_X"], r["Workgroup_Size_X"])
     agg[key].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-tot = sum(sum(v) for v in agg.values())
-fam = collections.defaultdict(int)
-for k, v in agg.items():
-    fam[k[0].split("<")[0]] += sum(v)
-print(f"total {tot / 1e6:.2f} ms over trace; per step ~{tot / 1e6 / steps:.2f} ms")
-for k, v in sorted(fam.items(), key=lambda kv: -kv[1])[:14]:
-    print(f"  {v / tot * 100:5.1f}%  {v / 1e6 / steps:7.2f} ms/step  {k}")
-print("top shapes:")
-for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:28]:
-    print(f"  {sum(v) / 1e6 / steps:6.2f} ms/step n={len(v):5d} avg={sum(v) / len(v) / 1e3:8.1f}us {k}")
+steps = sum(len(v) for k, v in agg.items() if k[0].startswith("ddim_cfg_kernel"))
+if steps == 0:
+    sys.exit("no ddim_cfg_kernel launches in the trace")
+per = {k: v for k, v in agg.items() if len(v) >= steps}
+tot = sum(sum(v) for v in per.values()) / steps
+fam = collections.defaultdict(float)
+for k, v in per.items():
+    fam[k[0].split("<")[0]] += sum(v) / steps
+print(f"{steps} steps in the trace; per-step kernel time {tot / 1e6:.2f} ms")
+for k, v in sorted(fam.items(), key=lambda kv: -kv[1])[:16]:
+    print(f"  {v / tot * 100:5.1f}%  {v / 1e6:7.3f} ms/step  {k}")
+print("top shapes (per step):")
+for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))[:40]:
+    print(f"  {sum(v) / steps / 1e3:8.1f} us  x{len(v) / steps:5.1f}  avg {sum(v) / len(v) / 1e3:8.1f} us  "
+          f"{k[0]} grid={k[1]} wg={k[2]}")

@@ -762,7 +762,116 @@ __global__ __launch_bounds__(NT) void temporal_attn_kernel(
   }
 }
 
+// ------------------------------------------------------- temporal (MFMA)
+// frames <= 16: one (b, p, h) item per wave iteration on v_mfma_f32_16x16x32_bf16.
+//   S^T[key][q] = K . Q^T   A = K rows, B = Q^T, both straight from the NHWC rows
+//                           (lane (fr, fq) holds row fr, dims 32*ks + 8*fq .. +7);
+//   softmax over the 16 keys of query fr: 4 keys per lane, two xor-shuffles;
+//   O^T[d][q] = V^T . P^T   P^T's k-slot (fq, j) is key 4*fq + j for j < 4 and an
+//                           empty slot (P = 0) for j >= 4, so the S^T accumulator
+//                           IS the B operand (no lane movement); V^T comes from a
+//                           per-wave LDS image with ds_read_b64_tr_b16 (T10), whose
+//                           column D is 1.0: row D of O^T is the softmax row sum.
+// Memory-bound (3 reads + 1 write of the head's 16 rows); 4 waves per block,
+// items strided over the grid so the LDS padding is written once per wave.
+template <int D>
+struct TmCfg {
+  static constexpr int KSTEPS = (D + 31) / 32;
+  static constexpr int DB = (D + 1 + 15) / 16;   // O^T row blocks incl. the ones row
+  static constexpr int VS = 16 * (DB | 1);       // LDS row (elements): 32 B x odd -> conflict-free tr reads
+  static constexpr int DCH = D / 8;
+};
+
+template <int D>
+__global__ __launch_bounds__(NT) void temporal_mfma_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
+    bf16_t* __restrict__ o, int64_t ldo, int64_t batch, int frames, int64_t positions, int heads,
+    float c) {
+  using C = TmCfg<D>;
+  __shared__ __attribute__((aligned(16))) bf16_t vimg[4][16 * C::VS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16_t* vl = vimg[wave];
+  // padding columns [D, VS) of every row: 1.0 at column D, 0 elsewhere (never overwritten);
+  // rows >= frames stay zero (their P is 0)
+  for (int idx = lane; idx < 16 * C::VS / 8; idx += 64) *(uint4*)(vl + idx * 8) = make_uint4(0, 0, 0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane < 16) vl[lane * C::VS + D] = (bf16_t)0x3F80;
+  const int64_t nitems = batch * positions * heads;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  const bool unitc = c == 1.0f;
+  const int vtr = (4 * fq + (fr >> 2)) * C::VS + 4 * (fr & 3);  // tr-read lane offset in a column block
+  for (int64_t item = (int64_t)blockIdx.x * 4 + wave; item < nitems; item += stride) {
+    const int h = (int)(item % heads);
+    const int64_t bp = item / heads;
+    const int64_t p = bp % positions, b = bp / positions;
+    const int64_t row0 = b * frames * positions + p;  // row of frame 0; frame f at + f * positions
+    const bool fok = fr < frames;
+    const int64_t rf = (row0 + (fok ? fr : 0) * positions) * ld + (int64_t)h * D;
+    // ---- V rows -> LDS (d < D only)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous item's tr reads done
+    for (int idx = lane; idx < frames * C::DCH; idx += 64) {
+      const int f = idx / C::DCH, cc = idx - f * C::DCH;
+      *(uint4*)(vl + f * C::VS + cc * 8) =
+          *(const uint4*)(v + (row0 + (int64_t)f * positions) * ld + (int64_t)h * D + cc * 8);
+    }
+    // ---- S^T = K . Q^T
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < C::KSTEPS; ++ks) {
+      const int dd = ks * 32 + 8 * fq;
+      uint4 kq = make_uint4(0, 0, 0, 0), qq = make_uint4(0, 0, 0, 0);
+      if (dd < D && fok) {
+        kq = *(const uint4*)(k + rf + dd);
+        qq = *(const uint4*)(q + rf + dd);
+      }
+      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kq), __builtin_bit_cast(bf16x8, qq), s,
+                                                  0, 0, 0);
+    }
+    // ---- softmax over keys 4*fq + j of query fr (log2 units)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (4 * fq + j >= frames) s[j] = -INFINITY;
+      else if (!unitc) s[j] *= c;
+      mx = fmaxf(mx, s[j]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    bf16x8 pf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pf[j] = (__bf16)__builtin_amdgcn_exp2f(s[j] - mx);
+      pf[4 + j] = (__bf16)0.0f;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // V image written
+    __builtin_amdgcn_wave_barrier();
+    // ---- O^T = V^T . P^T, one 16-row block of d at a time
+    f32x4 ot[C::DB];
+#pragma unroll
+    for (int a = 0; a < C::DB; ++a) {
+      const bf16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (bf16x4 __attribute__((address_space(3)))*)(vl + vtr + 16 * a));
+      const bf16x8 vf = {t[0], t[1], t[2], t[3], (__bf16)0.0f, (__bf16)0.0f, (__bf16)0.0f, (__bf16)0.0f};
+      ot[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+    // row sum = O^T row D: block D/16, lane group (D%16)/4, element D%4
+    const float l = __shfl(ot[D / 16][(D % 16) % 4], ((D % 16) / 4) * 16 + fr, 64);
+    const float inv = __builtin_amdgcn_rcpf(l);
+    if (fok) {
+      bf16_t* orow = o + (row0 + (int64_t)fr * positions) * ldo + (int64_t)h * D;
+#pragma unroll
+      for (int a = 0; a < C::DB; ++a) {
+        const int dd = 16 * a + 4 * fq;
+        if (dd + 4 <= D)
+          *(uint2*)(orow + dd) = make_uint2(pack2(ot[a][0] * inv, ot[a][1] * inv), pack2(ot[a][2] * inv, ot[a][3] * inv));
+      }
+    }
+  }
+}
+
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+int g_temporal_valu = 0;  // vd_temporal_force_valu
 
 }  // namespace
 
@@ -793,6 +902,12 @@ extern "C" int vd_attention(const void* q, int64_t ldq, const void* k, int64_t l
   }
 }
 
+// Test/benchmark hook: on != 0 runs every temporal attention on the VALU kernel.
+extern "C" int vd_temporal_force_valu(int32_t on) {
+  g_temporal_valu = on;
+  return VD_OK;
+}
+
 extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v, int64_t ld,
                                      void* o, int64_t ldo, int64_t batch, int32_t frames,
                                      int64_t positions, int32_t heads, int32_t d, float scale,
@@ -804,6 +919,18 @@ extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v
   const unsigned grid = (unsigned)((items + 3) / 4);
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
+  if (frames <= 16 && !g_temporal_valu && (d == 40 || d == 80 || d == 160) && ld % 8 == 0 && ldo % 4 == 0) {
+    const int64_t g = (items + 3) / 4;
+    const unsigned grid2 = (unsigned)(g < 8192 ? g : 8192);
+#define TM_LAUNCH(DD)                                                                                           \
+    hipLaunchKernelGGL(temporal_mfma_kernel<DD>, dim3(grid2), dim3(NT), 0, s, (const bf16_t*)q, (const bf16_t*)k, \
+                       (const bf16_t*)v, ld, (bf16_t*)o, ldo, batch, frames, positions, heads, sl2)
+    if (d == 40) TM_LAUNCH(40);
+    else if (d == 80) TM_LAUNCH(80);
+    else TM_LAUNCH(160);
+#undef TM_LAUNCH
+    return vd_launch_status();
+  }
   if (frames <= 8)
     hipLaunchKernelGGL(temporal_attn_kernel<8>, dim3(grid), dim3(NT), 0, s, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, ld, (bf16_t*)o, ldo, batch, frames,
