@@ -360,6 +360,9 @@ def _deferred_max_case(kind, sq=256, skv=640, d=40):
     elif kind == "late_spike":  # one query's max jumps in the last tile only (mixed lanes)
         k = 0.1 * k
         k[skv - 3] = q[37] * 6
+    elif kind == "huge_spike":  # a jump of ~180 (log2) in a late tile: exp2 would overflow -> exact rerun
+        k = 0.1 * k
+        k[skv - 70] = q[37] * 20
     elif kind == "offset":      # all scores ~ +70 (mu far from 0: bf16 rounding of mu)
         q, k = 8 * u + 0.3 * q, 40 * u + 0.1 * k
     elif kind == "negative":    # all scores ~ -70: the first tile's mu must come from the data
@@ -367,7 +370,7 @@ def _deferred_max_case(kind, sq=256, skv=640, d=40):
     return bf(q), bf(k), bf(v)
 
 
-@pytest.mark.parametrize("kind", ["ramp", "creep", "late_spike", "offset", "negative"])
+@pytest.mark.parametrize("kind", ["ramp", "creep", "late_spike", "huge_spike", "offset", "negative"])
 def test_flash_attention_deferred_max(attn_path, kind):
     q, k, v = _deferred_max_case(kind)
     sq, skv, d = q.shape[0], k.shape[0], q.shape[1]

@@ -133,3 +133,21 @@ for name, hw, d in [("temporal L1", 4096, 40), ("temporal L2", 1024, 80), ("temp
     out = torch.empty(B * F_ * hw, C, device=dev, dtype=torch.bfloat16)
     us = timeit(lambda: ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, F_, hw, 8, d, out=out))
     report(f"{name} F=16 pos={hw} d={d}", us, 4.0 * B * hw * 8 * F_ * F_ * d, 2 * B * F_ * hw * C * 4)
+
+for name, n_inst, pix, C, groups in [("gn L1 image", 32, 4096, 320, 32), ("gn L1 motion", 2, 65536, 320, 32),
+                                     ("gn L2 image", 32, 1024, 640, 32), ("gn L3 image", 32, 256, 1280, 32)]:
+    if flt not in name:
+        continue
+    x = rnd(n_inst * pix, C)
+    gam, bet = torch.ones(C, device=dev), torch.zeros(C, device=dev)
+    us = timeit(lambda: ops.group_norm(x, n_inst, pix, groups, 1e-6, gam, bet, silu=True))
+    report(f"{name} inst={n_inst} pix={pix} C={C}", us, 0, 2 * 2 * n_inst * pix * C + 2 * n_inst * pix * C)
+
+for name, rows, C in [("ln L1", 131072, 320), ("ln L2", 32768, 640), ("ln L3", 8192, 1280)]:
+    if flt not in name:
+        continue
+    x = rnd(rows, C)
+    gam, bet = torch.ones(C, device=dev), torch.zeros(C, device=dev)
+    out = torch.empty_like(x)
+    us = timeit(lambda: ops.layer_norm(x, gam, bet, out=out))
+    report(f"{name} rows={rows} C={C}", us, 0, 2 * 2 * rows * C)

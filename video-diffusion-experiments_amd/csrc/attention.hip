@@ -386,6 +386,207 @@ __device__ __forceinline__ float partner32(float x) {
   return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
 }
 
+// One pass of flash32's key loop (prologue tile load included).  EXACT tracks the
+// running max of every tile (deferred, THR); the fast pass computes it for the
+// first tile only and afterwards lets P grow up to 2^32 before raising mu by
+// log2(row sum) — the row sum comes free from the PV MFMA's ones column, so the
+// common tile has no max reduction at all (-40 VALU ops per 64 keys).  mu stays
+// >= the running max (l >= 2^(max - mu)), so nothing underflows that matters;
+// a row sum >= 2^100 (or non-finite) means a score jumped past the fp32/bf16
+// range and the pass reports `bad` so the block reruns EXACT.
+template <int D, bool UNITC, bool EXACT>
+__device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, const bf16_t* vb_ptr, int ldk32,
+                                         int ldv32, int64_t skv, const int (&krow)[F32Cfg<D>::LREG],
+                                         const uint32_t (&kcol)[F32Cfg<D>::LREG],
+                                         const uint32_t (&ldsk)[F32Cfg<D>::LREG],
+                                         const uint32_t (&ldsv)[F32Cfg<D>::LREG],
+                                         bf16x8 (&qf)[2][F32Cfg<D>::KSTEPS], f32x16 (&oacc)[F32Cfg<D>::NDB][2],
+                                         int r32, int hh, int vtr, float c) {
+  using C = F32Cfg<D>;
+  constexpr int QB = 2;
+  constexpr float RESCALE = 4294967296.0f;        // 2^32
+  constexpr float BAD = 1.2676506002282294e30f;   // 2^100
+#pragma unroll
+  for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[db][qb][i] = 0.f;
+  float mu[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) mu[qb] = 0.f;
+  bool bad = false;
+
+  const int ntiles = (int)((skv + KT - 1) / KT);
+  const bool ragged = (skv % KT) != 0;
+  stage_t<C::LREG> kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, 0, skv, krow, kcol);
+#pragma unroll
+  for (int i = 0; i < C::LREG; ++i) {
+    *(uint4*)(lds + ldsk[i]) = make_uint4(kvst[4 * i], kvst[4 * i + 1], kvst[4 * i + 2], kvst[4 * i + 3]);
+    *(uint4*)(lds + ldsv[i]) = make_uint4(kvst[4 * C::LREG + 4 * i], kvst[4 * C::LREG + 4 * i + 1],
+                                          kvst[4 * C::LREG + 4 * i + 2], kvst[4 * C::LREG + 4 * i + 3]);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, t + 1, skv, krow, kcol);
+    const bf16_t* kl = lds + buf * C::STAGE;
+    const bf16_t* vl = kl + C::K_ELEMS;
+
+    // ---- x^T = K'.Q'^T  (= s - mu)
+    f32x16 s[2][QB];
+    bf16x8 kfr[2][C::KSTEPS];  // all K fragments of the tile first: one LDS latency, not six
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < C::KSTEPS; ++ks)
+        kfr[kb][ks] = *(const bf16x8*)(kl + (kb * 32 + r32) * C::KS + ks * 16 + 8 * hh);
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them to their MFMAs)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int ks = 0; ks < C::KSTEPS; ++ks) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          if (ks == 0) {
+            f32x16 z;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) z[i] = 0.f;
+            s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], z, 0, 0, 0);
+          } else {
+            s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], s[kb][qb], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (ragged && t == ntiles - 1) {  // keys past skv: x = -inf (rows are clamped duplicates)
+      const int kvalid = (int)(skv - (int64_t)t * KT);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (key >= kvalid) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) s[kb][qb][i] = -INFINITY;
+          }
+        }
+    }
+    // V^T fragments for this tile's PV, issued now so their LDS latency hides
+    // under the softmax VALU work (key order of each step: 16*s2 + 8*(j>>2) + 4*hh + (j&3))
+    bf16x8 vfr[C::NDB][2][2];
+#pragma unroll
+    for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16_t* p0 = vl + (db * KT + kb * 32 + 16 * s2) * 32 + vtr;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (bf16x4 __attribute__((address_space(3)))*)(p0));
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (bf16x4 __attribute__((address_space(3)))*)(p0 + 8 * 32));
+          vfr[db][kb][s2] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+    __builtin_amdgcn_sched_barrier(0);
+    if (EXACT || t == 0) {  // ---- tile max (deferred, THR): every tile on the exact pass, tile 0 on the fast one
+      float tm[QB];
+      bool need = t == 0;
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const float m = tile_max(s[0][qb], s[1][qb]);
+        tm[qb] = vmax2(m, partner32(m));
+        need |= (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
+      }
+      if (__any(need)) {  // wave-uniform: first tile or a row max moved by > THR
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          const bool up = t == 0 || (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
+          const float nmu = up ? (float)(__bf16)(mu[qb] + tm[qb]) : mu[qb];
+          const float delta = nmu - mu[qb];  // exact: both bf16 values
+          const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
+          mu[qb] = nmu;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[kb][qb][i] -= delta;
+#pragma unroll
+          for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
+          if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
+        }
+      }
+    }
+    // ---- P = exp2(x), packed: registers 8*s2 .. 8*s2+7 of tile kb = k-step (kb, s2)
+    bf16x8 pf[2][2][QB];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            f[j] = (__bf16)__builtin_amdgcn_exp2f(UNITC ? s[kb][qb][8 * s2 + j] : s[kb][qb][8 * s2 + j] * c);
+          pf[kb][s2][qb] = f;
+        }
+    // ---- O^T += V^T.P^T
+#pragma unroll
+    for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb)
+            oacc[db][qb] =
+                __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[db][kb][s2], pf[kb][s2][qb], oacc[db][qb], 0, 0, 0);
+    if (!EXACT && t > 0) {  // ---- fast pass: rescale from the row sum when it outgrows 2^32
+      float lq[QB];
+      bool resc = false, over = false;
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const float lown = oacc[C::L_DB][qb][C::L_I];
+        const float lp = partner32(lown);
+        lq[qb] = hh == C::L_H ? lown : lp;
+        resc |= lq[qb] > RESCALE;
+        over |= !(lq[qb] < BAD);
+      }
+      if (__any(over)) {
+        bad = true;
+      } else if (__any(resc)) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          const float step = lq[qb] > RESCALE ? __builtin_amdgcn_logf(lq[qb]) : 0.f;  // log2(l)
+          const float nmu = (float)(__bf16)(mu[qb] + (UNITC ? step : step / c));
+          const float delta = nmu - mu[qb];
+          const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
+          mu[qb] = nmu;
+#pragma unroll
+          for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
+          if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
+        }
+      }
+    }
+    if (t + 1 < ntiles) {
+      bf16_t* nb = lds + (buf ^ 1) * C::STAGE;
+#pragma unroll
+      for (int i = 0; i < C::LREG; ++i) {
+        *(uint4*)(nb + ldsk[i]) = make_uint4(kvst[4 * i], kvst[4 * i + 1], kvst[4 * i + 2], kvst[4 * i + 3]);
+        *(uint4*)(nb + ldsv[i]) = make_uint4(kvst[4 * C::LREG + 4 * i], kvst[4 * C::LREG + 4 * i + 1],
+                                             kvst[4 * C::LREG + 4 * i + 2], kvst[4 * C::LREG + 4 * i + 3]);
+      }
+    }
+    __syncthreads();
+  }
+  return bad;
+}
+
 template <int D, bool UNITC>
 __global__ __launch_bounds__(NT, 2) void flash32_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
@@ -452,162 +653,19 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
     ldsv[i] = (uint32_t)(C::K_ELEMS + ((cc >> 2) * KT + r) * 32 + (cc & 3) * 8);
   }
   const int ldk32 = (int)ldk, ldv32 = (int)ldv;
-  stage_t<C::LREG> kvst;
 
-  f32x16 oacc[C::NDB][QB];
-#pragma unroll
-  for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[db][qb][i] = 0.f;
-  float mu[QB];
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb) mu[qb] = 0.f;
-
-  const int ntiles = (int)((skv + KT - 1) / KT);
-  const bool ragged = (skv % KT) != 0;
-  kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, 0, skv, krow, kcol);
-  {
-    bf16_t* b0 = lds;
-#pragma unroll
-    for (int i = 0; i < C::LREG; ++i) {
-      *(uint4*)(b0 + ldsk[i]) = make_uint4(kvst[4 * i], kvst[4 * i + 1], kvst[4 * i + 2], kvst[4 * i + 3]);
-      *(uint4*)(b0 + ldsv[i]) = make_uint4(kvst[4 * C::LREG + 4 * i], kvst[4 * C::LREG + 4 * i + 1],
-                                           kvst[4 * C::LREG + 4 * i + 2], kvst[4 * C::LREG + 4 * i + 3]);
-    }
-  }
-  __syncthreads();
   const int g16 = lane >> 4, i16 = lane & 15;
   // V^T tr-read lane offset inside a [32 d] image row block (elements)
   const int vtr = ((4 * hh + (i16 >> 2)) * 32) + 16 * (g16 & 1) + 4 * (i16 & 3);
-
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, t + 1, skv, krow, kcol);
-    const bf16_t* kl = lds + buf * C::STAGE;
-    const bf16_t* vl = kl + C::K_ELEMS;
-
-    // ---- x^T = K'.Q'^T  (= s - mu)
-    f32x16 s[2][QB];
-    bf16x8 kfr[2][C::KSTEPS];  // all K fragments of the tile first: one LDS latency, not six
+  f32x16 oacc[C::NDB][QB];
+  const bool bad = f32_loop<D, UNITC, false>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv,
+                                             qf, oacc, r32, hh, vtr, c);
+  if (__syncthreads_or(bad)) {  // a score jumped > ~100 (log2) past mu somewhere: exact pass
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int ks = 0; ks < C::KSTEPS; ++ks)
-        kfr[kb][ks] = *(const bf16x8*)(kl + (kb * 32 + r32) * C::KS + ks * 16 + 8 * hh);
-    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them to their MFMAs)
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int ks = 0; ks < C::KSTEPS; ++ks) {
-        const bf16x8 kf = kfr[kb][ks];
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
-          if (ks == 0) {
-            f32x16 z;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) z[i] = 0.f;
-            s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][ks], z, 0, 0, 0);
-          } else {
-            s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qb][ks], s[kb][qb], 0, 0, 0);
-          }
-        }
-      }
-    }
-    if (ragged && t == ntiles - 1) {  // keys past skv: u = -inf (rows are clamped duplicates)
-      const int kvalid = (int)(skv - (int64_t)t * KT);
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (key >= kvalid) {
-#pragma unroll
-            for (int qb = 0; qb < QB; ++qb) s[kb][qb][i] = -INFINITY;
-          }
-        }
-    }
-    // V^T fragments for this tile's PV, issued now so their LDS latency hides
-    // under the softmax VALU work (key order of each step: 16*s2 + 8*(j>>2) + 4*hh + (j&3))
-    bf16x8 vfr[C::NDB][2][2];
-#pragma unroll
-    for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16_t* p0 = vl + (db * KT + kb * 32 + 16 * s2) * 32 + vtr;
-          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-              (bf16x4 __attribute__((address_space(3)))*)(p0));
-          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-              (bf16x4 __attribute__((address_space(3)))*)(p0 + 8 * 32));
-          vfr[db][kb][s2] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- deferred max
-    float tm[QB];
-    bool need = t == 0;
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-      const float m = tile_max(s[0][qb], s[1][qb]);
-      tm[qb] = vmax2(m, partner32(m));
-      need |= (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
-    }
-    if (__any(need)) {  // wave-uniform: first tile or a row max moved by > THR
-#pragma unroll
-      for (int qb = 0; qb < QB; ++qb) {
-        const bool up = t == 0 || (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
-        const float nmu = up ? (float)(__bf16)(mu[qb] + tm[qb]) : mu[qb];
-        const float delta = nmu - mu[qb];  // exact: both bf16 values
-        const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
-        mu[qb] = nmu;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) s[kb][qb][i] -= delta;
-#pragma unroll
-        for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
-        if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
-      }
-    }
-    // ---- P = exp2(u), packed: registers 8*s2 .. 8*s2+7 of tile kb = k-step (kb, s2)
-    bf16x8 pf[2][2][QB];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int qb = 0; qb < QB; ++qb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 f;
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            f[j] = (__bf16)__builtin_amdgcn_exp2f(UNITC ? s[kb][qb][8 * s2 + j] : s[kb][qb][8 * s2 + j] * c);
-          pf[kb][s2][qb] = f;
-        }
-    // ---- O^T += V^T.P^T
-#pragma unroll
-    for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int qb = 0; qb < QB; ++qb)
-            oacc[db][qb] =
-                __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[db][kb][s2], pf[kb][s2][qb], oacc[db][qb], 0, 0, 0);
-    if (t + 1 < ntiles) {
-      bf16_t* nb = lds + (buf ^ 1) * C::STAGE;
-#pragma unroll
-      for (int i = 0; i < C::LREG; ++i) {
-        *(uint4*)(nb + ldsk[i]) = make_uint4(kvst[4 * i], kvst[4 * i + 1], kvst[4 * i + 2], kvst[4 * i + 3]);
-        *(uint4*)(nb + ldsv[i]) = make_uint4(kvst[4 * C::LREG + 4 * i], kvst[4 * C::LREG + 4 * i + 1],
-                                             kvst[4 * C::LREG + 4 * i + 2], kvst[4 * C::LREG + 4 * i + 3]);
-      }
-    }
-    __syncthreads();
+    for (int qb = 0; qb < QB; ++qb)
+      if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)0.0f;
+    f32_loop<D, UNITC, true>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv, qf, oacc, r32, hh,
+                             vtr, c);
   }
 
   // ---- epilogue: O[q][d] = O^T[d][q] / l; register i of d-block db holds

@@ -46,14 +46,37 @@ __global__ __launch_bounds__(NT) void gn_partial_kernel(const bf16_t* x0, int64_
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; sh[e] = 0.f; }
     if (active) {
-      for (int64_t p = pb + pl; p < pe; p += PL) {
-        const uint4 u = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row0 + p, (int64_t)j * 8);
+      // shift = the first pixel of this lane's run (shifted sums: no cancellation
+      // when |mean| >> std); then 4 independent 16-byte loads in flight per step
+      int64_t p = pb + pl;
+      if (p < pe) {
         float f[8];
-        unpack8(u, f);
-        if (cnt == 0) {
+        unpack8(*(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row0 + p, (int64_t)j * 8), f);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) sh[e] = f[e];
+        for (int e = 0; e < 8; ++e) sh[e] = f[e];
+        cnt = 1;
+        p += PL;
+      }
+      for (; p + 3 * PL < pe; p += 4 * PL) {
+        uint4 u[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) u[r] = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row0 + p + r * PL, (int64_t)j * 8);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float f[8];
+          unpack8(u[r], f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float t = f[e] - sh[e];
+            s1[e] += t;
+            s2[e] = fmaf(t, t, s2[e]);
+          }
         }
+        cnt += 4;
+      }
+      for (; p < pe; p += PL) {
+        float f[8];
+        unpack8(*(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row0 + p, (int64_t)j * 8), f);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float t = f[e] - sh[e];
@@ -106,9 +129,10 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
                                            float m22) {
   if (n2 == 0.f) return;
   const float nn = n + n2;
+  const float rn = __builtin_amdgcn_rcpf(nn);  // counts are exact small integers: ~1 ulp
   const float delta = mean2 - mean;
-  mean += delta * (n2 / nn);
-  m2 += m22 + delta * delta * (n * n2 / nn);
+  mean += delta * (n2 * rn);
+  m2 += m22 + delta * delta * (n * n2 * rn);
   n = nn;
 }
 
@@ -123,13 +147,22 @@ __global__ __launch_bounds__(NT) void gn_finalize_kernel(const float4* ws, int n
   const int cpg = (int)(C / groups);
   const int nrec = n_split * cpg;
   const float4* src = ws + (int64_t)inst * n_split * C + (int64_t)g * cpg;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int r = threadIdx.x; r < nrec; r += NT) {
-    const int s = r / cpg, q = r - s * cpg;
-    const float4 v = src[(int64_t)s * C + q];
-    chan_merge(n, mean, m2, v.x, v.y, v.z);
+  // 4 independent accumulators: 4 record loads in flight and 4 merge chains
+  float n[4] = {0.f, 0.f, 0.f, 0.f}, mean[4] = {0.f, 0.f, 0.f, 0.f}, m2[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r0 = threadIdx.x; r0 < nrec; r0 += 4 * NT) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + u * NT;
+      const int s = r / cpg, q = r - s * cpg;
+      v[u] = r < nrec ? src[(int64_t)s * C + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) chan_merge(n[u], mean[u], m2[u], v[u].x, v[u].y, v[u].z);
   }
-  red[threadIdx.x] = make_float3(n, mean, m2);
+#pragma unroll
+  for (int u = 1; u < 4; ++u) chan_merge(n[0], mean[0], m2[0], n[u], mean[u], m2[u]);
+  red[threadIdx.x] = make_float3(n[0], mean[0], m2[0]);
   __syncthreads();
   for (int off = NT / 2; off > 0; off >>= 1) {
     if (threadIdx.x < off) {

@@ -113,7 +113,10 @@ def conv3x3(x, n_img, h_in, w_in, w, *, x1=None, stride=1, upsample=False, bias=
 
 # ---------------------------------------------------------------- norms
 def gn_splits(n_inst: int, pix: int) -> int:
-    return max(1, min(pix // 16, math.ceil(2048 / n_inst)))
+    """Pixel splits per instance for vd_gn_partial: ~2048 partial blocks in total, at
+    most 256 per instance (the finalize pass combines n_split x C/groups records per
+    group; the motion-module norm has only 2 instances per rank)."""
+    return max(1, min(pix // 16, math.ceil(2048 / n_inst), 256))
 
 
 def gn_partial(x, C, n_inst, pix, n_split, x1=None):
