@@ -2,32 +2,38 @@
 
 usage: python tools/prof_summary.py gpurun_out/prof/.../run_kernel_trace.csv
 
-The step count is the number of ddim_cfg_kernel launches in the trace (one per step,
-priming and warmup included); kernel groups launched fewer times than that (weight
-init, graph-capture probes) are one-off work and are left out of the per-step table.
+Only the steady-state steps are counted: the window runs from the end of the 3rd
+ddim_cfg_kernel launch (one per step; priming, weight init and graph capture come
+before it) to the end of the last one, and everything launched inside it is divided
+by the number of steps it spans.  The bench's own roofline timing of the attention
+kernel runs after the last step and falls outside the window.
 """
 import collections
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+ddim = [r for r in rows if "ddim_cfg_kernel" in r["Kernel_Name"]]
+if len(ddim) < 5:
+    sys.exit("fewer than 5 ddim_cfg_kernel launches in the trace")
+t0, t1 = int(ddim[2]["End_Timestamp"]), int(ddim[-1]["End_Timestamp"])
+steps = len(ddim) - 3
+win = [r for r in rows if t0 < int(r["Start_Timestamp"]) and int(r["End_Timestamp"]) <= t1]
 agg = collections.defaultdict(list)
-for r in rows:
+for r in win:
     n = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
     key = (n[:44], r["Grid_Size_X"], r["Workgroup_Size_X"])
     agg[key].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-steps = sum(len(v) for k, v in agg.items() if k[0].startswith("ddim_cfg_kernel"))
-if steps == 0:
-    sys.exit("no ddim_cfg_kernel launches in the trace")
-per = {k: v for k, v in agg.items() if len(v) >= steps}
-tot = sum(sum(v) for v in per.values()) / steps
+busy = sum(sum(v) for v in agg.values()) / steps
 fam = collections.defaultdict(float)
-for k, v in per.items():
+for k, v in agg.items():
     fam[k[0].split("<")[0]] += sum(v) / steps
-print(f"{steps} steps in the trace; per-step kernel time {tot / 1e6:.2f} ms")
-for k, v in sorted(fam.items(), key=lambda kv: -kv[1])[:16]:
-    print(f"  {v / tot * 100:5.1f}%  {v / 1e6:7.3f} ms/step  {k}")
+print(f"{steps} steady-state steps; wall {(t1 - t0) / steps / 1e6:.2f} ms/step, kernel-busy {busy / 1e6:.2f} ms/step, "
+      f"{len(win) / steps:.0f} launches/step")
+for k, v in sorted(fam.items(), key=lambda kv: -kv[1])[:20]:
+    print(f"  {v / busy * 100:5.1f}%  {v / 1e6:7.3f} ms/step  {k}")
 print("top shapes (per step):")
-for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))[:40]:
-    print(f"  {sum(v) / steps / 1e3:8.1f} us  x{len(v) / steps:5.1f}  avg {sum(v) / len(v) / 1e3:8.1f} us  "
+for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:40]:
+    print(f"  {sum(v) / steps / 1e3:9.1f} us  x{len(v) / steps:5.1f}  avg {sum(v) / len(v) / 1e3:8.1f} us  "
           f"{k[0]} grid={k[1]} wg={k[2]}")
