@@ -92,7 +92,8 @@ int64_t vd_gemm_ws_bytes(const vd_gemm_desc* d);
 int vd_gemm_force_v1(int32_t on);
 /* Test/benchmark hook: 0 = automatic (default), 1 = v1 (register-staged, any shape),
  * 2 = v2 (256 x {128,160} persistent LDS-DMA), 3 = v3 (256 x 256 8-phase, dense A only;
- * shapes it cannot take fall back to the automatic choice). */
+ * shapes it cannot take fall back to the automatic choice), 5 = v5 (256 x 320, BK 32,
+ * 4-stage ring, load-free epilogue). */
 int vd_gemm_select_path(int32_t path);
 
 /* ---------------------------------------------------------------- GroupNorm

@@ -98,11 +98,11 @@ def test_gemm_geglu(cuda):
 
 
 # ---------------------------------------------------------------- v2 (LDS-DMA) paths
-@pytest.fixture(params=["v3", "v2", "v1"])
+@pytest.fixture(params=["v5", "v3", "v2", "v1"])
 def gemm_path(request, cuda):
     """Force one GEMM kernel (v3 only takes dense A; other shapes fall back to auto)."""
     from vdiff._lib import lib
-    lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3}[request.param])
+    lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5}[request.param])
     yield request.param
     lib().vd_gemm_select_path(0)
 
@@ -139,6 +139,56 @@ def test_gemm_v3_shapes(cuda, M, N, K, k0):
         got = ops.gemm(a, w, a1=a1, bias=b, res=res)
         x = a if a1 is None else torch.cat([a, a1], 1)
         close_bf16(got, x.float() @ w.float().T + b + res.float())
+    finally:
+        lib().vd_gemm_select_path(0)
+
+
+@pytest.mark.parametrize("M,N,K,k0", [(256, 160, 32, 32), (300, 128, 96, 64), (513, 1000, 192, 160),
+                                      (2048, 1280, 2560, 2560), (8192, 480, 640, 320), (1024, 320, 5120, 5120),
+                                      (131072, 320, 320, 320)])
+@pytest.mark.parametrize("path", [5, 0])
+def test_gemm_v5_shapes(cuda, path, M, N, K, k0):
+    """v5 (BK 32 ring; path 0 = automatic, which takes v5 for k0 % 64 != 0) pipeline edges: 1-3 k-steps (shorter than the ring), ragged M and
+    N, the a0|a1 concat split at k0 (a multiple of 32, not of 64), few tiles (split-K), and
+    the L1 shape whose units wrap the persistent grid several times."""
+    from vdiff._lib import lib
+    lib().vd_gemm_select_path(path)
+    try:
+        a = rnd(M, k0)
+        a1 = rnd(M, K - k0) if K > k0 else None
+        w = rnd(N, K, std=K ** -0.5)
+        b = torch.randn(N, device=cuda)
+        res = rnd(M, N)
+        got = ops.gemm(a, w, a1=a1, bias=b, res=res)
+        x = a if a1 is None else torch.cat([a, a1], 1)
+        close_bf16(got, x.float() @ w.float().T + b + res.float())
+    finally:
+        lib().vd_gemm_select_path(0)
+
+
+@pytest.mark.parametrize("M,N,K", [(131072, 960, 320), (1000, 328, 96), (4096, 640, 32), (300, 2560, 640)])
+@pytest.mark.parametrize("epi", ["bias", "nobias", "silu", "geglu"])
+@pytest.mark.parametrize("path", [5])
+def test_gemm_v5_load_free_epilogue(cuda, path, M, N, K, epi):
+    """v5's load-free epilogue (bias DMA'd into an LDS slot per unit, unconditional buffer
+    stores with out-of-range lanes dropped, the stores left in flight across the next
+    k-steps' counted waits): ragged M and N, one-k-step units, every activation."""
+    from vdiff._lib import lib
+    lib().vd_gemm_select_path(path)
+    try:
+        a = rnd(M, K)
+        if epi == "geglu":
+            N = N // 32 * 32
+        w = rnd(N, K, std=K ** -0.5)
+        b = None if epi == "nobias" else torch.randn(N, device=cuda)
+        if epi == "geglu":
+            got = ops.gemm(a, pack_geglu(w), bias=pack_geglu(b), act=ops.ACT_GEGLU)
+            h, g = (a.float() @ w.float().T + b).chunk(2, -1)
+            close_bf16(got, h * F.gelu(g))
+        else:
+            got = ops.gemm(a, w, bias=b, act=ops.ACT_SILU if epi == "silu" else ops.ACT_NONE)
+            want = a.float() @ w.float().T + (b if b is not None else 0)
+            close_bf16(got, F.silu(want) if epi == "silu" else want)
     finally:
         lib().vd_gemm_select_path(0)
 

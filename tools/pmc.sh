@@ -1,13 +1,13 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run; never combined with trace domains)
-# usage: bash tools/pmc.sh <outdir> <kbench filter>
+# usage: KB_PATHS=v2,v4 bash tools/pmc.sh <outdir> <kbench filter>
 R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out/$1; shift
-mkdir -p $OUT; cd /tmp && export TMPDIR=/tmp KB_PATHS=v2
+mkdir -p $OUT; cd /tmp && export TMPDIR=/tmp KB_PATHS=${KB_PATHS:-v2}
 i=0
 for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM SQ_INSTS_SALU" \
-           "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
+           "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE" ${PMC_EXTRA}; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o p -- python3 $R/tools/kbench.py "$@" > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+  timeout -k 10 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o p -- python3 $R/tools/kbench.py "$@" > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -3 $OUT/p$i.log; exit 1; }
 done
 echo done

@@ -38,16 +38,12 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
   const int M = (int)d.M, N = (int)d.N;
   const int fr = lane & 15, fq = lane >> 4;
   const int nw = nbase;
-  int mrow[MB];
-  bool mok[MB];
-  const float* rbrow[MB];
-#pragma unroll
-  for (int b = 0; b < MB; ++b) {
-    const int m = mbase + b * 16 + fr;
-    mok[b] = m < M;
-    mrow[b] = mok[b] ? m : 0;
-    rbrow[b] = d.rowbias ? d.rowbias + (int64_t)(mrow[b] / (int)d.rb_div) * d.ld_rb : nullptr;
-  }
+  // per-row values are recomputed inside each loop (arrays of MB row pointers kept
+  // live across the whole epilogue cost 3 x MB VGPRs beside MB x NB x 4 accumulators)
+#define VD_EPI_ROW(b)                                       \
+  const int m_ = mbase + (b) * 16 + fr;                     \
+  const bool mok_ = m_ < M;                                 \
+  const int mrow_ = mok_ ? m_ : 0;
   // Wide path (T21 for the 16x16 layout): v_permlane16_swap of 16-column blocks
   // (a, a+1) leaves each lane 8 CONSECUTIVE channels — lane group g of the pair
   // holds columns 16a + 16(g&1) + 8(g>>1) .. +7 — so residual loads and bf16
@@ -77,6 +73,7 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
           const int nout = nw / 2 + (a / 2) * 16 + wcol;
 #pragma unroll
           for (int b = 0; b < MB; ++b) {
+            VD_EPI_ROW(b)
             uint32_t x[2], y[2];
 #pragma unroll
             for (int h2 = 0; h2 < 2; ++h2) {
@@ -90,8 +87,8 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
               x[h2] = r[0];
               y[h2] = r[1];
             }
-            if (mok[b] && 2 * nout < N)
-              *(uint4*)(out + (uint32_t)(mrow[b] * (int)d.ldc + nout)) = make_uint4(x[0], x[1], y[0], y[1]);
+            if (mok_ && 2 * nout < N)
+              *(uint4*)(out + (uint32_t)(mrow_ * (int)d.ldc + nout)) = make_uint4(x[0], x[1], y[0], y[1]);
           }
         }
         return;
@@ -114,11 +111,12 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
         }
 #pragma unroll
         for (int b = 0; b < MB; ++b) {
-          if (!mok[b]) continue;
+          VD_EPI_ROW(b)
+          if (!mok_) continue;
           float o[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) o[j] = (acc[a][b][j] + bh[j]) * gelu_erf(acc[a + 1][b][j] + bg[j]);
-          *(uint2*)(out + (uint32_t)(mrow[b] * (int)d.ldc + nout)) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          *(uint2*)(out + (uint32_t)(mrow_ * (int)d.ldc + nout)) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
         }
       }
     }
@@ -139,6 +137,7 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
       }
 #pragma unroll
       for (int b = 0; b < MB; ++b) {
+        VD_EPI_ROW(b)
         float o[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -147,9 +146,10 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
           o[j] = __uint_as_float(r[0]) + bv[j];
           o[4 + j] = __uint_as_float(r[1]) + bv[4 + j];
         }
-        if (!mok[b] || !nok) continue;
+        if (!mok_ || !nok) continue;
         if (d.rowbias) {
-          const float4 t0 = *(const float4*)(rbrow[b] + n), t1 = *(const float4*)(rbrow[b] + n + 4);
+          const float* rbrow = d.rowbias + (int64_t)(mrow_ / (int)d.rb_div) * d.ld_rb;
+          const float4 t0 = *(const float4*)(rbrow + n), t1 = *(const float4*)(rbrow + n + 4);
           o[0] += t0.x; o[1] += t0.y; o[2] += t0.z; o[3] += t0.w;
           o[4] += t1.x; o[5] += t1.y; o[6] += t1.z; o[7] += t1.w;
         }
@@ -159,11 +159,11 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
         }
         if (d.res) {
           float rf[8];
-          unpack8(*(const uint4*)((const bf16_t*)d.res + (uint32_t)(mrow[b] * (int)d.ld_res + n)), rf);
+          unpack8(*(const uint4*)((const bf16_t*)d.res + (uint32_t)(mrow_ * (int)d.ld_res + n)), rf);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += rf[j];
         }
-        *(uint4*)(out + (uint32_t)(mrow[b] * (int)d.ldc + n)) = pack8(o);
+        *(uint4*)(out + (uint32_t)(mrow_ * (int)d.ldc + n)) = pack8(o);
       }
     }
     if constexpr (NB % 2 == 0) return;
@@ -180,12 +180,13 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
     }
 #pragma unroll
     for (int b = 0; b < MB; ++b) {
-      if (!mok[b]) continue;
+      VD_EPI_ROW(b)
+      if (!mok_) continue;
       float o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = acc[a][b][j] + bv[j];
       if (d.rowbias) {
-        const float4 t = *(const float4*)(rbrow[b] + n);
+        const float4 t = *(const float4*)(d.rowbias + (int64_t)(mrow_ / (int)d.rb_div) * d.ld_rb + n);
         o[0] += t.x; o[1] += t.y; o[2] += t.z; o[3] += t.w;
       }
       if (d.act == VD_ACT_SILU) {
@@ -193,10 +194,10 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
         for (int j = 0; j < 4; ++j) o[j] = silu_f(o[j]);
       }
       if (d.res) {
-        const uint2 r = *(const uint2*)((const bf16_t*)d.res + (uint32_t)(mrow[b] * (int)d.ld_res + n));
+        const uint2 r = *(const uint2*)((const bf16_t*)d.res + (uint32_t)(mrow_ * (int)d.ld_res + n));
         o[0] += bf_lo(r.x); o[1] += bf_hi(r.x); o[2] += bf_lo(r.y); o[3] += bf_hi(r.y);
       }
-      const uint32_t off = (uint32_t)(mrow[b] * (int)d.ldc + n);
+      const uint32_t off = (uint32_t)(mrow_ * (int)d.ldc + n);
       if (d.out_f32) {
         *(float4*)((float*)d.out + off) = make_float4(o[0], o[1], o[2], o[3]);
       } else {
@@ -205,6 +206,8 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
     }
   }
 }
+
+#undef VD_EPI_ROW
 
 template <int BM, int BN, int MODE>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
@@ -792,6 +795,429 @@ __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, u
   }
 }
 
+// ============================================================================ v5
+// Persistent 256 x 320 GEMM / implicit-GEMM conv, BK = 32, 8 waves as 4(M) x 2(N)
+// (64 x 160 per wave: 4 x 10 accumulators of 16x16), 4-stage LDS-DMA ring (36 KiB per
+// stage, three k-steps in flight), persistent strided unit walk as v2.  320 divides
+// every N of the UNet (320 ... 10240): no padding.  One raw s_barrier per k-step behind
+// a counted vmcnt; the DMA for k-step it+3 goes out right after the barrier of k-step
+// it into the stage read at it-1.  Load-free epilogue (epi_fast) where it applies: the
+// stores stay in flight across the next k-steps' counted waits.
+// Measured against v2/v3 (tools/kbench.py): wins on the L1 attention QKV
+// projection (M 131072, K 320, N 960: 145 vs 169 us), ties or loses elsewhere — the
+// k-loop is bound by LDS-read / MFMA phase lock of the two waves on each SIMD and by
+// the DMA of 64-B row segments, which neither two workgroups per CU, a dedicated
+// L2-prefetch wave nor a two-group ping-pong schedule (all built and measured this
+// round) removed.
+// LDS operand image: rows of 64 B (4 chunks of 16 B); logical chunk c of row r
+// sits in physical chunk c ^ ((r >> 2) & 2), which makes the 16x16x32 fragment
+// reads (ds_read_b128: 16-lane groups over rows 0-3/12-15 and 4-11) conflict
+// free.  The permutation is applied to the per-lane DMA SOURCE address, the
+// image stays lane-linear (cdna_hip_programming.md rule 21).
+constexpr int G4_BM = 256, G4_BK = 32;
+
+template <int BN, int WM, int WN, int STAGES>
+struct G4 {
+  static constexpr int NT = WM * WN * 64;
+  static constexpr int NW = WM * WN;
+  static constexpr int A_BYTES = G4_BM * G4_BK * 2;  // 16 KiB
+  static constexpr int B_BYTES = BN * G4_BK * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int NPA = G4_BM / 16;             // A DMA pieces (16 rows x 64 B = 1 KiB) per k-step
+  static constexpr int NPB = BN / 16;                // W DMA pieces per k-step
+  // wave w issues A pieces w + NW*j (j < NAMAX) and W pieces w + NW*j (j < NBMAX)
+  static constexpr int NAMAX = (NPA + NW - 1) / NW;
+  static constexpr int NBMAX = (NPB + NW - 1) / NW;
+  static constexpr int WROWS = G4_BM / WM, WCOLS = BN / WN;
+  static constexpr int MB = WROWS / 16, NB = WCOLS / 16;
+  // a ring of 4 per-unit bias slots (2 KiB each: two 1-KiB DMA pieces) for epi_fast
+  static constexpr int BIAS_SLOTS = 4;
+  static constexpr int LDS_BYTES = STAGES * STAGE + BIAS_SLOTS * 2048;
+  static_assert(BN % (16 * WN) == 0 && G4_BM % (16 * WM) == 0, "tile / wave grid mismatch");
+};
+
+__device__ __forceinline__ uint32_t g4_off(int row, int chunk) {  // byte offset in an operand image
+  return (uint32_t)(row * 64 + ((chunk ^ ((row >> 2) & 2)) << 4));
+}
+
+// s_waitcnt vmcnt(n) (expcnt / lgkmcnt left at max) for a wave-uniform runtime n;
+// n > 63 waits for 63 (more than asked: always safe).
+template <int N>
+__device__ __forceinline__ void s_wait_vm() {
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+__device__ __forceinline__ void wait_vm_rt(int n) {
+#define VM4(B) case B: s_wait_vm<B>(); break; case B + 1: s_wait_vm<B + 1>(); break; \
+               case B + 2: s_wait_vm<B + 2>(); break; case B + 3: s_wait_vm<B + 3>(); break;
+  switch (n) {
+    VM4(0) VM4(4) VM4(8) VM4(12) VM4(16) VM4(20) VM4(24) VM4(28)
+    VM4(32) VM4(36) VM4(40) VM4(44) VM4(48) VM4(52) VM4(56) VM4(60)
+    default: s_wait_vm<63>(); break;
+  }
+#undef VM4
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// Load-free epilogue (v5, split == 1, bf16 out, no residual / row bias): the bias
+// comes from the unit's LDS slot (DMA'd with its first k-step) and every store is
+// an UNCONDITIONAL buffer store whose out-of-range lanes carry an offset past the
+// resource's num_records (dropped by the hardware).  So the epilogue issues no
+// vector-memory load — nothing makes the wave wait for the k-steps still in flight
+// — and a compile-time number of stores, which the k-loop's counted vmcnt then
+// leaves outstanding instead of draining.  Returns that number.
+template <int MB, int NB>
+__device__ __forceinline__ int epi_fast(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], int mbase, int nbase, int lane,
+                                        const float* bsl, int n0, __amdgpu_buffer_rsrc_t ro) {
+  static_assert(NB % 2 == 0, "epi_fast: whole 16-column pairs");
+  const int M = (int)d.M, N = (int)d.N, ldc = (int)d.ldc;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int wcol = 16 * (fq & 1) + 8 * (fq >> 1);
+  int nst = 0;
+  if (d.act == VD_ACT_GEGLU) {
+    // pairs (a, a+1) = (hidden, gate) blocks -> 16 output columns; pair-pairs swapped
+    // by permlane16 into 8 consecutive columns per lane (16-B stores), a lone last
+    // pair stores 4 columns (8 B)
+    constexpr int NP = NB / 2;
+#pragma unroll
+    for (int pp = 0; pp + 1 < NP; pp += 2) {
+      const int a = 2 * pp;
+      const int c0 = nbase - n0 + a * 16 + 4 * fq;  // column of acc[a][.][0] inside the tile
+      const float4 th0 = *(const float4*)(bsl + c0), tg0 = *(const float4*)(bsl + c0 + 16);
+      const float4 th1 = *(const float4*)(bsl + c0 + 32), tg1 = *(const float4*)(bsl + c0 + 48);
+      const float bh0[4] = {th0.x, th0.y, th0.z, th0.w}, bg0[4] = {tg0.x, tg0.y, tg0.z, tg0.w};
+      const float bh1[4] = {th1.x, th1.y, th1.z, th1.w}, bg1[4] = {tg1.x, tg1.y, tg1.z, tg1.w};
+      const int nout = nbase / 2 + pp * 16 + wcol;
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        const int m = mbase + b * 16 + fr;
+        uint32_t x[2], y[2];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const float o0 = (acc[a][b][2 * h2] + bh0[2 * h2]) * gelu_erf(acc[a + 1][b][2 * h2] + bg0[2 * h2]);
+          const float o1 = (acc[a][b][2 * h2 + 1] + bh0[2 * h2 + 1]) * gelu_erf(acc[a + 1][b][2 * h2 + 1] + bg0[2 * h2 + 1]);
+          const float p0 = (acc[a + 2][b][2 * h2] + bh1[2 * h2]) * gelu_erf(acc[a + 3][b][2 * h2] + bg1[2 * h2]);
+          const float p1 = (acc[a + 2][b][2 * h2 + 1] + bh1[2 * h2 + 1]) * gelu_erf(acc[a + 3][b][2 * h2 + 1] + bg1[2 * h2 + 1]);
+          auto r = __builtin_amdgcn_permlane16_swap(pack2(o0, o1), pack2(p0, p1), false, false);
+          x[h2] = r[0];
+          y[h2] = r[1];
+        }
+        const bool ok = m < M && 2 * nout < N;
+        const uint32_t off = ok ? (uint32_t)(m * ldc + nout) * 2u : G2_OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{x[0], x[1], y[0], y[1]}, ro, off, 0, 0);
+        ++nst;
+      }
+    }
+    if constexpr (NP % 2 == 1) {
+      const int a = NB - 2;
+      const int c0 = nbase - n0 + a * 16 + 4 * fq;
+      const float4 th = *(const float4*)(bsl + c0), tg = *(const float4*)(bsl + c0 + 16);
+      const float bh[4] = {th.x, th.y, th.z, th.w}, bg[4] = {tg.x, tg.y, tg.z, tg.w};
+      const int nout = nbase / 2 + (a / 2) * 16 + 4 * fq;
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        const int m = mbase + b * 16 + fr;
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (acc[a][b][j] + bh[j]) * gelu_erf(acc[a + 1][b][j] + bg[j]);
+        const bool ok = m < M && 2 * nout < N;
+        const uint32_t off = ok ? (uint32_t)(m * ldc + nout) * 2u : G2_OOB;
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])}, ro, off, 0, 0);
+        ++nst;
+      }
+    }
+    return nst;
+  }
+#pragma unroll
+  for (int a = 0; a < NB; a += 2) {
+    const int n = nbase + a * 16 + wcol;  // first of this lane's 8 columns after the swap
+    const float4 t0 = *(const float4*)(bsl + (n - n0)), t1 = *(const float4*)(bsl + (n - n0) + 4);
+    const float bv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      const int m = mbase + b * 16 + fr;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[a][b][j]), __float_as_uint(acc[a + 1][b][j]),
+                                                  false, false);
+        o[j] = __uint_as_float(r[0]) + bv[j];
+        o[4 + j] = __uint_as_float(r[1]) + bv[4 + j];
+      }
+      if (d.act == VD_ACT_SILU) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = silu_f(o[j]);
+      }
+      const uint4 pk = pack8(o);
+      const bool ok = m < M && n < N;
+      const uint32_t off = ok ? (uint32_t)(m * ldc + n) * 2u : G2_OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{pk.x, pk.y, pk.z, pk.w}, ro, off, 0, 0);
+      ++nst;
+    }
+  }
+  return nst;
+}
+
+template <int BN, int WM, int WN, int STAGES, int MODE>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_waves_per_eu(2))) void gemm4_kernel(
+    const vd_gemm_desc d, uint32_t a0_bytes, uint32_t a1_bytes, uint32_t w_bytes, int split) {
+  using C = G4<BN, WM, WN, STAGES>;
+  __shared__ __attribute__((aligned(1024))) char smem[C::LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int64_t M = d.M, N = d.N, K = d.K;
+  const int tiles_n = (int)((N + BN - 1) / BN);
+  const int tiles_m = (int)((M + G4_BM - 1) / G4_BM);
+  const int units = tiles_n * tiles_m * split;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);  // see v2: XCD-contiguous strided walk
+  const int G = gridDim.x;
+  const int nk_all = (int)(K / G4_BK);
+
+  const int rb = lane >> 2;                                               // row within the 16-row DMA piece
+  const uint32_t lc16 = (uint32_t)(((lane & 3) ^ ((rb >> 2) & 2)) * 16);  // logical source chunk (bytes)
+  const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)d.a0, 0, a0_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ra1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(d.a1 ? d.a1 : d.a0), 0, d.a1 ? a1_bytes : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, w_bytes, 0x00020000);
+  // this wave's pieces per k-step
+  const int na_w = (C::NPA - wid + C::NW - 1) / C::NW;
+  const int nb_w = (C::NPB - wid + C::NW - 1) / C::NW;
+  const int per_step = na_w + nb_w;
+  const int cin = MODE == VD_A_CONV3X3 ? (int)(K / 9) : 0;
+  const int hgrid = d.upsample ? 2 * d.h_in : d.h_in;
+  const int wgrid = d.upsample ? 2 * d.w_in : d.w_in;
+  // load-free epilogue (epi_fast) for plain bf16 outputs
+  const bool fast = split == 1 && !d.res && !d.rowbias && !d.out_f32 && (N % 8) == 0 &&
+                    (d.ldc % 8) == 0 && (((uintptr_t)d.out) & 15) == 0;
+  const __amdgpu_buffer_rsrc_t rbias = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(d.bias ? d.bias : (const float*)d.a0), 0, d.bias ? (uint32_t)(N * 4) : 0u, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rout =
+      __builtin_amdgcn_make_buffer_rsrc(d.out, 0, (uint32_t)(M * d.ldc * 2), 0x00020000);
+  int iun = 0, cun = 0;  // per-workgroup unit ordinals of the issue and compute cursors (bias slot)
+
+  // ---- issue cursor: the (unit, k-step) whose DMA goes out next
+  int iu = lid, ikt = 0, ikt1 = 0;
+  uint32_t boff[C::NBMAX], aoff0[C::NAMAX], aoff1[C::NAMAX];
+  // conv rows: base pixel of the row's image and its (oh, ow) packed 16:16
+  int pimg[C::NAMAX], pohw[C::NAMAX];
+  int c_tap = 0, c_ci = 0;
+  bool c_new = true;
+  auto unit_kr = [&](int u, int& kt0, int& kt1) {
+    const int sp = u % split;
+    kt0 = (int)((int64_t)nk_all * sp / split);
+    kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
+  };
+  auto setup_unit = [&](int u) {
+    const int tile = u / split;
+    const int64_t m0 = (int64_t)(tile / tiles_n) * G4_BM, n0 = (int64_t)(tile % tiles_n) * BN;
+    int kt0;
+    unit_kr(u, kt0, ikt1);
+    ikt = kt0;
+#pragma unroll
+    for (int j = 0; j < C::NBMAX; ++j) {
+      int64_t n = n0 + (wid + C::NW * j) * 16 + rb;
+      n = n < N ? n : N - 1;
+      boff[j] = (uint32_t)(n * d.ldw * 2) + lc16;
+    }
+    if constexpr (MODE == VD_A_DENSE) {
+#pragma unroll
+      for (int j = 0; j < C::NAMAX; ++j) {
+        int64_t m = m0 + (wid + C::NW * j) * 16 + rb;
+        m = m < M ? m : M - 1;
+        aoff0[j] = (uint32_t)(m * d.lda0 * 2) + lc16;
+        aoff1[j] = (uint32_t)(m * d.lda1 * 2) + lc16;
+      }
+    } else {
+      const int hw = d.h_out * d.w_out;
+#pragma unroll
+      for (int j = 0; j < C::NAMAX; ++j) {
+        int64_t m = m0 + (wid + C::NW * j) * 16 + rb;
+        m = m < M ? m : M - 1;
+        const int img = (int)(m / hw);
+        const int p = (int)(m - (int64_t)img * hw);
+        const int oh = p / d.w_out;
+        pimg[j] = img * d.h_in * d.w_in;
+        pohw[j] = (oh << 16) | (p - oh * d.w_out);
+      }
+      c_tap = kt0 * G4_BK / cin;
+      c_ci = kt0 * G4_BK - c_tap * cin;
+      c_new = true;
+    }
+  };
+  auto issue = [&](int stage) {  // DMA of the cursor's k-step into `stage`, then advance the cursor
+    char* la = smem + stage * C::STAGE;
+    char* lb = la + C::A_BYTES;
+    const int kb = ikt * G4_BK;
+    {
+      if (fast && wid == 0 && ikt == (int)((int64_t)nk_all * (iu % split) / split)) {
+        // first k-step of a unit: its BN bias values (zeros past N or without bias) into slot iun & 3
+        char* bs = smem + STAGES * C::STAGE + (iun & (C::BIAS_SLOTS - 1)) * 2048;
+        const uint32_t nb0 = (uint32_t)((iu / split) % tiles_n) * BN * 4 + lane * 16;
+        dma16(rbias, bs, nb0);
+        dma16(rbias, bs + 1024, nb0 + 1024);
+      }
+      if constexpr (MODE == VD_A_DENSE) {
+        const bool s0 = kb < d.k0;
+        const uint32_t koff = (uint32_t)(s0 ? kb : kb - (int)d.k0) * 2;
+#pragma unroll
+        for (int j = 0; j < C::NAMAX; ++j)
+          if (j < na_w) dma16(s0 ? ra0 : ra1, la + (wid + C::NW * j) * 1024, (s0 ? aoff0[j] : aoff1[j]) + koff);
+      } else {
+        if (c_new) {  // new tap: recompute the rows' pixel offsets
+          c_new = false;
+          const int dy = c_tap / 3, dx = c_tap - 3 * dy;
+#pragma unroll
+          for (int j = 0; j < C::NAMAX; ++j) {
+            int ih = (pohw[j] >> 16) * d.stride + dy - 1, iw = (pohw[j] & 0xffff) * d.stride + dx - 1;
+            const bool ok = ih >= 0 && ih < hgrid && iw >= 0 && iw < wgrid;
+            ih >>= d.upsample;
+            iw >>= d.upsample;
+            const uint32_t pix = (uint32_t)(pimg[j] + ih * d.w_in + iw);
+            aoff0[j] = ok ? pix * (uint32_t)(d.lda0 * 2) + lc16 : G2_OOB;
+            aoff1[j] = ok ? pix * (uint32_t)(d.lda1 * 2) + lc16 : G2_OOB;
+          }
+        }
+        const bool s0 = c_ci < d.k0;
+        const uint32_t coff = (uint32_t)(s0 ? c_ci : c_ci - (int)d.k0) * 2;
+#pragma unroll
+        for (int j = 0; j < C::NAMAX; ++j) {
+          const uint32_t o = s0 ? aoff0[j] : aoff1[j];
+          if (j < na_w) dma16(s0 ? ra0 : ra1, la + (wid + C::NW * j) * 1024, o == G2_OOB ? G2_OOB : o + coff);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < C::NBMAX; ++j)
+        if (j < nb_w) dma16(rw, lb + (wid + C::NW * j) * 1024, boff[j] + (uint32_t)kb * 2);
+    }
+    if constexpr (MODE == VD_A_CONV3X3) {
+      c_ci += G4_BK;
+      if (c_ci == cin) { c_ci = 0; ++c_tap; c_new = true; }
+    }
+    if (++ikt == ikt1) {
+      ++iun;
+      if ((iu += G) < units) setup_unit(iu);
+    }
+  };
+
+  f32x4 acc[C::NB][C::MB];
+#pragma unroll
+  for (int a = 0; a < C::NB; ++a)
+#pragma unroll
+    for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int n_it = 0;
+  for (int u = lid; u < units; u += G) {
+    int a0_, a1_;
+    unit_kr(u, a0_, a1_);
+    n_it += a1_ - a0_;
+  }
+  if (n_it == 0) return;
+  setup_unit(lid);
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < n_it) issue(s);
+  const int fr = lane & 15, fq = lane >> 4;
+  const uint32_t wlane = C::A_BYTES + g4_off(wn * C::WCOLS + fr, fq);
+  const uint32_t xlane = g4_off(wm * C::WROWS + fr, fq);
+  int cu = lid, ckt, ckt1;
+  unit_kr(cu, ckt, ckt1);
+  int stage = 0;
+  int st1 = 0, st2 = 0, st3 = 0;  // epilogue stores issued 1, 2, 3 iterations ago (still younger than k-step it's DMA)
+  for (int it = 0; it < n_it; ++it) {
+    // this wave's DMA for k-step `it` has landed once only the younger k-steps' (at
+    // most S-2 of them) remain outstanding, plus the epilogue stores issued since
+    // k-step it's DMA went out (iterations it-S+1 .. it-1); the barrier then publishes
+    // every wave's part and certifies that stage (it-1)%S, the target of the next
+    // issue, is no longer read.
+    {
+      const int younger = n_it - 1 - it < STAGES - 2 ? n_it - 1 - it : STAGES - 2;
+      const int pend = st1 + (STAGES >= 3 ? st2 : 0) + (STAGES >= 4 ? st3 : 0);
+      wait_vm_rt(younger * per_step + pend);
+    }
+    st3 = st2;
+    st2 = st1;
+    st1 = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (it + STAGES - 1 < n_it) issue(stage == 0 ? STAGES - 1 : stage - 1);
+    const char* sbase = smem + stage * C::STAGE;
+    if constexpr (C::MB == 8) {
+      // W once, X in two halves of 4 (caps the live fragment registers)
+      bf16x8 wf[C::NB], xf[4];
+#pragma unroll
+      for (int a = 0; a < C::NB; ++a) wf[a] = *(const bf16x8*)(sbase + wlane + a * 1024);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) xf[b] = *(const bf16x8*)(sbase + xlane + (4 * h + b) * 1024);
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int a = 0; a < C::NB; ++a)
+            acc[a][4 * h + b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][4 * h + b], 0, 0, 0);
+      }
+    } else {
+      // X once, W in two halves
+      constexpr int HN = (C::NB + 1) / 2;
+      bf16x8 xf[C::MB], wf[HN];
+#pragma unroll
+      for (int b = 0; b < C::MB; ++b) xf[b] = *(const bf16x8*)(sbase + xlane + b * 1024);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int a = 0; a < HN; ++a)
+          if (h * HN + a < C::NB) wf[a] = *(const bf16x8*)(sbase + wlane + (h * HN + a) * 1024);
+#pragma unroll
+        for (int a = 0; a < HN; ++a)
+          if (h * HN + a < C::NB)
+#pragma unroll
+            for (int b = 0; b < C::MB; ++b)
+              acc[h * HN + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[h * HN + a][b], 0, 0, 0);
+      }
+    }
+    if (++ckt == ckt1) {  // unit finished: epilogue
+      const int tile = cu / split, sp = cu % split;
+      const int64_t m0 = (int64_t)(tile / tiles_n) * G4_BM, n0 = (int64_t)(tile % tiles_n) * BN;
+      bool done = false;
+      {
+        if (fast) {
+          const float* bsl = (const float*)(smem + STAGES * C::STAGE + (cun & (C::BIAS_SLOTS - 1)) * 2048);
+          st1 = epi_fast<C::MB, C::NB>(d, acc, (int)m0 + wm * C::WROWS, (int)n0 + wn * C::WCOLS, lane, bsl,
+                                       (int)n0, rout);
+          done = true;
+        }
+      }
+      if (!done) {
+        if (split == 1) {
+          gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::WROWS, (int)n0 + wn * C::WCOLS, lane);
+        } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
+          float* slab = (float*)d.ws + (int64_t)sp * M * N;
+#pragma unroll
+          for (int a = 0; a < C::NB; ++a) {
+            const int64_t n = n0 + wn * C::WCOLS + a * 16 + 4 * fq;
+            if (n >= N) continue;
+#pragma unroll
+            for (int b = 0; b < C::MB; ++b) {
+              const int64_t m = m0 + wm * C::WROWS + b * 16 + fr;
+              if (m < M)
+                *(float4*)(slab + m * N + n) = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < C::NB; ++a)
+#pragma unroll
+        for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ++cun;
+      if ((cu += G) < units) unit_kr(cu, ckt, ckt1);
+    }
+    stage = stage == STAGES - 1 ? 0 : stage + 1;
+  }
+}
+
 // Sum the split-K slabs and apply the GEMM epilogue (4 output columns per thread).
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, int split) {
   const int64_t M = d.M, N = d.N;
@@ -879,6 +1305,28 @@ int launch(const vd_gemm_desc& d, hipStream_t s) {
   return vd_launch_status();
 }
 
+template <int BN, int WM, int WN, int STAGES>
+int launch4(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
+  using C = G4<BN, WM, WN, STAGES>;
+  const int64_t units = ((d.M + G4_BM - 1) / G4_BM) * ((d.N + BN - 1) / BN) * split;
+  // persistent: one workgroup per CU, ceil(units / grid) rounds, balanced grid
+  const int64_t slots = (int64_t)g_num_cus;
+  const int64_t rounds = (units + slots - 1) / slots;
+  const int64_t grid = (units + rounds - 1) / rounds;
+  if (d.a_mode == VD_A_CONV3X3)
+    hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_CONV3X3>), dim3((unsigned)grid), dim3(C::NT), 0,
+                       s, d, a0b, a1b, wb, split);
+  else
+    hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_DENSE>), dim3((unsigned)grid), dim3(C::NT), 0, s,
+                       d, a0b, a1b, wb, split);
+  int rc = vd_launch_status();
+  if (rc != VD_OK || split == 1) return rc;
+  const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
+  const int64_t blocks = (work + 255) / 256;
+  hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, d, split);
+  return vd_launch_status();
+}
+
 int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
   const int64_t units = ((d.M + G3_BM - 1) / G3_BM) * ((d.N + G3_BN - 1) / G3_BN) * split;
   if (units > 0x7fffffff) return VD_EINVAL;
@@ -893,7 +1341,7 @@ int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
-int g_path = 0;  // 0 auto, 1 v1, 2 v2, 3 v3 (tests / benchmarks)
+int g_path = 0;  // 0 auto, 1 v1, 2 v2, 3 v3, 5 v5 (tests / benchmarks)
 
 struct Plan {
   int ver = 1;
@@ -915,11 +1363,27 @@ inline int split_for(int64_t tiles, int64_t nk) {
 // the 256 CUs.
 Plan plan(const vd_gemm_desc& d) {
   Plan p;
-  if (g_path == 1 || d.K % BK || d.k0 % BK || d.M < G2_BM || d.N < 64) return p;
+  if (g_path == 1 || d.K % G4_BK || d.k0 % G4_BK || d.M < G2_BM || d.N < 64) return p;
   const int64_t a_rows = d.a_mode == VD_A_CONV3X3 ? (int64_t)d.n_img * d.h_in * d.w_in : d.M;
   const int64_t a0b = a_rows * d.lda0 * 2, a1b = d.a1 ? a_rows * d.lda1 * 2 : 0, wb = d.N * d.ldw * 2;
   if (a0b >= (int64_t)G2_OOB || a1b >= (int64_t)G2_OOB || wb >= (int64_t)G2_OOB) return p;
   p.a0b = (uint32_t)a0b; p.a1b = (uint32_t)a1b; p.wb = (uint32_t)wb;
+  const bool cin32 = d.a_mode != VD_A_CONV3X3 || (d.K / 9) % G4_BK == 0;
+  const bool k64 = d.K % BK == 0 && d.k0 % BK == 0 && (d.a_mode != VD_A_CONV3X3 || (d.K / 9) % BK == 0);
+  // v5 (256 x 320, BK 32): forced, where K or k0 is not a multiple of 64, and on the shape
+  // it wins (tools/kbench.py: the L1 attention QKV projection M 131072 x N 960 x K 320)
+  const bool v5auto = d.a_mode == VD_A_DENSE && d.M >= 65536 && d.K <= 320 && d.N % 320 == 0 && d.N >= 640 &&
+                      d.N < 2560 && !d.res && !d.rowbias && d.act != VD_ACT_GEGLU;
+  if (g_path == 5 || (g_path == 0 && (!k64 || v5auto))) {
+    if (!cin32) return p;
+    p.ver = 5;
+    p.bn = 320;
+    const int64_t tiles = ((d.M + G4_BM - 1) / G4_BM) * ((d.N + 319) / 320);
+    p.split = split_for(tiles, d.K / BK);
+    p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 : 0;
+    return p;
+  }
+  if (!k64) return p;
   const int64_t nk = d.K / BK;
   const bool v3ok = d.a_mode == VD_A_DENSE && d.N >= 256 && g_path != 2;
   const int64_t p256 = (d.N + 255) / 256 * 256;
@@ -952,7 +1416,7 @@ extern "C" int vd_gemm_force_v1(int32_t on) {
   return VD_OK;
 }
 extern "C" int vd_gemm_select_path(int32_t path) {
-  if (path < 0 || path > 3) return VD_EINVAL;
+  if (path < 0 || path > 5 || path == 4) return VD_EINVAL;
   g_path = path;
   return VD_OK;
 }
@@ -1002,6 +1466,7 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   const Plan p = plan(d);
   if (p.ver >= 2 && p.split > 1) VD_CHECK_ARG(d.ws && al16(d.ws) && d.ws_bytes >= p.ws_bytes);
   if (p.ver == 3) return launch3(d, s, p.a0b, p.a1b, p.wb, p.split);
+  if (p.ver == 5) return launch4<320, 4, 2, 4>(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 2)
     return p.bn == 160 ? launch2<160>(d, s, p.a0b, p.a1b, p.wb, p.split)
                        : launch2<128>(d, s, p.a0b, p.a1b, p.wb, p.split);
