@@ -98,11 +98,11 @@ def test_gemm_geglu(cuda):
 
 
 # ---------------------------------------------------------------- v2 (LDS-DMA) paths
-@pytest.fixture(params=["v5", "v3", "v2", "v1"])
+@pytest.fixture(params=["v6", "v5", "v3", "v2", "v1"])
 def gemm_path(request, cuda):
     """Force one GEMM kernel (v3 only takes dense A; other shapes fall back to auto)."""
     from vdiff._lib import lib
-    lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5}[request.param])
+    lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6}[request.param])
     yield request.param
     lib().vd_gemm_select_path(0)
 
@@ -189,6 +189,62 @@ def test_gemm_v5_load_free_epilogue(cuda, path, M, N, K, epi):
             got = ops.gemm(a, w, bias=b, act=ops.ACT_SILU if epi == "silu" else ops.ACT_NONE)
             want = a.float() @ w.float().T + (b if b is not None else 0)
             close_bf16(got, F.silu(want) if epi == "silu" else want)
+    finally:
+        lib().vd_gemm_select_path(0)
+
+
+@pytest.mark.parametrize("M,N,K,kind", [(256, 1280, 1280, "res"), (1024, 1280, 5120, "rowbias"), (100, 320, 2560, "silu"),
+                                       (256, 2560, 1280, "geglu"), (4096, 640, 640, "f32"), (64, 1280, 23040, "res")])
+def test_gemm_v6_small_m_splitk(cuda, M, N, K, kind):
+    """v6 (64 x 64 tiles, split K reduced in-kernel by the last-arriving K-slice): small M
+    with long K (the split path), every epilogue flavour, and a second launch on the
+    same workspace (the counters were reset)."""
+    from vdiff._lib import lib
+    lib().vd_gemm_select_path(6)
+    try:
+        a = rnd(M, K)
+        w = rnd(N, K, std=K ** -0.5)
+        b = torch.randn(N, device=cuda)
+        x = a.float()
+        for _ in range(2):
+            if kind == "geglu":
+                got = ops.gemm(a, pack_geglu(w), bias=pack_geglu(b), act=ops.ACT_GEGLU)
+                h, g = (x @ w.float().T + b).chunk(2, -1)
+                close_bf16(got, h * F.gelu(g))
+            elif kind == "res":
+                res = rnd(M, N)
+                close_bf16(ops.gemm(a, w, bias=b, res=res), x @ w.float().T + b + res.float())
+            elif kind == "rowbias":
+                rb = torch.randn(4, N, device=cuda)
+                got = ops.gemm(a, w, bias=b, rowbias=rb, rb_div=M // 4)
+                close_bf16(got, x @ w.float().T + b + rb.repeat_interleave(M // 4, 0))
+            elif kind == "silu":
+                close_bf16(ops.gemm(a, w, bias=b, act=ops.ACT_SILU), F.silu(x @ w.float().T + b))
+            else:
+                close_f32(ops.gemm(a, w, bias=b, out_f32=True), x.double() @ w.double().T + b.double(),
+                          rtol=1e-3, atol=1e-3)
+    finally:
+        lib().vd_gemm_select_path(0)
+
+
+@pytest.mark.parametrize("case", ["l3", "l4cat"])
+def test_conv3x3_v6_splitk(cuda, case):
+    """Small-M implicit-GEMM conv on v6 with split K (L3/L4 shapes at 2 frames per GPU),
+    including the up-block channel concat."""
+    from vdiff._lib import lib
+    lib().vd_gemm_select_path(6)
+    try:
+        n, hw, c0, c1, co = (4, 16, 640, 0, 640) if case == "l3" else (4, 8, 1280, 1280, 1280)
+        x0 = rnd(n * hw * hw, c0)
+        x1 = rnd(n * hw * hw, c1) if c1 else None
+        wt = bf(torch.randn(co, c0 + c1, 3, 3, device="cuda") * (9 * (c0 + c1)) ** -0.5)
+        b = torch.randn(co, device="cuda")
+        res = rnd(n * hw * hw, co)
+        out, _, _ = ops.conv3x3(x0, n, hw, hw, pack_conv3x3(wt), x1=x1, bias=b, res=res)
+        xin = x0 if x1 is None else torch.cat([x0, x1], 1)
+        img = xin.float().reshape(n, hw, hw, -1).permute(0, 3, 1, 2)
+        want = F.conv2d(img, wt.float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, co) + res.float()
+        close_bf16(out, want)
     finally:
         lib().vd_gemm_select_path(0)
 

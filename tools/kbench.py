@@ -38,10 +38,11 @@ def report(name, us, flop, byts):
     print(f"{name:58s} {us:9.1f} us {flop / us / 1e6:8.1f} TF/s {byts / us / 1e3:8.1f} GB/s", flush=True)
 
 
+IMGS = int(__import__("os").environ.get("KB_IMGS", "32"))  # images per call (32 = 16 frames x CFG 2)
 cases = []
 # dense GEMMs (M, N, K, extra)
 for lvl, (hw, C) in enumerate([(4096, 320), (1024, 640), (256, 1280), (64, 1280)]):
-    M = 32 * hw
+    M = IMGS * hw
     cases += [(f"L{lvl+1} dense proj   M={M} N={C} K={C} +res", "dense", M, C, C, True),
               (f"L{lvl+1} dense proj   M={M} N={C} K={C} nores", "dense", M, C, C, False),
               (f"L{lvl+1} dense qkv    M={M} N={3*C} K={C}", "dense", M, 3 * C, C, False),
@@ -49,9 +50,9 @@ for lvl, (hw, C) in enumerate([(4096, 320), (1024, 640), (256, 1280), (64, 1280)
               (f"L{lvl+1} geglu        M={M} N={8*C} K={C}", "geglu", M, 8 * C, C, False)]
 cases += [("big 4096^3", "dense", 4096, 4096, 4096, False), ("big 8192^3", "dense", 8192, 8192, 8192, False),
           ("big M=32768 N=4096 K=1280", "dense", 32768, 4096, 1280, False)]
-convs = [("L1 conv 320->320", 32, 64, 320, 320), ("L2 conv 640->640", 32, 32, 640, 640),
-         ("L3 conv 1280->1280", 32, 16, 1280, 1280), ("L4 conv 1280->1280", 32, 8, 1280, 1280),
-         ("L4 conv 2560->1280", 32, 8, 2560, 1280), ("L1 conv 640->320", 32, 64, 640, 320)]
+convs = [("L1 conv 320->320", IMGS, 64, 320, 320), ("L2 conv 640->640", IMGS, 32, 640, 640),
+         ("L3 conv 1280->1280", IMGS, 16, 1280, 1280), ("L4 conv 1280->1280", IMGS, 8, 1280, 1280),
+         ("L4 conv 2560->1280", IMGS, 8, 2560, 1280), ("L1 conv 640->320", IMGS, 64, 640, 320)]
 
 for name, kind, M, N, K, res in cases:
     if flt not in name:
@@ -65,7 +66,7 @@ for name, kind, M, N, K, res in cases:
             us = timeit(lambda: torch.nn.functional.linear(a, w))
             report(f"{name} [hipblaslt]", us, 2.0 * M * N * K, 2 * (M * K + N * K + M * N))
             continue
-        lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5}[path])
+        lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6}[path])
         act = ops.ACT_GEGLU if kind == "geglu" else ops.ACT_NONE
         nout = N // 2 if kind == "geglu" else N
         out = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
@@ -88,7 +89,7 @@ for name, n, hw, ci, co in convs:
             report(f"{name} M={n*hw*hw} K={9*ci} [miopen]", us, 2.0 * n * hw * hw * co * 9 * ci,
                    2 * (n * hw * hw * (ci + co) + co * 9 * ci))
             continue
-        lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5}[path])
+        lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6}[path])
         us = timeit(lambda: ops.conv3x3(x, n, hw, hw, w, out=out))
         report(f"{name} M={n*hw*hw} K={9*ci} [{path}]", us, 2.0 * n * hw * hw * co * 9 * ci,
                2 * (n * hw * hw * (ci + co) + co * 9 * ci))

@@ -1218,6 +1218,240 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
   }
 }
 
+// ============================================================================ v6
+// Small-M GEMM / implicit-GEMM conv: tile 64 x 64, BK = 64, 4 waves as 2 x 2 (32 x 32
+// per wave), 3-stage LDS-DMA ring (48 KiB: three workgroups per CU), one workgroup
+// per (tile, K-slice) — non-persistent, so the grid fills the chip at the M of a
+// frame-sharded rank (M = 256 ... 16384 rows at 2-8 frames per GPU), where the
+// 256-row v2/v3/v5 tiles leave most CUs idle and split K into a separate reduce
+// launch.  Split K is reduced IN the kernel: every slice writes its fp32 slab, and the
+// last slice to arrive at the tile's counter sums the slabs and runs the epilogue
+// (cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2: plain slab stores
+// -> every wave s_waitcnt vmcnt(0) -> barrier -> lane 0 agent release fence + asm
+// vmcnt(0) -> relaxed agent atomic add; the last arriver: agent acquire fence + asm
+// vmcnt(0) -> barrier -> plain slab loads).  The counters live in the workspace after
+// the slabs and are zeroed by a memset node ahead of the launch; the last arriver
+// also resets its counter.
+constexpr int G6_BM = 64, G6_BN = 64, G6_NT = 256, G6_S = 3;
+constexpr int G6_A = G6_BM * BK * 2, G6_W = G6_BN * BK * 2, G6_STAGE = G6_A + G6_W;  // 8 + 8 KiB
+
+template <int MODE>
+__global__ __launch_bounds__(G6_NT, 3) void gemm6_kernel(const vd_gemm_desc d, uint32_t a0_bytes, uint32_t a1_bytes,
+                                                         uint32_t w_bytes, int split) {
+  constexpr int MB = 2, NB = 2;
+  __shared__ __attribute__((aligned(1024))) char smem[G6_S * G6_STAGE + 16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int64_t M = d.M, N = d.N, K = d.K;
+  const int tiles_n = (int)((N + G6_BN - 1) / G6_BN);
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);  // a tile's K-slices adjacent (one XCD)
+  const int tile = lid / split, sp = lid % split;
+  const int64_t m0 = (int64_t)(tile / tiles_n) * G6_BM, n0 = (int64_t)(tile % tiles_n) * G6_BN;
+  const int nk_all = (int)(K / BK);
+  const int kt0 = (int)((int64_t)nk_all * sp / split), kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
+  const int nk = kt1 - kt0;
+
+  const int rb = lane >> 3;
+  const uint32_t lc16 = (uint32_t)(((lane & 7) ^ rb) * 16);
+  const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)d.a0, 0, a0_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ra1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(d.a1 ? d.a1 : d.a0), 0, d.a1 ? a1_bytes : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, w_bytes, 0x00020000);
+  // DMA pieces: 8 rows x 128 B; A rows 16*wid + 8*j + rb, W rows the same (j = 0, 1)
+  uint32_t aoff0[2], aoff1[2], boff[2];
+  int pimg[2], pohw[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    int64_t n = n0 + 16 * wid + 8 * j + rb;
+    n = n < N ? n : N - 1;
+    boff[j] = (uint32_t)(n * d.ldw * 2) + lc16;
+    int64_t m = m0 + 16 * wid + 8 * j + rb;
+    m = m < M ? m : M - 1;
+    if constexpr (MODE == VD_A_DENSE) {
+      aoff0[j] = (uint32_t)(m * d.lda0 * 2) + lc16;
+      aoff1[j] = (uint32_t)(m * d.lda1 * 2) + lc16;
+    } else {
+      const int hw = d.h_out * d.w_out;
+      const int img = (int)(m / hw);
+      const int p = (int)(m - (int64_t)img * hw);
+      const int oh = p / d.w_out;
+      pimg[j] = img * d.h_in * d.w_in;
+      pohw[j] = (oh << 16) | (p - oh * d.w_out);
+    }
+  }
+  const int cin = MODE == VD_A_CONV3X3 ? (int)(K / 9) : 0;
+  const int hgrid = d.upsample ? 2 * d.h_in : d.h_in;
+  const int wgrid = d.upsample ? 2 * d.w_in : d.w_in;
+  int c_tap = 0, c_ci = 0, ikt = kt0;
+  bool c_new = true;
+  if constexpr (MODE == VD_A_CONV3X3) {
+    c_tap = kt0 * BK / cin;
+    c_ci = kt0 * BK - c_tap * cin;
+  }
+  auto issue = [&](int stage) __attribute__((always_inline)) {
+    char* la = smem + stage * G6_STAGE;
+    char* lb = la + G6_A;
+    const int kb = ikt * BK;
+    if constexpr (MODE == VD_A_DENSE) {
+      const bool s0 = kb < d.k0;
+      const uint32_t koff = (uint32_t)(s0 ? kb : kb - (int)d.k0) * 2;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) dma16(s0 ? ra0 : ra1, la + (2 * wid + j) * 1024, (s0 ? aoff0[j] : aoff1[j]) + koff);
+    } else {
+      if (c_new) {
+        c_new = false;
+        const int dy = c_tap / 3, dx = c_tap - 3 * dy;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          int ih = (pohw[j] >> 16) * d.stride + dy - 1, iw = (pohw[j] & 0xffff) * d.stride + dx - 1;
+          const bool ok = ih >= 0 && ih < hgrid && iw >= 0 && iw < wgrid;
+          ih >>= d.upsample;
+          iw >>= d.upsample;
+          const uint32_t pix = (uint32_t)(pimg[j] + ih * d.w_in + iw);
+          aoff0[j] = ok ? pix * (uint32_t)(d.lda0 * 2) + lc16 : G2_OOB;
+          aoff1[j] = ok ? pix * (uint32_t)(d.lda1 * 2) + lc16 : G2_OOB;
+        }
+      }
+      const bool s0 = c_ci < d.k0;
+      const uint32_t coff = (uint32_t)(s0 ? c_ci : c_ci - (int)d.k0) * 2;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t o = s0 ? aoff0[j] : aoff1[j];
+        dma16(s0 ? ra0 : ra1, la + (2 * wid + j) * 1024, o == G2_OOB ? G2_OOB : o + coff);
+      }
+      c_ci += BK;
+      if (c_ci == cin) { c_ci = 0; ++c_tap; c_new = true; }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16(rw, lb + (2 * wid + j) * 1024, boff[j] + (uint32_t)kb * 2);
+    ++ikt;
+  };
+
+  f32x4 acc[NB][MB];
+#pragma unroll
+  for (int a = 0; a < NB; ++a)
+#pragma unroll
+    for (int b = 0; b < MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) issue(0);
+  if (nk > 1) issue(1);
+  const int fr = lane & 15, fq = lane >> 4;
+  int stage = 0;
+  for (int it = 0; it < nk; ++it) {
+    if (it + 1 < nk) wait_vm<4>();  // k-step it+1's 4 pieces may stay in flight
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (it + 2 < nk) issue(stage == 0 ? 2 : stage - 1);
+    const char* sb = smem + stage * G6_STAGE;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 wf[NB], xf[MB];
+#pragma unroll
+      for (int a = 0; a < NB; ++a) wf[a] = *(const bf16x8*)(sb + G6_A + 2 * lds_off(wn * 32 + a * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int b = 0; b < MB; ++b) xf[b] = *(const bf16x8*)(sb + 2 * lds_off(wm * 32 + b * 16 + fr, ks * 4 + fq));
+#pragma unroll
+      for (int a = 0; a < NB; ++a)
+#pragma unroll
+        for (int b = 0; b < MB; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][b], 0, 0, 0);
+    }
+    stage = stage == 2 ? 0 : stage + 1;
+  }
+  const int mbase = (int)m0 + wm * 32, nbase = (int)n0 + wn * 32;
+  if (split == 1) {
+    gemm_epilogue<MB, NB>(d, acc, mbase, nbase, lane);
+    return;
+  }
+  // ---- split K: slab, arrival counter, last arriver reduces
+  float* slabs = (float*)d.ws;
+  float* slab = slabs + (int64_t)sp * M * N;
+#pragma unroll
+  for (int a = 0; a < NB; ++a) {
+    const int64_t n = nbase + a * 16 + 4 * fq;
+    if (n >= N) continue;
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      const int64_t m = mbase + b * 16 + fr;
+      if (m < M) *(float4*)(slab + m * N + n) = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* cnt = (int*)(slabs + (int64_t)split * M * N);
+  int* last_flag = (int*)(smem + G6_S * G6_STAGE);
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == split - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      cnt[tile] = 0;  // ready for the next launch (the memset node zeroes it as well)
+    }
+    *last_flag = last;
+  }
+  __syncthreads();
+  if (!*last_flag) return;
+  // 64 x 64 outputs (GEGLU: 64 x 32), 4 consecutive columns per thread-step
+  const bool geglu = d.act == VD_ACT_GEGLU;
+  const int ncol = geglu ? G6_BN / 2 : G6_BN;
+  for (int e = tid; e < G6_BM * ncol / 4; e += G6_NT) {
+    const int r = e / (ncol / 4), c4 = (e % (ncol / 4)) * 4;
+    const int64_t m = m0 + r;
+    if (m >= M) continue;
+    float o4[4];
+    if (geglu) {
+      // packed column blocks of 16: hidden block i at 32i, gate block at 32i + 16
+      const int64_t nh = n0 + (c4 / 16) * 32 + (c4 % 16), ng = nh + 16;
+      if (ng >= N) continue;
+      float h[4] = {0, 0, 0, 0}, g[4] = {0, 0, 0, 0};
+      for (int s2 = 0; s2 < split; ++s2) {
+        const float4 a4 = *(const float4*)(slabs + ((int64_t)s2 * M + m) * N + nh);
+        const float4 b4 = *(const float4*)(slabs + ((int64_t)s2 * M + m) * N + ng);
+        h[0] += a4.x; h[1] += a4.y; h[2] += a4.z; h[3] += a4.w;
+        g[0] += b4.x; g[1] += b4.y; g[2] += b4.z; g[3] += b4.w;
+      }
+      if (d.bias) {
+        const float4 a4 = *(const float4*)(d.bias + nh), b4 = *(const float4*)(d.bias + ng);
+        h[0] += a4.x; h[1] += a4.y; h[2] += a4.z; h[3] += a4.w;
+        g[0] += b4.x; g[1] += b4.y; g[2] += b4.z; g[3] += b4.w;
+      }
+      for (int j = 0; j < 4; ++j) o4[j] = h[j] * gelu_erf(g[j]);
+      const int64_t o = n0 / 2 + c4;
+      *(uint2*)((bf16_t*)d.out + m * d.ldc + o) = make_uint2(pack2(o4[0], o4[1]), pack2(o4[2], o4[3]));
+      continue;
+    }
+    const int64_t o = n0 + c4;
+    if (o >= N) continue;
+    float v[4] = {0, 0, 0, 0};
+    for (int s2 = 0; s2 < split; ++s2) {
+      const float4 a4 = *(const float4*)(slabs + ((int64_t)s2 * M + m) * N + o);
+      v[0] += a4.x; v[1] += a4.y; v[2] += a4.z; v[3] += a4.w;
+    }
+    if (d.bias) {
+      const float4 a4 = *(const float4*)(d.bias + o);
+      v[0] += a4.x; v[1] += a4.y; v[2] += a4.z; v[3] += a4.w;
+    }
+    if (d.rowbias) {
+      const float4 a4 = *(const float4*)(d.rowbias + (m / d.rb_div) * d.ld_rb + o);
+      v[0] += a4.x; v[1] += a4.y; v[2] += a4.z; v[3] += a4.w;
+    }
+    if (d.act == VD_ACT_SILU)
+      for (int j = 0; j < 4; ++j) v[j] = silu_f(v[j]);
+    if (d.res) {
+      const uint2 r2 = *(const uint2*)((const bf16_t*)d.res + m * d.ld_res + o);
+      v[0] += bf_lo(r2.x); v[1] += bf_hi(r2.x); v[2] += bf_lo(r2.y); v[3] += bf_hi(r2.y);
+    }
+    if (d.out_f32)
+      *(float4*)((float*)d.out + m * d.ldc + o) = make_float4(v[0], v[1], v[2], v[3]);
+    else
+      *(uint2*)((bf16_t*)d.out + m * d.ldc + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+  }
+}
+
 // Sum the split-K slabs and apply the GEMM epilogue (4 output columns per thread).
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, int split) {
   const int64_t M = d.M, N = d.N;
@@ -1327,6 +1561,22 @@ int launch4(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   return vd_launch_status();
 }
 
+int launch6(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
+  const int64_t tiles = ((d.M + G6_BM - 1) / G6_BM) * ((d.N + G6_BN - 1) / G6_BN);
+  if (tiles * split > 0x7fffffff) return VD_EINVAL;
+  if (split > 1) {  // arrival counters after the slabs
+    char* cnt = (char*)d.ws + (int64_t)split * d.M * d.N * 4;
+    if (hipMemsetAsync(cnt, 0, (size_t)tiles * 4, s) != hipSuccess) return vd_launch_status();
+  }
+  if (d.a_mode == VD_A_CONV3X3)
+    hipLaunchKernelGGL((gemm6_kernel<VD_A_CONV3X3>), dim3((unsigned)(tiles * split)), dim3(G6_NT), 0, s, d, a0b, a1b,
+                       wb, split);
+  else
+    hipLaunchKernelGGL((gemm6_kernel<VD_A_DENSE>), dim3((unsigned)(tiles * split)), dim3(G6_NT), 0, s, d, a0b, a1b, wb,
+                       split);
+  return vd_launch_status();
+}
+
 int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
   const int64_t units = ((d.M + G3_BM - 1) / G3_BM) * ((d.N + G3_BN - 1) / G3_BN) * split;
   if (units > 0x7fffffff) return VD_EINVAL;
@@ -1341,7 +1591,7 @@ int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
-int g_path = 0;  // 0 auto, 1 v1, 2 v2, 3 v3, 5 v5 (tests / benchmarks)
+int g_path = 0;  // 0 auto, 1 v1, 2 v2, 3 v3, 5 v5, 6 v6 (tests / benchmarks)
 
 struct Plan {
   int ver = 1;
@@ -1361,7 +1611,19 @@ inline int split_for(int64_t tiles, int64_t nk) {
 // 8-phase ping-pong) for wide dense shapes that fill the chip, v2 (256 x
 // {128,160}, persistent) otherwise; split K when the output tiles cannot fill
 // the 256 CUs.
+void read_num_cus() {  // once per process: the plan (and the workspace size) depends on it
+  static bool cus_read = false;
+  if (!cus_read) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_num_cus = n;
+    cus_read = true;
+  }
+}
+
 Plan plan(const vd_gemm_desc& d) {
+  read_num_cus();
   Plan p;
   if (g_path == 1 || d.K % G4_BK || d.k0 % G4_BK || d.M < G2_BM || d.N < 64) return p;
   const int64_t a_rows = d.a_mode == VD_A_CONV3X3 ? (int64_t)d.n_img * d.h_in * d.w_in : d.M;
@@ -1385,6 +1647,24 @@ Plan plan(const vd_gemm_desc& d) {
   }
   if (!k64) return p;
   const int64_t nk = d.K / BK;
+  // v6 (64 x 64 tiles): forced, or automatically at the small M of a frame-sharded rank
+  // (M <= 16384) where its tiles fill two workgroups per CU without splitting K (tools/
+  // kbench.py KB_IMGS=4: L1/L2 projections 17-20 -> 10-11 us, ff2 33-35 -> 27 us); with
+  // K split, and for GEGLU, v2/v3 stay faster
+  {
+    const int64_t tiles6 = ((d.M + G6_BM - 1) / G6_BM) * ((d.N + G6_BN - 1) / G6_BN);
+    const bool v6auto = d.M <= 16384 && d.act != VD_ACT_GEGLU && tiles6 >= 2 * g_num_cus;
+    if (g_path == 6 || (g_path == 0 && v6auto)) {
+      p.ver = 6;
+      p.bn = 64;
+      int64_t sp = 1;
+      // aim for >= 2 workgroups per CU, each slice >= 4 k-tiles
+      while (tiles6 * sp < 2 * g_num_cus && nk / (sp * 2) >= 4 && sp < 16) sp *= 2;
+      p.split = (int)sp;
+      p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 + ((tiles6 * 4 + 255) / 256) * 256 : 0;
+      return p;
+    }
+  }
   const bool v3ok = d.a_mode == VD_A_DENSE && d.N >= 256 && g_path != 2;
   const int64_t p256 = (d.N + 255) / 256 * 256;
   // measured (tools/kbench.py): v3 wins on the wide projections (qkv, GEGLU) once the
@@ -1416,7 +1696,7 @@ extern "C" int vd_gemm_force_v1(int32_t on) {
   return VD_OK;
 }
 extern "C" int vd_gemm_select_path(int32_t path) {
-  if (path < 0 || path > 5 || path == 4) return VD_EINVAL;
+  if (path < 0 || path > 6 || path == 4) return VD_EINVAL;
   g_path = path;
   return VD_OK;
 }
@@ -1455,17 +1735,10 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
     if (d.k0 < d.K) VD_CHECK_ARG(d.a1 != nullptr);
   }
   if (d.act == VD_ACT_GEGLU) VD_CHECK_ARG(d.N % 32 == 0 && !d.res && !d.rowbias && !d.out_f32);
-  static bool cus_read = false;
-  if (!cus_read) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-      g_num_cus = n;
-    cus_read = true;
-  }
   const Plan p = plan(d);
   if (p.ver >= 2 && p.split > 1) VD_CHECK_ARG(d.ws && al16(d.ws) && d.ws_bytes >= p.ws_bytes);
   if (p.ver == 3) return launch3(d, s, p.a0b, p.a1b, p.wb, p.split);
+  if (p.ver == 6) return launch6(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 5) return launch4<320, 4, 2, 4>(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 2)
     return p.bn == 160 ? launch2<160>(d, s, p.a0b, p.a1b, p.wb, p.split)
