@@ -93,7 +93,8 @@ int vd_gemm_force_v1(int32_t on);
 /* Test/benchmark hook: 0 = automatic (default), 1 = v1 (register-staged, any shape),
  * 2 = v2 (256 x {128,160} persistent LDS-DMA), 3 = v3 (256 x 256 8-phase, dense A only;
  * shapes it cannot take fall back to the automatic choice), 5 = v5 (256 x 320, BK 32,
- * 4-stage ring, load-free epilogue). */
+ * 4-stage ring, load-free epilogue), 6 = v6 (64 x 64, in-kernel split-K reduction), 7 = the
+ * automatic choice without v6. */
 int vd_gemm_select_path(int32_t path);
 
 /* ---------------------------------------------------------------- GroupNorm
@@ -158,8 +159,9 @@ int vd_temporal_force_valu(int32_t on);
 /* ---------------------------------------------------------------- step glue
  * vd_timestep_embed: diffusers Timesteps(dim, flip_sin_to_cos=True, shift 0)
  *   (a12) -> bf16 [B][dim].  Timestep = ts[*step_idx] if step_idx else ts[b].
- * vd_pack_latents: x (B,C,F,H,W) fp32 -> NHWC bf16 rows [(dup*B*F*H*W)][cpad],
- *   channels >= C zero; dup = 2 repeats the batch (the CFG cat([x, x])).
+ * vd_pack_latents: x (B,C,F,H,W) fp32 / in_div -> NHWC bf16 rows [(dup*B*F*H*W)][cpad],
+ *   channels >= C zero; dup = 2 repeats the batch (the CFG cat([x, x])); in_div is
+ *   the scheduler's scale_model_input divisor (1 for DDIM, sqrt(sigma^2+1) for Euler).
  * vd_unpack_nhwc: NHWC rows (fp32 if src_f32 else bf16, row stride ld) ->
  *   (B,C,F,H,W) fp32.
  * vd_ddim_cfg_step: eps rows NHWC fp32 [(ncfg*B*F*H*W)][ld_eps]; if ncfg == 2
@@ -168,18 +170,27 @@ int vd_temporal_force_valu(int32_t on);
  *   sqrt(1-a_t), sqrt(a_prev), sqrt(1-a_prev)}, step = *step_idx (or 0 if
  *   NULL); optional x0_out (B,C,F,H,W) fp32; optional next_in = the packed
  *   bf16 UNet input of the next step (dup = ncfg) — a1 + a13 fused.
+ * vd_euler_cfg_step: as vd_ddim_cfg_step, with the EulerDiscreteScheduler.step
+ *   update (s_churn 0, epsilon; diffusers' fp32 order x0 = x - s*eps,
+ *   d = (x - x0)/s, x += d*(s_next - s)) and coef[4*step] = {sigma, sigma_next,
+ *   sqrt(sigma_next^2 + 1), 0}; next_in = the next step's scale_model_input(x)
+ *   packed to bf16 — §8f rank 2 (experiments/01_baseline_generation.py:76-80).
  * vd_step_advance: ++*step_idx (one thread; the last node of a captured step).
  */
 int vd_timestep_embed(const float* ts, const int32_t* step_idx, int64_t B, int32_t dim,
                       void* out, vd_stream_t stream);
 int vd_pack_latents(const float* x, int64_t B, int64_t C, int64_t F, int64_t H, int64_t W,
-                    int32_t dup, void* out, int64_t cpad, vd_stream_t stream);
+                    int32_t dup, void* out, int64_t cpad, float in_div, vd_stream_t stream);
 int vd_unpack_nhwc(const void* src, int32_t src_f32, int64_t ld, int64_t B, int64_t C,
                    int64_t F, int64_t H, int64_t W, float* dst, vd_stream_t stream);
 int vd_ddim_cfg_step(const float* eps, int64_t ld_eps, int32_t ncfg, float guidance,
                      float* latents, int64_t B, int64_t C, int64_t F, int64_t H, int64_t W,
                      const float* coef, const int32_t* step_idx, float* x0_out,
                      void* next_in, int64_t cpad, vd_stream_t stream);
+int vd_euler_cfg_step(const float* eps, int64_t ld_eps, int32_t ncfg, float guidance,
+                      float* latents, int64_t B, int64_t C, int64_t F, int64_t H, int64_t W,
+                      const float* coef, const int32_t* step_idx, float* x0_out,
+                      void* next_in, int64_t cpad, vd_stream_t stream);
 int vd_step_advance(int32_t* step_idx, vd_stream_t stream);
 
 /* Row-block permute for the frame<->position re-shard around motion modules:

@@ -10,6 +10,10 @@ tiny_unet.npz  — BASELINE config 1: tiny UNetMotionModel,
                  step from t=961 (50-step schedule), and a 3-step loop result.
 ddim_tables.npz — DDIM leading timesteps and {sqrt a_t, sqrt 1-a_t, sqrt a_p,
                  sqrt 1-a_p} tables for N in {15, 25, 50}.
+euler.npz      — EulerDiscreteScheduler (linspace spacing, linear betas; the reference's
+                 experiments/01_baseline_generation.py:76-80 configuration): timesteps and
+                 sigmas for N in {15, 25, 50}, and a 3-step Euler CFG loop of the tiny UNet
+                 from latents * init_noise_sigma (python tests/golden/make_golden.py euler).
 
 Both come from oracle/ (the CPU restatement); see the oracle header for what
 that pins and what it cannot (diffusers numerics are unpinned).
@@ -24,7 +28,7 @@ HERE = Path(__file__).resolve().parent
 ROOT = HERE.parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "video-diffusion-experiments_amd")]
 
-from oracle import ddim_ref, unet_ref  # noqa: E402
+from oracle import ddim_ref, euler_ref, unet_ref  # noqa: E402
 from vdiff.config import TINY  # noqa: E402
 from vdiff.models import UNetMotionModel  # noqa: E402
 from vdiff.weights import init_synthetic_  # noqa: E402
@@ -77,5 +81,23 @@ def main():
     print({k: v.shape for k, v in out.items()})
 
 
+def make_euler():
+    out = {}
+    for n in (15, 25, 50):
+        ts, sig = euler_ref.set_timesteps(n)
+        out[f"ts{n}"], out[f"sigmas{n}"] = ts.numpy(), sig.numpy()
+    sd, lat, _ = tiny_inputs()
+    ehs = torch.from_numpy(np.load(HERE / "tiny_unet.npz")["ehs"])
+    fn = lambda x, t, e: unet_ref.unet_forward(sd, TINY, x, t, e)  # noqa: E731
+    with torch.no_grad():
+        out["loop3_x"] = euler_ref.denoise_loop(fn, lat, ehs, 25, 7.5, steps=3).numpy()
+    np.savez_compressed(HERE / "euler.npz", **out)
+    print({k: v.shape for k, v in out.items()})
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["euler"]:
+        make_euler()
+    else:
+        main()
+        make_euler()

@@ -573,6 +573,37 @@ def test_ddim_cfg_step_matches_oracle(cuda):
     close_bf16(ops.unpack_nhwc(nxt[: Fr * H * W], 1, 4, Fr, H, W), want)
 
 
+@pytest.mark.parametrize("ncfg", [2, 1])
+def test_euler_cfg_step_matches_oracle(cuda, ncfg):
+    """CFG + EulerDiscreteScheduler.step in diffusers' fp32 operation order: bit-exact against
+    the oracle on the same inputs (no FMA contraction in the kernel); the packed next input is
+    scale_model_input(x, sigma_next) rounded once to bf16."""
+    from oracle import euler_ref
+    _, sig = euler_ref.set_timesteps(25)
+    B, Cc, Fr, H, W = 1, 4, 3, 8, 8
+    for i in (0, 11, 24):  # first, interior, last (sigma_next = 0, divisor 1)
+        s, sn = sig[i], sig[i + 1]
+        coef = torch.stack([s, sn, (sn ** 2 + 1) ** 0.5, torch.zeros(())]).float()
+        lat = torch.randn(B, Cc, Fr, H, W, device=cuda) * float(s)
+        eps_rows = torch.randn(ncfg * Fr * H * W, 4, device=cuda)
+        x = lat.clone()
+        x0 = torch.empty_like(x)
+        nxt = torch.empty(ncfg * Fr * H * W, 8, device=cuda, dtype=BF)
+        ops.euler_cfg_step(eps_rows, ncfg, 7.5, x, coef.to(cuda), x0_out=x0, next_in=nxt)
+        e = eps_rows.cpu().reshape(ncfg, Fr, H, W, 4).permute(0, 4, 1, 2, 3)
+        e = e[0:1] + 7.5 * (e[1:2] - e[0:1]) if ncfg == 2 else e
+        want, want0 = euler_ref.euler_step(e, lat.cpu(), s, sn)
+        close_f32(x, want, rtol=1e-6, atol=1e-6)
+        close_f32(x0, want0, rtol=1e-6, atol=1e-6)
+        close_bf16(ops.unpack_nhwc(nxt[: Fr * H * W], 1, 4, Fr, H, W), euler_ref.scale_model_input(want, sn))
+
+
+def test_pack_latents_input_divisor(cuda):
+    x = torch.randn(1, 4, 2, 8, 8, device=cuda) * 25.0
+    rows = ops.pack_latents(x, dup=1, cpad=8, in_div=25.17)
+    close_bf16(ops.unpack_nhwc(rows, 1, 4, 2, 8, 8), x / 25.17)
+
+
 def test_step_advance_and_block_transpose(cuda):
     s = torch.zeros(1, device=cuda, dtype=torch.int32)
     ops.step_advance(s)

@@ -19,7 +19,7 @@ import pytest
 import torch
 
 from oracle import ddim_ref, unet_ref
-from vdiff import DDIMScheduler, DenoiseLoop, UNetMotionModel, init_synthetic_, ops
+from vdiff import DDIMScheduler, DenoiseLoop, EulerDiscreteScheduler, UNetMotionModel, init_synthetic_, ops
 from vdiff.config import TINY
 from vdiff.models.blocks import AnimateDiffTransformer3D, Ctx, ResnetBlock2D, Transformer2DModel
 from vdiff.models.layers import Act, prepare_tree
@@ -166,3 +166,39 @@ def test_denoise_loop_graph_matches_oracle(tiny_unet, gold, use_graph):
     x = loop.run(3)
     assert int(loop.step_idx.item()) == 3
     assert rel_l2(x, torch.from_numpy(gold["loop3_x"])) < 0.01
+
+
+def test_euler_scheduler_api_and_graph_loop_match_oracle(tiny_unet, gold):
+    """EulerDiscreteScheduler (the reference's
+    01_baseline_generation.py:76-80 configuration) behind the same surface: the
+    scale_model_input -> unet -> CFG -> step API on the device, and the hipGraph loop
+    with the fused Euler kernel, against the oracle's 3-step Euler loop (rel-L2 1%)."""
+    from oracle import euler_ref
+    eu = np.load(GOLD / "euler.npz")
+    lat = torch.from_numpy(gold["latents"]).cuda()
+    ehs = torch.from_numpy(gold["ehs"]).cuda()
+    want = torch.from_numpy(eu["loop3_x"])
+
+    s = EulerDiscreteScheduler.from_config(DDIMScheduler().config, timestep_spacing="linspace",
+                                           beta_schedule="linear")
+    s.set_timesteps(25)
+    x = lat * s.init_noise_sigma
+    for t in s.timesteps[:3]:
+        xi = s.scale_model_input(torch.cat([x, x]), t)
+        eps = tiny_unet(xi, t, encoder_hidden_states=ehs).sample
+        u, c = eps.chunk(2)
+        out = s.step(u + 7.5 * (c - u), t, x)
+        if t == s.timesteps[0]:  # exact Euler arithmetic on identical eps
+            e = (u + 7.5 * (c - u)).cpu()
+            w1, w0 = euler_ref.euler_step(e, x.cpu(), s.sigmas[0], s.sigmas[1])
+            torch.testing.assert_close(out.prev_sample.cpu(), w1, rtol=1e-6, atol=1e-5)
+            torch.testing.assert_close(out.pred_original_sample.cpu(), w0, rtol=1e-6, atol=1e-5)
+        x = out.prev_sample
+    assert s.step_index == 3
+    assert rel_l2(x, want) < 0.01
+
+    s.set_timesteps(25)
+    loop = DenoiseLoop(tiny_unet, s, lat * s.init_noise_sigma, ehs, 7.5, use_graph=True).prime()
+    assert loop.graph is not None, loop.graph_error
+    x = loop.run(3)
+    assert rel_l2(x, want) < 0.01

@@ -101,3 +101,61 @@ def test_oracle_reproduces_committed_fixture():
     with torch.no_grad():
         eps = unet_ref.unet_forward(sd, TINY, torch.cat([lat, lat]), 961, ehs)
     np.testing.assert_allclose(eps.numpy(), gold["eps_t961"], rtol=1e-4, atol=1e-5)
+
+
+# ---------------------------------------------------------------- Euler
+def test_euler_sigma_tables_closed_form():
+    """sigma_i = sqrt((1 - a_bar) / a_bar) interpolated at linspace(0, 999, n)[::-1];
+    endpoints are exact training sigmas, the table ends in 0."""
+    from oracle import euler_ref
+    acp = ddim_ref.alphas_cumprod().double()
+    sig_train = ((1 - acp) / acp) ** 0.5
+    ts, sig = euler_ref.set_timesteps(25)
+    assert ts[0] == 999.0 and ts[-1] == 0.0 and len(sig) == 26 and sig[-1] == 0.0
+    assert abs(float(sig[0]) - float(sig_train[999])) < 1e-5 * float(sig_train[999])
+    assert abs(float(sig[-2]) - float(sig_train[0])) < 1e-6
+    # an interior, fractional timestep interpolates linearly between its neighbours
+    t = float(ts[1])
+    lo = int(math.floor(t))
+    want = float(sig_train[lo]) + (t - lo) * float(sig_train[lo + 1] - sig_train[lo])
+    assert abs(float(sig[1]) - want) < 1e-5 * want
+    assert abs(euler_ref.init_noise_sigma(sig) - float(sig[0])) == 0  # linspace: max sigma, no sqrt(s^2+1)
+    assert 25.0 < float(sig[0]) < 25.3  # linear betas (the reference override): sigma_max ~ 25.15
+
+
+def test_euler_product_scheduler_matches_oracle_tables():
+    """The product's host math (vdiff.EulerDiscreteScheduler built with the reference's
+    override idiom) reproduces the committed oracle tables exactly."""
+    from vdiff.sched import EulerDiscreteScheduler
+    tab = np.load(GOLD / "euler.npz")
+    s = EulerDiscreteScheduler.from_config(DDIMScheduler().config, timestep_spacing="linspace",
+                                           beta_schedule="linear")
+    for n in (15, 25, 50):
+        s.set_timesteps(n)
+        np.testing.assert_array_equal(s.timesteps.numpy(), tab[f"ts{n}"])
+        np.testing.assert_array_equal(s.sigmas.numpy(), tab[f"sigmas{n}"])
+        assert s.init_noise_sigma == float(tab[f"sigmas{n}"].max())
+        coef = s.coefficient_table().numpy()
+        np.testing.assert_array_equal(coef[:, 0], tab[f"sigmas{n}"][:-1])
+        np.testing.assert_array_equal(coef[:, 1], tab[f"sigmas{n}"][1:])
+        assert coef[-1, 2] == 1.0
+    # step-index bookkeeping and scale_model_input (x / sqrt(sigma^2 + 1))
+    s.set_timesteps(25)
+    x = torch.randn(4, 8)
+    y = s.scale_model_input(x, s.timesteps[0])
+    assert s.step_index == 0
+    torch.testing.assert_close(y, x / float((s.sigmas[0] ** 2 + 1) ** 0.5), rtol=0, atol=0)
+    assert s.index_for_timestep(s.timesteps[3]) == 3 and s.order == 1
+    with pytest.raises(ValueError):
+        s.index_for_timestep(123.456)
+
+
+def test_euler_oracle_step_is_probability_flow_update():
+    """The diffusers operation order reduces to x + (sigma_next - sigma) * eps up to fp32 rounding
+    (docs/01_diffusion_fundamentals.md's Euler step in the sigma parameterisation)."""
+    from oracle import euler_ref
+    g = torch.Generator().manual_seed(3)
+    x, e = torch.randn(1000, generator=g) * 14.0, torch.randn(1000, generator=g)
+    got, x0 = euler_ref.euler_step(e, x, 14.6, 12.0)
+    torch.testing.assert_close(got, x + (12.0 - 14.6) * e, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(x0, x - 14.6 * e, rtol=1e-6, atol=1e-5)

@@ -1591,7 +1591,7 @@ int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
-int g_path = 0;  // 0 auto, 1 v1, 2 v2, 3 v3, 5 v5, 6 v6 (tests / benchmarks)
+int g_path = 0;  // 0 auto, 1 v1, 2 v2, 3 v3, 5 v5, 6 v6, 7 auto without v6 (tests / benchmarks)
 
 struct Plan {
   int ver = 1;
@@ -1636,7 +1636,7 @@ Plan plan(const vd_gemm_desc& d) {
   // it wins (tools/kbench.py: the L1 attention QKV projection M 131072 x N 960 x K 320)
   const bool v5auto = d.a_mode == VD_A_DENSE && d.M >= 65536 && d.K <= 320 && d.N % 320 == 0 && d.N >= 640 &&
                       d.N < 2560 && !d.res && !d.rowbias && d.act != VD_ACT_GEGLU;
-  if (g_path == 5 || (g_path == 0 && (!k64 || v5auto))) {
+  if (g_path == 5 || ((g_path == 0 || g_path == 7) && (!k64 || v5auto))) {
     if (!cin32) return p;
     p.ver = 5;
     p.bn = 320;
@@ -1647,13 +1647,17 @@ Plan plan(const vd_gemm_desc& d) {
   }
   if (!k64) return p;
   const int64_t nk = d.K / BK;
-  // v6 (64 x 64 tiles): forced, or automatically at the small M of a frame-sharded rank
-  // (M <= 16384) where its tiles fill two workgroups per CU without splitting K (tools/
-  // kbench.py KB_IMGS=4: L1/L2 projections 17-20 -> 10-11 us, ff2 33-35 -> 27 us); with
-  // K split, and for GEGLU, v2/v3 stay faster
+  // v6 (64 x 64 tiles): forced, or automatically where the 256-row tiles leave the chip
+  // underfilled (fewer tiles than CUs: the small M of a frame-sharded rank, or L4 at full
+  // size) while v6's tiles fill two workgroups per CU without splitting K, on N <= 1280 and
+  // K <= 2560 (tools/kb_sweep.sh, profiles/r01_gemm_paths.txt: e.g. 4 images L1/L2
+  // projections 16-20 -> 11 us, 32 images L4 projection 28 -> 16 us); with K split, wide N,
+  // long K and GEGLU, v2/v3 stay faster (L3 qkv at 32 images 78 us vs 180 us on v6)
   {
     const int64_t tiles6 = ((d.M + G6_BM - 1) / G6_BM) * ((d.N + G6_BN - 1) / G6_BN);
-    const bool v6auto = d.M <= 16384 && d.act != VD_ACT_GEGLU && tiles6 >= 2 * g_num_cus;
+    const int64_t tiles256 = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + 159) / 160);
+    const bool v6auto = d.act != VD_ACT_GEGLU && d.N <= 1280 && d.K <= 2560 && tiles6 >= 2 * g_num_cus &&
+                        tiles256 < g_num_cus;
     if (g_path == 6 || (g_path == 0 && v6auto)) {
       p.ver = 6;
       p.bn = 64;
@@ -1696,7 +1700,7 @@ extern "C" int vd_gemm_force_v1(int32_t on) {
   return VD_OK;
 }
 extern "C" int vd_gemm_select_path(int32_t path) {
-  if (path < 0 || path > 6 || path == 4) return VD_EINVAL;
+  if (path < 0 || path > 7 || path == 4) return VD_EINVAL;
   g_path = path;
   return VD_OK;
 }

@@ -15,6 +15,11 @@ namespace {
 
 constexpr int NT = 256;
 
+// fp32 quotient, correctly rounded (via double: 53 >= 2*24 + 2, so the second rounding is
+// innocuous) — the GPU's default f32 division is a reciprocal-refinement sequence
+__device__ __forceinline__ float div_rn(float a, float b) { return (float)((double)a / (double)b); }
+
+
 __global__ void timestep_embed_kernel(const float* ts, const int32_t* step_idx, int64_t B, int dim,
                                       bf16_t* out) {
   const int half = dim / 2;
@@ -32,8 +37,8 @@ __global__ void timestep_embed_kernel(const float* ts, const int32_t* step_idx, 
 }
 
 __global__ void pack_latents_kernel(const float* x, int64_t B, int64_t C, int64_t F, int64_t HW,
-                                    int dup, bf16_t* out, int64_t cpad) {
-  // out row r = ((d*B + b)*F + f)*HW + p, channel c  <-  x[b][c][f][p]
+                                    int dup, bf16_t* out, int64_t cpad, float in_div) {
+  // out row r = ((d*B + b)*F + f)*HW + p, channel c  <-  x[b][c][f][p] / in_div
   const int64_t rows = dup * B * F * HW;
   const int64_t total = rows * cpad;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
@@ -43,7 +48,7 @@ __global__ void pack_latents_kernel(const float* x, int64_t B, int64_t C, int64_
     const int64_t f = (r / HW) % F;
     const int64_t b = (r / (HW * F)) % B;
     float val = 0.f;
-    if (c < C) val = x[((b * C + c) * F + f) * HW + p];
+    if (c < C) val = in_div == 1.f ? x[((b * C + c) * F + f) * HW + p] : div_rn(x[((b * C + c) * F + f) * HW + p], in_div);
     out[i] = f2bf(val);
   }
 }
@@ -94,6 +99,46 @@ __global__ void ddim_cfg_kernel(const float* eps, int64_t ld_eps, int ncfg, floa
   }
 }
 
+// CFG combine + diffusers:EulerDiscreteScheduler.step (s_churn = 0, epsilon
+// prediction), in diffusers' fp32 operation order:
+//   x0 = x - sigma*eps;  d = (x - x0) / sigma;  x <- x + d * (sigma_next - sigma)
+// and the next step's UNet input = scale_model_input(x, sigma_next) = x / sqrt(sigma_next^2 + 1)
+// (coef[4*st] = {sigma, sigma_next, sqrt(sigma_next^2 + 1), 0}).
+__global__ void euler_cfg_kernel(const float* eps, int64_t ld_eps, int ncfg, float g, float* lat,
+                                 int64_t B, int64_t C, int64_t F, int64_t HW, const float* coef,
+                                 const int32_t* step_idx, float* x0_out, bf16_t* next_in,
+                                 int64_t cpad) {
+#pragma clang fp contract(off)  // one rounding per operation, as torch's separate fp32 ops
+  const int st = step_idx ? *step_idx : 0;
+  const float sig = coef[4 * st + 0], sig_n = coef[4 * st + 1], in_div = coef[4 * st + 2];
+  const float dt = sig_n - sig;
+  const int64_t total = B * C * F * HW;
+  const int64_t half_rows = B * F * HW;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int64_t p = i % HW;
+    const int64_t f = (i / HW) % F;
+    const int64_t c = (i / (HW * F)) % C;
+    const int64_t b = i / (HW * F * C);
+    const int64_t r = (b * F + f) * HW + p;
+    float e = eps[r * ld_eps + c];
+    if (ncfg == 2) {
+      const float ec = eps[(r + half_rows) * ld_eps + c];
+      e = e + g * (ec - e);
+    }
+    const float x = lat[i];
+    const float x0 = x - sig * e;
+    const float d = div_rn(x - x0, sig);
+    const float xn = x + d * dt;
+    lat[i] = xn;
+    if (x0_out) x0_out[i] = x0;
+    if (next_in) {
+      const bf16_t v = f2bf(div_rn(xn, in_div));
+      next_in[r * cpad + c] = v;
+      if (ncfg == 2) next_in[(r + half_rows) * cpad + c] = v;
+    }
+  }
+}
+
 __global__ void step_advance_kernel(int32_t* step_idx) { *step_idx += 1; }
 
 __global__ void block_transpose_kernel(const bf16_t* src, bf16_t* dst, int64_t nb, int64_t na,
@@ -128,11 +173,12 @@ extern "C" int vd_timestep_embed(const float* ts, const int32_t* step_idx, int64
 }
 
 extern "C" int vd_pack_latents(const float* x, int64_t B, int64_t C, int64_t F, int64_t H,
-                               int64_t W, int32_t dup, void* out, int64_t cpad, vd_stream_t stream) {
-  VD_CHECK_ARG(x && out && B > 0 && C > 0 && F > 0 && H > 0 && W > 0 && cpad >= C && dup >= 1);
+                               int64_t W, int32_t dup, void* out, int64_t cpad, float in_div,
+                               vd_stream_t stream) {
+  VD_CHECK_ARG(x && out && B > 0 && C > 0 && F > 0 && H > 0 && W > 0 && cpad >= C && dup >= 1 && in_div > 0.f);
   const int64_t total = dup * B * F * H * W * cpad;
   hipLaunchKernelGGL(pack_latents_kernel, dim3(grid_for(total)), dim3(NT), 0, (hipStream_t)stream,
-                     x, B, C, F, H * W, dup, (bf16_t*)out, cpad);
+                     x, B, C, F, H * W, dup, (bf16_t*)out, cpad, in_div);
   return vd_launch_status();
 }
 
@@ -151,6 +197,18 @@ extern "C" int vd_ddim_cfg_step(const float* eps, int64_t ld_eps, int32_t ncfg, 
   VD_CHECK_ARG(eps && latents && coef && (ncfg == 1 || ncfg == 2) && ld_eps >= C);
   if (next_in) VD_CHECK_ARG(cpad >= C);
   hipLaunchKernelGGL(ddim_cfg_kernel, dim3(grid_for(B * C * F * H * W)), dim3(NT), 0,
+                     (hipStream_t)stream, eps, ld_eps, ncfg, guidance, latents, B, C, F, H * W,
+                     coef, step_idx, x0_out, (bf16_t*)next_in, cpad);
+  return vd_launch_status();
+}
+
+extern "C" int vd_euler_cfg_step(const float* eps, int64_t ld_eps, int32_t ncfg, float guidance,
+                                 float* latents, int64_t B, int64_t C, int64_t F, int64_t H,
+                                 int64_t W, const float* coef, const int32_t* step_idx,
+                                 float* x0_out, void* next_in, int64_t cpad, vd_stream_t stream) {
+  VD_CHECK_ARG(eps && latents && coef && (ncfg == 1 || ncfg == 2) && ld_eps >= C);
+  if (next_in) VD_CHECK_ARG(cpad >= C);
+  hipLaunchKernelGGL(euler_cfg_kernel, dim3(grid_for(B * C * F * H * W)), dim3(NT), 0,
                      (hipStream_t)stream, eps, ld_eps, ncfg, guidance, latents, B, C, F, H * W,
                      coef, step_idx, x0_out, (bf16_t*)next_in, cpad);
   return vd_launch_status();

@@ -35,9 +35,10 @@ SIGNATURES = {
     "vd_attention": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_i64, c_f32, c_vp], c_i32),
     "vd_temporal_attention": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
     "vd_timestep_embed": ([c_vp, c_vp, c_i64, c_i32, c_vp, c_vp], c_i32),
-    "vd_pack_latents": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp], c_i32),
+    "vd_pack_latents": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_f32, c_vp], c_i32),
     "vd_unpack_nhwc": ([c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp], c_i32),
     "vd_ddim_cfg_step": ([c_vp, c_i64, c_i32, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
+    "vd_euler_cfg_step": ([c_vp, c_i64, c_i32, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
     "vd_step_advance": ([c_vp, c_vp], c_i32),
     "vd_block_transpose": ([c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp], c_i32),
 }

@@ -203,13 +203,13 @@ def timestep_embed(ts, dim, step_idx=None, batch=None, out=None):
     return out
 
 
-def pack_latents(x, dup=1, cpad=8, out=None):
+def pack_latents(x, dup=1, cpad=8, out=None, in_div=1.0):
     _dev(x, out)
     x = x.contiguous().float()
     B, Cc, Fr, H, W = x.shape
     if out is None:
         out = torch.empty(dup * B * Fr * H * W, cpad, device=x.device, dtype=BF16)
-    check(lib().vd_pack_latents(_p(x), B, Cc, Fr, H, W, dup, _p(out), cpad, _stream()), "vd_pack_latents")
+    check(lib().vd_pack_latents(_p(x), B, Cc, Fr, H, W, dup, _p(out), cpad, float(in_div), _stream()), "vd_pack_latents")
     return out
 
 
@@ -231,6 +231,21 @@ def ddim_cfg_step(eps, ncfg, guidance, latents, coef, step_idx=None, x0_out=None
                                  _p(coef), _p(step_idx), _p(x0_out), _p(next_in),
                                  next_in.shape[1] if next_in is not None else 0, _stream()),
           "vd_ddim_cfg_step")
+
+
+def euler_cfg_step(eps, ncfg, guidance, latents, coef, step_idx=None, x0_out=None, next_in=None):
+    """CFG combine + EulerDiscreteScheduler.step (+ next input's scale_model_input), fused."""
+    _dev(eps, latents, coef, step_idx, x0_out, next_in)
+    if latents.dtype != torch.float32 or not latents.is_contiguous():
+        raise ValueError("latents must be contiguous fp32")
+    B, Cc, Fr, H, W = latents.shape
+    check(lib().vd_euler_cfg_step(_p(eps), eps.stride(0), ncfg, guidance, _p(latents), B, Cc, Fr, H, W,
+                                  _p(coef), _p(step_idx), _p(x0_out), _p(next_in),
+                                  next_in.shape[1] if next_in is not None else 0, _stream()),
+          "vd_euler_cfg_step")
+
+
+SCHED_STEP = {"ddim": ddim_cfg_step, "euler": euler_cfg_step}
 
 
 def step_advance(step_idx):

@@ -53,7 +53,7 @@ class SyntheticTextEncoder:
 class DenoiseLoop:
     """Preallocated device state + the captured graph of one denoising step."""
 
-    def __init__(self, unet: UNetMotionModel, scheduler: DDIMScheduler, latents: torch.Tensor,
+    def __init__(self, unet: UNetMotionModel, scheduler, latents: torch.Tensor,
                  prompt_embeds: torch.Tensor, guidance_scale: float, timesteps=None,
                  use_graph: bool = True):
         if not unet._prepared:
@@ -69,13 +69,20 @@ class DenoiseLoop:
         self.n_steps = len(ts)
         self.ts = torch.as_tensor(ts).to(dev, torch.float32)
         self.coef = scheduler.coefficient_table(torch.as_tensor(ts).cpu()).to(dev)
+        # the scheduler's fused CFG+update kernel; Euler's also applies the next step's
+        # scale_model_input, and the first input is packed with step 0's divisor
+        self.kind = getattr(scheduler, "kind", "ddim")
+        self.sched_step = ops.SCHED_STEP[self.kind]
+        self.in_div0 = 1.0
+        if self.kind == "euler":
+            self.in_div0 = scheduler.input_divisor(scheduler.index_for_timestep(float(torch.as_tensor(ts)[0])))
         self.step_idx = torch.zeros(1, device=dev, dtype=torch.int32)
         pe = prompt_embeds.to(dev, torch.bfloat16).contiguous()
         if pe.shape[0] != self.Bt:
             raise ValueError(f"prompt_embeds batch {pe.shape[0]} != {self.Bt} (uncond first when CFG)")
         self.L = pe.shape[1]
         self.ehs_rows = pe.reshape(self.Bt * self.L, -1)
-        self.x_in = ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD)
+        self.x_in = ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD, in_div=self.in_div0)
         self.kv_cache = {}
         self.use_graph = use_graph
         self.graph = None
@@ -86,14 +93,14 @@ class DenoiseLoop:
         te = ops.timestep_embed(self.ts, u.time_proj.num_channels, step_idx=self.step_idx, batch=self.Bt)
         ctx = u.make_ctx(te, self.ehs_rows, self.Bt, self.F, self.L, kv_cache=self.kv_cache)
         eps = u.forward_rows(self.x_in, self.H, self.W, ctx)
-        ops.ddim_cfg_step(eps, self.ncfg, self.g, self.lat, self.coef, step_idx=self.step_idx,
-                          next_in=self.x_in)
+        self.sched_step(eps, self.ncfg, self.g, self.lat, self.coef, step_idx=self.step_idx,
+                        next_in=self.x_in)
         ops.step_advance(self.step_idx)
 
     def reset(self, latents):
         self.lat.copy_(latents)
         self.step_idx.zero_()
-        ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD, out=self.x_in)
+        ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD, out=self.x_in, in_div=self.in_div0)
 
     def prime(self):
         """One eager step (loads kernels, fills the cross-attention K/V cache,

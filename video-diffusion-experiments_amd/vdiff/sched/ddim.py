@@ -49,6 +49,7 @@ class _Cfg(dict):
 
 class DDIMScheduler:
     order = 1
+    kind = "ddim"  # selects the fused device update (ops.SCHED_STEP)
     init_noise_sigma = 1.0
 
     def __init__(self, **kwargs):
