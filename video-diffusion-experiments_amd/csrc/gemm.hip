@@ -1591,7 +1591,8 @@ int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
-int g_path = 0;  // 0 auto, 1 v1, 2 v2, 3 v3, 5 v5, 6 v6, 7 auto without v6 (tests / benchmarks)
+int g_path = 0;  // 0 auto, 1 v1, 2 v2, 3 v3, 5 v5, 6 v6, 7 auto without v6, 8 v6 unsplit,
+                  // 9 auto with split-K cap 8 (tests / benchmarks)
 
 struct Plan {
   int ver = 1;
@@ -1600,11 +1601,16 @@ struct Plan {
   int64_t ws_bytes = 0;
 };
 
+// max K slices of the v2/v3/v5 split path: 32 (L4 convs at 4-8 images per rank, 64 -> 176
+// workgroups: 66 -> 38 us, 41 -> 30 us; neutral elsewhere — profiles/r01_gemm_paths.txt);
+// path 9 restores the earlier cap of 8 for comparisons
+int g_split_cap = 32;
+
 inline int split_for(int64_t tiles, int64_t nk) {
   if (tiles >= 192 || nk < 16) return 1;
   int64_t sp = (256 + tiles - 1) / tiles;
   sp = sp < nk / 8 ? sp : nk / 8;
-  return (int)(sp < 8 ? sp : 8);
+  return (int)(sp < g_split_cap ? sp : g_split_cap);
 }
 
 // LDS-DMA kernels wherever the operands fit 32-bit buffer offsets: v3 (256x256,
@@ -1647,23 +1653,26 @@ Plan plan(const vd_gemm_desc& d) {
   }
   if (!k64) return p;
   const int64_t nk = d.K / BK;
-  // v6 (64 x 64 tiles): forced, or automatically where the 256-row tiles leave the chip
+  // v6 (64 x 64 tiles, never split automatically): where the 256-row tiles leave the chip
   // underfilled (fewer tiles than CUs: the small M of a frame-sharded rank, or L4 at full
-  // size) while v6's tiles fill two workgroups per CU without splitting K, on N <= 1280 and
-  // K <= 2560 (tools/kb_sweep.sh, profiles/r01_gemm_paths.txt: e.g. 4 images L1/L2
-  // projections 16-20 -> 11 us, 32 images L4 projection 28 -> 16 us); with K split, wide N,
-  // long K and GEGLU, v2/v3 stay faster (L3 qkv at 32 images 78 us vs 180 us on v6)
+  // size) and K <= 1280 (K <= 2560 when v6 alone gives >= 2 workgroups per CU); wide N only
+  // up to 4 workgroups per CU (64 x 64 tiles are L2-bandwidth bound), GEGLU only at tiny M.
+  // tools/kb_sweep.sh, profiles/r01_gemm_paths.txt: 4 images L3/L4 projections 21-27 ->
+  // 11 us, L4 qkv 24 -> 11 us; v2/v3 stay faster on long K, wide N at M >= 2048, and convs.
   {
     const int64_t tiles6 = ((d.M + G6_BM - 1) / G6_BM) * ((d.N + G6_BN - 1) / G6_BN);
     const int64_t tiles256 = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + 159) / 160);
-    const bool v6auto = d.act != VD_ACT_GEGLU && d.N <= 1280 && d.K <= 2560 && tiles6 >= 2 * g_num_cus &&
-                        tiles256 < g_num_cus;
-    if (g_path == 6 || (g_path == 0 && v6auto)) {
+    const bool v6auto = tiles256 < g_num_cus && (d.N <= 1280 || tiles6 <= 4 * g_num_cus) &&
+                        (d.act != VD_ACT_GEGLU || 2 * tiles256 <= g_num_cus) &&
+                        (d.K <= 1280 || (d.K <= 2560 && tiles6 >= 2 * g_num_cus));
+    if (g_path == 6 || g_path == 8 || (g_path == 0 && v6auto)) {
       p.ver = 6;
       p.bn = 64;
       int64_t sp = 1;
-      // aim for >= 2 workgroups per CU, each slice >= 4 k-tiles
-      while (tiles6 * sp < 2 * g_num_cus && nk / (sp * 2) >= 4 && sp < 16) sp *= 2;
+      // forced v6: aim for >= 2 workgroups per CU, each slice >= 4 k-tiles (the automatic
+      // choice never splits: the in-kernel reduction's agent-scope release/acquire fences
+      // write back / invalidate L2 and cost ~25 us — profiles/r01_gemm_paths.txt)
+      while (g_path == 6 && tiles6 * sp < 2 * g_num_cus && nk / (sp * 2) >= 4 && sp < 16) sp *= 2;
       p.split = (int)sp;
       p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 + ((tiles6 * 4 + 255) / 256) * 256 : 0;
       return p;
@@ -1700,8 +1709,9 @@ extern "C" int vd_gemm_force_v1(int32_t on) {
   return VD_OK;
 }
 extern "C" int vd_gemm_select_path(int32_t path) {
-  if (path < 0 || path > 7 || path == 4) return VD_EINVAL;
-  g_path = path;
+  if (path < 0 || path > 9 || path == 4) return VD_EINVAL;
+  g_split_cap = path == 9 ? 8 : 32;
+  g_path = path == 9 ? 0 : path;
   return VD_OK;
 }
 
