@@ -156,6 +156,13 @@ int vd_temporal_attention(const void* q, const void* k, const void* v, int64_t l
  * for frames <= 16 and d in {40, 80, 160}). */
 int vd_temporal_force_valu(int32_t on);
 
+/* Row softmax over fp32 scores in log2 units (p = exp2(s - max) / sum, bf16 out):
+ * the materialised-score attention of the VAE decoder's single-head (d = 512) mid-block
+ * Attention (diffusers AttnProcessor2_0 with upcast softmax).
+ * rows x cols, cols % 4 == 0, row strides ld_s / ld_p in elements. */
+int vd_softmax_rows(const float* s, int64_t ld_s, int64_t rows, int64_t cols, void* p,
+                    int64_t ld_p, vd_stream_t stream);
+
 /* ---------------------------------------------------------------- step glue
  * vd_timestep_embed: diffusers Timesteps(dim, flip_sin_to_cos=True, shift 0)
  *   (a12) -> bf16 [B][dim].  Timestep = ts[*step_idx] if step_idx else ts[b].

@@ -14,6 +14,10 @@ euler.npz      — EulerDiscreteScheduler (linspace spacing, linear betas; the r
                  experiments/01_baseline_generation.py:76-80 configuration): timesteps and
                  sigmas for N in {15, 25, 50}, and a 3-step Euler CFG loop of the tiny UNet
                  from latents * init_noise_sigma (python tests/golden/make_golden.py euler).
+vae_tiny.npz   — AutoencoderKL decode of the tiny VAE config, synthetic
+                 weights seed 0: latents randn seed 5 (1, 4, 2, 16, 16) through
+                 AnimateDiffPipeline.decode_latents -> (1, 3, 2, 32, 32), plus the bf16-storage
+                 emulating oracle (python tests/golden/make_golden.py vae).
 
 Both come from oracle/ (the CPU restatement); see the oracle header for what
 that pins and what it cannot (diffusers numerics are unpinned).
@@ -28,7 +32,7 @@ HERE = Path(__file__).resolve().parent
 ROOT = HERE.parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "video-diffusion-experiments_amd")]
 
-from oracle import ddim_ref, euler_ref, unet_ref  # noqa: E402
+from oracle import ddim_ref, euler_ref, unet_ref, vae_ref  # noqa: E402
 from vdiff.config import TINY  # noqa: E402
 from vdiff.models import UNetMotionModel  # noqa: E402
 from vdiff.weights import init_synthetic_  # noqa: E402
@@ -95,9 +99,26 @@ def make_euler():
     print({k: v.shape for k, v in out.items()})
 
 
+def make_vae():
+    from vdiff.models.vae import VAE_TINY, AutoencoderKL
+    m = init_synthetic_(AutoencoderKL("tiny"), seed=0)
+    sd = {k: v.float() for k, v in m.state_dict().items()}
+    lat = torch.randn((1, 4, 2, 16, 16), generator=torch.Generator().manual_seed(5))
+    lat = (lat * VAE_TINY["scaling_factor"]).to(torch.bfloat16).float()  # device packs bf16 rows of z/0.18215 ~ N(0,1)
+    with torch.no_grad():
+        out = {"latents": lat.numpy(),
+               "video": vae_ref.decode_latents(sd, VAE_TINY, lat).numpy(),
+               "video_bf16emu": vae_ref.decode_latents(sd, VAE_TINY, lat, rnd=unet_ref.ROUNDERS["bf16"]).numpy()}
+    np.savez_compressed(HERE / "vae_tiny.npz", **out)
+    print({k: v.shape for k, v in out.items()})
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["euler"]:
         make_euler()
+    elif sys.argv[1:] == ["vae"]:
+        make_vae()
     else:
         main()
         make_euler()
+        make_vae()

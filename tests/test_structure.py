@@ -85,3 +85,23 @@ def test_state_dict_keys_are_diffusers_names():
         assert k in sd, k
     assert "up_blocks.3.upsamplers.0.conv.weight" not in sd
     assert "down_blocks.3.downsamplers.0.conv.weight" not in sd
+
+
+def test_vae_decoder_tree():
+    """SD-1.5 AutoencoderKL decode side: the decoder + post_quant_conv
+    of the public SD-1.5 vae/config.json.  49,490,199 = 83,653,863 (SD-1.5 VAE total, public)
+    - 34,163,592 (encoder) - 72 (quant_conv); not a reference-published number, so a
+    consistency check of the tree rather than a parity pin."""
+    from vdiff.models.vae import AutoencoderKL
+    with torch.device("meta"):
+        m = AutoencoderKL("full")
+    assert sum(p.numel() for p in m.parameters()) == 49_490_199
+    keys = set(m.state_dict())
+    for k in ("post_quant_conv.weight", "decoder.conv_in.weight",
+              "decoder.mid_block.attentions.0.group_norm.weight", "decoder.mid_block.attentions.0.to_out.0.bias",
+              "decoder.mid_block.resnets.1.conv2.weight", "decoder.up_blocks.0.upsamplers.0.conv.weight",
+              "decoder.up_blocks.2.resnets.0.conv_shortcut.weight", "decoder.up_blocks.3.resnets.2.norm2.bias",
+              "decoder.conv_norm_out.weight", "decoder.conv_out.bias"):
+        assert k in keys, k
+    assert not any(k.startswith("decoder.up_blocks.3.upsamplers") for k in keys)
+    assert m.decoder.mid_block.attentions[0].heads == 1

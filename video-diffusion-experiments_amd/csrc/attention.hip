@@ -928,6 +928,45 @@ __global__ __launch_bounds__(NT) void temporal_mfma_kernel(
   }
 }
 
+// Row softmax for the materialised-score attention of the VAE mid block (one head,
+// d = 512: S = 4096 keys per frame fits HBM easily, the flash kernels stop at d = 160).
+// Scores arrive fp32 in log2 units (the caller folded d^-1/2 * log2(e) into q):
+// p = exp2(s - max) / sum, written bf16 as the A operand of the P.V GEMM.  One
+// workgroup per row, 4 columns per thread-step, three passes over the row (max,
+// sum, write) — the row (16 KiB at 4096 keys) stays in L1/L2 between them.
+__global__ __launch_bounds__(NT) void softmax_rows_kernel(const float* __restrict__ s, int64_t lds,
+                                                          int64_t cols, bf16_t* __restrict__ p,
+                                                          int64_t ldp) {
+  __shared__ float red[NT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* row = s + (int64_t)blockIdx.x * lds;
+  bf16_t* out = p + (int64_t)blockIdx.x * ldp;
+  float m = -INFINITY;
+  for (int64_t c = 4 * tid; c < cols; c += 4 * NT) {
+    const float4 v = *(const float4*)(row + c);
+    m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+  }
+  m = wave_max(m);
+  if (lane == 0) red[w] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int64_t c = 4 * tid; c < cols; c += 4 * NT) {
+    const float4 v = *(const float4*)(row + c);
+    sum += (exp2f(v.x - m) + exp2f(v.y - m)) + (exp2f(v.z - m) + exp2f(v.w - m));
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) red[w] = sum;
+  __syncthreads();
+  const float inv = 1.f / ((red[0] + red[1]) + (red[2] + red[3]));
+  for (int64_t c = 4 * tid; c < cols; c += 4 * NT) {
+    const float4 v = *(const float4*)(row + c);
+    *(uint2*)(out + c) = make_uint2(pack2(exp2f(v.x - m) * inv, exp2f(v.y - m) * inv),
+                                    pack2(exp2f(v.z - m) * inv, exp2f(v.w - m) * inv));
+  }
+}
+
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 int g_temporal_valu = 0;  // vd_temporal_force_valu
 
@@ -1001,5 +1040,14 @@ extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v
     hipLaunchKernelGGL(temporal_attn_kernel<32>, dim3(grid), dim3(NT), 0, s, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, ld, (bf16_t*)o, ldo, batch, frames,
                        positions, heads, d, sl2);
+  return vd_launch_status();
+}
+
+extern "C" int vd_softmax_rows(const float* s, int64_t ld_s, int64_t rows, int64_t cols, void* p, int64_t ld_p,
+                               vd_stream_t stream) {
+  VD_CHECK_ARG(s && p && rows > 0 && cols > 0 && cols % 4 == 0 && ld_s % 4 == 0 && ld_p % 4 == 0);
+  VD_CHECK_ARG(ld_s >= cols && ld_p >= cols && al16(s) && ((uintptr_t)p & 7) == 0 && rows < 0x7fffffff);
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)rows), dim3(NT), 0, (hipStream_t)stream, s, ld_s, cols,
+                     (bf16_t*)p, ld_p);
   return vd_launch_status();
 }

@@ -1232,12 +1232,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
 // vmcnt(0) -> barrier -> plain slab loads).  The counters live in the workspace after
 // the slabs and are zeroed by a memset node ahead of the launch; the last arriver
 // also resets its counter.
-constexpr int G6_BM = 64, G6_BN = 64, G6_NT = 256, G6_S = 3;
+// The ring depth S is picked per launch: 3 stages (48 KiB, three workgroups per CU) when
+// the grid oversubscribes the CUs, 4 / 6 stages (2 / 1 per CU) on small grids, where
+// each workgroup's k-loop is latency-bound and more tiles in flight pay directly.
+constexpr int G6_BM = 64, G6_BN = 64, G6_NT = 256;
 constexpr int G6_A = G6_BM * BK * 2, G6_W = G6_BN * BK * 2, G6_STAGE = G6_A + G6_W;  // 8 + 8 KiB
 
-template <int MODE>
-__global__ __launch_bounds__(G6_NT, 3) void gemm6_kernel(const vd_gemm_desc d, uint32_t a0_bytes, uint32_t a1_bytes,
-                                                         uint32_t w_bytes, int split) {
+template <int MODE, int G6_S>
+__global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void gemm6_kernel(
+    const vd_gemm_desc d, uint32_t a0_bytes, uint32_t a1_bytes, uint32_t w_bytes, int split) {
   constexpr int MB = 2, NB = 2;
   __shared__ __attribute__((aligned(1024))) char smem[G6_S * G6_STAGE + 16];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1333,16 +1336,23 @@ __global__ __launch_bounds__(G6_NT, 3) void gemm6_kernel(const vd_gemm_desc d, u
   for (int a = 0; a < NB; ++a)
 #pragma unroll
     for (int b = 0; b < MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (nk > 0) issue(0);
-  if (nk > 1) issue(1);
+#pragma unroll
+  for (int j = 0; j < G6_S - 1; ++j)
+    if (j < nk) issue(j);
   const int fr = lane & 15, fq = lane >> 4;
   int stage = 0;
   for (int it = 0; it < nk; ++it) {
-    if (it + 1 < nk) wait_vm<4>();  // k-step it+1's 4 pieces may stay in flight
-    else wait_vm<0>();
+    // k-steps it+1 .. it+S-2 (4 pieces each) may stay in flight
+    const int ahead = nk - 1 - it < G6_S - 2 ? nk - 1 - it : G6_S - 2;
+    if constexpr (G6_S == 3) {
+      if (ahead) wait_vm<4>();
+      else wait_vm<0>();
+    } else {
+      wait_vm_rt(4 * ahead);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (it + 2 < nk) issue(stage == 0 ? 2 : stage - 1);
+    if (it + G6_S - 1 < nk) issue(stage == 0 ? G6_S - 1 : stage - 1);
     const char* sb = smem + stage * G6_STAGE;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
@@ -1357,7 +1367,7 @@ __global__ __launch_bounds__(G6_NT, 3) void gemm6_kernel(const vd_gemm_desc d, u
         for (int b = 0; b < MB; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][b], 0, 0, 0);
     }
-    stage = stage == 2 ? 0 : stage + 1;
+    stage = stage == G6_S - 1 ? 0 : stage + 1;
   }
   const int mbase = (int)m0 + wm * 32, nbase = (int)n0 + wn * 32;
   if (split == 1) {
@@ -1568,12 +1578,21 @@ int launch6(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
     char* cnt = (char*)d.ws + (int64_t)split * d.M * d.N * 4;
     if (hipMemsetAsync(cnt, 0, (size_t)tiles * 4, s) != hipSuccess) return vd_launch_status();
   }
-  if (d.a_mode == VD_A_CONV3X3)
-    hipLaunchKernelGGL((gemm6_kernel<VD_A_CONV3X3>), dim3((unsigned)(tiles * split)), dim3(G6_NT), 0, s, d, a0b, a1b,
-                       wb, split);
-  else
-    hipLaunchKernelGGL((gemm6_kernel<VD_A_DENSE>), dim3((unsigned)(tiles * split)), dim3(G6_NT), 0, s, d, a0b, a1b, wb,
-                       split);
+  const int64_t wgs = tiles * split;
+  const dim3 grid((unsigned)wgs);
+#define G6_LAUNCH(S)                                                                                    \
+  if (d.a_mode == VD_A_CONV3X3)                                                                         \
+    hipLaunchKernelGGL((gemm6_kernel<VD_A_CONV3X3, S>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split); \
+  else                                                                                                  \
+    hipLaunchKernelGGL((gemm6_kernel<VD_A_DENSE, S>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split);
+  if (wgs <= g_num_cus) {
+    G6_LAUNCH(6)
+  } else if (wgs <= 2 * g_num_cus) {
+    G6_LAUNCH(4)
+  } else {
+    G6_LAUNCH(3)
+  }
+#undef G6_LAUNCH
   return vd_launch_status();
 }
 

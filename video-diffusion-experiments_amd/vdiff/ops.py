@@ -193,6 +193,17 @@ def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, 
     return out
 
 
+def softmax_rows(s, out=None):
+    """fp32 scores [rows, cols] in log2 units -> bf16 probabilities (row softmax)."""
+    _dev(s, out)
+    rows, cols = s.shape
+    if out is None:
+        out = torch.empty(rows, cols, device=s.device, dtype=BF16)
+    check(lib().vd_softmax_rows(_p(s), s.stride(0), rows, cols, _p(out), out.stride(0), _stream()),
+          "vd_softmax_rows")
+    return out
+
+
 # ---------------------------------------------------------------- step glue
 def timestep_embed(ts, dim, step_idx=None, batch=None, out=None):
     _dev(ts, step_idx)

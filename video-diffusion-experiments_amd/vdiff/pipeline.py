@@ -19,9 +19,11 @@ num_inference_steps times with no host work in between.  The cross-attention
 K/V of the (constant) prompt embeddings are projected once per video, outside
 the graph.
 
-Out of scope: CLIP text encoding (a deterministic stub
-encoder stands in; real embeddings can be passed as prompt_embeds) and VAE
-decoding (output_type="latent" only).
+Out of scope: CLIP text encoding (a deterministic stub encoder
+stands in; real embeddings can be passed as prompt_embeds).  VAE decoding (§8f
+rank 1) runs when the pipeline holds a `vdiff.AutoencoderKL`: output_type "pt" /
+"np" return diffusers' postprocessed video ((B, F, 3, H, W) tensor / (B, F, H, W, 3)
+array in [0, 1]), "latent" the final latents.
 """
 from __future__ import annotations
 
@@ -32,6 +34,7 @@ import torch
 
 from . import ops
 from .models.unet_motion import CIN_PAD, UNetMotionModel
+from .models.vae import AutoencoderKL
 from .sched.ddim import DDIMScheduler
 from .weights import init_synthetic_
 
@@ -142,14 +145,18 @@ class AnimateDiffPipeline:
         self.unet.dist = dist
 
     @classmethod
-    def from_config(cls, config="full", device="cuda", seed=0, scheduler=None, dist=None):
+    def from_config(cls, config="full", device="cuda", seed=0, scheduler=None, dist=None, vae=None):
+        """Synthetic-weight pipeline; vae=None (latents only), "tiny"/"full" (a synthetic
+        AutoencoderKL of that config) or an AutoencoderKL instance."""
         unet = UNetMotionModel(config)
         init_synthetic_(unet, seed)
         unet = unet.to(device=device, dtype=torch.bfloat16)
         unet.prepare()
         sched = scheduler or DDIMScheduler.from_config(None, beta_schedule="linear", steps_offset=1,
                                                        clip_sample=False)
-        return cls(unet, sched, dist=dist)
+        if isinstance(vae, str):
+            vae = init_synthetic_(AutoencoderKL(vae), seed).to(device=device, dtype=torch.bfloat16).prepare()
+        return cls(unet, sched, dist=dist, vae=vae)
 
     @classmethod
     def from_pretrained(cls, *args, **kwargs):
@@ -157,7 +164,7 @@ class AnimateDiffPipeline:
                                   "and vdiff.weights.load_diffusers_state_dict() for local safetensors")
 
     def enable_vae_slicing(self):
-        pass
+        pass  # decoding is always chunked (AutoencoderKL.frames_per_chunk)
 
     def enable_model_cpu_offload(self, *a, **k):
         pass  # 288 GB HBM: the 12 GB-GPU workaround is unnecessary
@@ -171,15 +178,38 @@ class AnimateDiffPipeline:
         return torch.stack([self.text_encoder(p) for p in prompt])
 
     @torch.no_grad()
+    def decode_latents(self, latents):
+        """diffusers AnimateDiffPipeline.decode_latents: latents / scaling_factor, frames
+        batched frame-major through vae.decode, -> (B, 3, F, H, W) fp32 in about [-1, 1]."""
+        if self.vae is None:
+            raise ValueError("this pipeline has no VAE (pass vae=vdiff.AutoencoderKL(...).to(...))")
+        B, Cc, Fr, h, w = latents.shape
+        z = latents.float() / self.vae.config["scaling_factor"]
+        z = z.permute(0, 2, 1, 3, 4).reshape(B * Fr, Cc, h, w)
+        img = self.vae.decode(z).sample
+        return img[None].reshape((B, Fr) + tuple(img.shape[1:])).permute(0, 2, 1, 3, 4).float()
+
+    @staticmethod
+    def postprocess_video(video, output_type):
+        """diffusers VideoProcessor.postprocess_video for "pt" / "np": per video, frames first,
+        denormalised (x / 2 + 0.5).clamp(0, 1)."""
+        v = (video / 2 + 0.5).clamp(0, 1).permute(0, 2, 1, 3, 4)      # (B, F, 3, H, W)
+        if output_type == "pt":
+            return v
+        return v.permute(0, 1, 3, 4, 2).cpu().numpy()                  # (B, F, H, W, 3)
+
+    @torch.no_grad()
     def __call__(self, prompt=None, num_frames=16, height=None, width=None, num_inference_steps=50,
                  guidance_scale=7.5, negative_prompt=None, num_videos_per_prompt=1, eta=0.0,
                  generator=None, latents=None, prompt_embeds=None, negative_prompt_embeds=None,
                  output_type="latent", return_dict=True, use_graph=True, **unused):
         if eta != 0.0:
             raise NotImplementedError("eta > 0")
-        if output_type != "latent":
-            raise NotImplementedError("VAE decode is out of scope for this build (SURVEY.md §8f): "
-                                      "use output_type='latent'")
+        if output_type not in ("latent", "pt", "np"):
+            raise NotImplementedError(f"output_type {output_type!r}: PIL is not part of this build; "
+                                      "use 'pt', 'np' or 'latent'")
+        if output_type != "latent" and self.vae is None:
+            raise ValueError(f"output_type {output_type!r} needs a VAE: AnimateDiffPipeline(..., vae=...)")
         dev = self.unet.device
         sample = self.unet.config["sample_size"]
         h = (height or sample * 8) // 8
@@ -212,4 +242,6 @@ class AnimateDiffPipeline:
         out = loop.run()
         if self.dist is not None:
             out = self.dist.all_gather_frames(out)
+        if output_type != "latent":
+            out = self.postprocess_video(self.decode_latents(out), output_type)
         return AnimateDiffPipelineOutput(frames=out) if return_dict else (out,)
