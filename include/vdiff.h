@@ -163,6 +163,15 @@ int vd_temporal_force_valu(int32_t on);
 int vd_softmax_rows(const float* s, int64_t ld_s, int64_t rows, int64_t cols, void* p,
                     int64_t ld_p, vd_stream_t stream);
 
+/* Temporal-consistency metric cores (experiments/
+ * 06_measure_grid_search.py compute_mse :209-211 over consecutive frames and
+ * compute_flicker_index :221-235) for a batch of uint8 videos [videos][frames][bytes]
+ * (bytes_per_frame = H*W*3, multiple of 16, base 16-byte aligned), exact integers:
+ *   sse[v][f] = sum (x[f+1]-x[f])^2 (f < frames-1); sad[v][f] = sum |x[f]-2x[f+1]+x[f+2]|
+ * (f < frames-2; sad may be NULL when frames == 2).  2 <= frames <= 32. */
+int vd_frame_metrics(const void* frames_u8, int64_t videos, int32_t frames, int64_t bytes_per_frame,
+                     uint64_t* sse, uint64_t* sad, vd_stream_t stream);
+
 /* ---------------------------------------------------------------- step glue
  * vd_timestep_embed: diffusers Timesteps(dim, flip_sin_to_cos=True, shift 0)
  *   (a12) -> bf16 [B][dim].  Timestep = ts[*step_idx] if step_idx else ts[b].

@@ -159,3 +159,22 @@ def test_euler_oracle_step_is_probability_flow_update():
     got, x0 = euler_ref.euler_step(e, x, 14.6, 12.0)
     torch.testing.assert_close(got, x + (12.0 - 14.6) * e, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(x0, x - 14.6 * e, rtol=1e-6, atol=1e-5)
+
+
+# ---------------------------------------------------------------- metrics
+def test_metrics_oracle_pinned_to_reference_records():
+    """oracle/metrics_ref.py on the committed frames of one reference experiment reproduces the
+    reference's own outputs/06_grid_search_metrics record; the recorded sweep over all 78
+    experiments (tests/golden/make_metrics_golden.py) stays within 1e-6 relative."""
+    import json
+    from oracle import metrics_ref
+    d = GOLD / "metrics" / "portrait_cfg9.0_steps25"
+    ref = json.loads((d / "metrics.json").read_text())
+    frames = metrics_ref.load_frames_u8(d / "frames")
+    assert frames.shape == (16, 512, 512, 3)
+    got = metrics_ref.measure_frames(frames, lpips=[m["lpips"] for m in ref["frame_metrics"]])
+    for k in ("mean_mse", "std_mse", "mean_psnr", "flicker_index", "temporal_consistency_score"):
+        assert got[k] == pytest.approx(ref[k], rel=1e-6), k
+    sweep = json.loads((GOLD / "metrics" / "oracle_vs_reference.json").read_text())
+    assert sweep["experiments"] == 78
+    assert max(sweep["max_relative_deviation"].values()) < 1e-6
