@@ -519,6 +519,43 @@ __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, cons
         }
       }
     }
+    if (!EXACT && t > 1) {
+      // ---- fast pass: rescale from the row sum of tiles 0..t-1 when it outgrows 2^32.
+      // Checked one tile late, after this tile's QK^T MFMAs are issued, so reading the PV
+      // accumulator does not drain the MFMA pipe right behind the PV chain; this tile's
+      // scores (formed with the old mu) take the same shift as the exact path's.
+      float lq[QB];
+      bool resc = false, over = false;
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const float lown = oacc[C::L_DB][qb][C::L_I];
+        const float lp = partner32(lown);
+        lq[qb] = hh == C::L_H ? lown : lp;
+        resc |= lq[qb] > RESCALE;
+        over |= !(lq[qb] < BAD);
+      }
+      if (__any(over)) {
+        bad = true;
+      } else if (__any(resc)) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          const float step = lq[qb] > RESCALE ? __builtin_amdgcn_logf(lq[qb]) : 0.f;  // log2(l)
+          const float nmu = (float)(__bf16)(mu[qb] + (UNITC ? step : step / c));
+          const float delta = nmu - mu[qb];
+          const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
+          mu[qb] = nmu;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[kb][qb][i] -= delta;
+#pragma unroll
+          for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
+          if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
+        }
+      }
+    }
     // ---- P = exp2(x), packed: registers 8*s2 .. 8*s2+7 of tile kb = k-step (kb, s2)
     bf16x8 pf[2][2][QB];
 #pragma unroll
@@ -544,35 +581,6 @@ __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, cons
           for (int qb = 0; qb < QB; ++qb)
             oacc[db][qb] =
                 __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[db][kb][s2], pf[kb][s2][qb], oacc[db][qb], 0, 0, 0);
-    if (!EXACT && t > 0) {  // ---- fast pass: rescale from the row sum when it outgrows 2^32
-      float lq[QB];
-      bool resc = false, over = false;
-#pragma unroll
-      for (int qb = 0; qb < QB; ++qb) {
-        const float lown = oacc[C::L_DB][qb][C::L_I];
-        const float lp = partner32(lown);
-        lq[qb] = hh == C::L_H ? lown : lp;
-        resc |= lq[qb] > RESCALE;
-        over |= !(lq[qb] < BAD);
-      }
-      if (__any(over)) {
-        bad = true;
-      } else if (__any(resc)) {
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
-          const float step = lq[qb] > RESCALE ? __builtin_amdgcn_logf(lq[qb]) : 0.f;  // log2(l)
-          const float nmu = (float)(__bf16)(mu[qb] + (UNITC ? step : step / c));
-          const float delta = nmu - mu[qb];
-          const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
-          mu[qb] = nmu;
-#pragma unroll
-          for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
-          if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
-        }
-      }
-    }
     if (t + 1 < ntiles) {
       bf16_t* nb = lds + (buf ^ 1) * C::STAGE;
 #pragma unroll
@@ -583,6 +591,16 @@ __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, cons
       }
     }
     __syncthreads();
+  }
+  if (!EXACT) {  // the last tiles' row sums were not checked in the loop
+    bool over = false;
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      const float lown = oacc[C::L_DB][qb][C::L_I];
+      const float lp = partner32(lown);  // every lane takes part in the swap
+      over |= !((hh == C::L_H ? lown : lp) < BAD);
+    }
+    bad |= __any(over);
   }
   return bad;
 }
