@@ -383,11 +383,11 @@ def test_layer_norm_pe(cuda):
 
 
 # ---------------------------------------------------------------- attention
-def sdpa_ref(q, k, v, batch, heads, sq, skv, d, kv_div=1):
+def sdpa_ref(q, k, v, batch, heads, sq, skv, d, kv_div=1, scale=None):
     q = q.double().reshape(batch, sq, heads, d).transpose(1, 2)
     kb = k.double().reshape(batch // kv_div, skv, heads, d).transpose(1, 2).repeat_interleave(kv_div, 0)
     vb = v.double().reshape(batch // kv_div, skv, heads, d).transpose(1, 2).repeat_interleave(kv_div, 0)
-    w = torch.softmax(q @ kb.transpose(-1, -2) / math.sqrt(d), -1)
+    w = torch.softmax(q @ kb.transpose(-1, -2) * (d ** -0.5 if scale is None else scale), -1)
     return (w @ vb).transpose(1, 2).reshape(batch * sq, heads * d)
 
 
@@ -487,6 +487,19 @@ def test_flash_attention_deferred_max(attn_path, kind):
     # weights on a few keys and |O| << |V|); a mis-scaled tile shows up as errors >= 0.1.
     close_bf16(got, sdpa_ref(q, k, v, 1, 1, sq, skv, d), abs_frac=2e-3 * v.float().abs().max().item()
                / sdpa_ref(q, k, v, 1, 1, sq, skv, d).abs().max().item())
+
+
+@pytest.mark.parametrize("kind", ["ramp", "creep", "late_spike", "huge_spike", "offset", "negative"])
+def test_flash_attention_deferred_max_unit_scale(attn_path, kind):
+    """The same score patterns through the unit-scale fast pass (the model's call, softmax
+    scale folded into q; its row-sum check runs one tile late)."""
+    q, k, v = _deferred_max_case(kind)
+    sq, skv, d = q.shape[0], k.shape[0], q.shape[1]
+    q = bf(q.float() * d ** -0.5 * math.log2(math.e))  # scores in log2 units
+    got = ops.attention(q, k, v, 1, 1, sq, skv, d, scale=1.0 / math.log2(math.e))
+    assert torch.isfinite(got.float()).all()
+    want = sdpa_ref(q, k, v, 1, 1, sq, skv, d, scale=1.0 / math.log2(math.e))
+    close_bf16(got, want, abs_frac=2e-3 * v.float().abs().max().item() / want.abs().max().item())
 
 
 def test_flash_attention_unit_scale(cuda):
