@@ -130,6 +130,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--attn-reps", type=int, default=20)
+    ap.add_argument("--no-nocfg", action="store_true", help="skip the B=1 (no-CFG) variant")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -185,6 +186,30 @@ def main():
     sps = args.steps / elapsed
     ms = 1e3 * elapsed / args.steps
 
+    # the B=1 (no-CFG, guidance 1) variant, labelled — same graph-captured
+    # loop on the conditional half only
+    nocfg = None
+    if not args.no_nocfg:
+        loop1 = DenoiseLoop(unet, sched, lat, ehs[1:].cuda(), 1.0, timesteps=ts, use_graph=not args.no_graph)
+        loop1.prime()
+        loop1.run(args.warmup)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        loop1.run(args.steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e1 = time.perf_counter() - t1
+        if world > 1:
+            tt = torch.tensor([e1], device="cuda", dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            e1 = tt.item()
+        nocfg = {"value": round(args.steps / e1, 4), "unit": "denoising steps/s", "ms_per_step": round(1e3 * e1 / args.steps, 3),
+                 "config": "guidance_scale 1 (no CFG): UNet batch 1 per step, same frames/latents"}
+        del loop1
+
     roof = time_attention(2 * fl, args.attn_reps, torch.cuda.current_stream())
     roof["traffic"], roof["traffic_source"] = pmc_traffic(2 * fl)
     step_tf = STEP_TFLOP[cfg_name] * (frames / (16 if cfg_name == "full" else 4)) / (ms * 1e-3) / world
@@ -223,6 +248,7 @@ def main():
                           "achieved": round(step_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                           "frac": round(step_tf / PEAK_BF16_TFLOPS, 4)},
             "cpu_baseline": cpu,
+            "no_cfg": nocfg,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

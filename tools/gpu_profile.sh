@@ -14,7 +14,7 @@ if [ -z "$NO_BENCH" ]; then
   [ $rc -ne 0 ] && exit $rc
 fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps ${PROF_STEPS:-5} --warmup 2 --no-cpu-baseline $PROF_ARGS > $GRAFT_REPO_ROOT/gpurun_out/prof/bench_prof.log 2>&1
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps ${PROF_STEPS:-5} --warmup 2 --no-cpu-baseline --no-nocfg $PROF_ARGS > $GRAFT_REPO_ROOT/gpurun_out/prof/bench_prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -2 $GRAFT_REPO_ROOT/gpurun_out/prof/bench_prof.log
 find $GRAFT_REPO_ROOT/gpurun_out/prof -name "*.csv" | head
 exit $rc

@@ -37,3 +37,14 @@ print("top shapes (per step):")
 for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:40]:
     print(f"  {sum(v) / steps / 1e3:9.1f} us  x{len(v) / steps:5.1f}  avg {sum(v) / len(v) / 1e3:8.1f} us  "
           f"{k[0]} grid={k[1]} wg={k[2]}")
+
+# bench.py's roofline kernel: after the last step, time_attention() launches the L1
+# self-attention kernel (3 warm-up + attn_reps timed) on its own; those launches close the
+# trace and their average must agree with the bench line's roofline.avg_launch_ms.
+after = [r for r in rows if int(r["Start_Timestamp"]) > t1 and "flash32_kernel" in r["Kernel_Name"]]
+if len(after) > 3:
+    timed = after[3:]
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed]
+    print(f"roofline kernel (bench time_attention): {len(d)} timed launches of "
+          f"{timed[0]['Kernel_Name'].split('(')[0].replace('void ', '')[:60]} "
+          f"grid={timed[0]['Grid_Size_X']}, avg {sum(d) / len(d) / 1e3:.1f} us")
