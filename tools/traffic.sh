@@ -6,7 +6,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT; ROUND=$1; CASE=$2; KERN=$3
 OUT=$R/gpurun_out/traffic_$ROUND; mkdir -p $OUT
-cd /tmp && export TMPDIR=/tmp KB_PATHS=v2
+cd /tmp && export TMPDIR=/tmp KB_PATHS=${KB_PATHS:-v2}
 i=0
 for c in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
