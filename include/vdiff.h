@@ -120,6 +120,19 @@ int vd_gn_finalize(const float* ws, int64_t n_inst, int32_t n_split_total, int64
 int vd_gn_apply(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1,
                 int64_t C, int64_t n_inst, int64_t pix_per_inst, const float* scale_shift,
                 int32_t silu, void* y, int64_t ldy, vd_stream_t stream);
+/* Two-launch GroupNorm for image instances (ResnetBlock2D / Transformer2DModel / VAE
+ * norms): vd_gn_partial_g writes ONE {n, mean, M2} record per (instance, split, group)
+ * (ws: n_inst*n_split*groups float4; C <= 2560, 256 % groups == 0), and vd_gn_apply_g
+ * finalizes those records itself (prologue, per workgroup of rows_per_blk rows) before
+ * applying y = (x-mean)*rstd*gamma + beta (+SiLU) — no finalize launch. */
+int vd_gn_partial_g(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1,
+                    int64_t C, int64_t n_inst, int64_t pix_per_inst, int32_t n_split,
+                    int32_t groups, float* ws, vd_stream_t stream);
+int vd_gn_apply_g(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1,
+                  int64_t C, int64_t n_inst, int64_t pix_per_inst, const float* ws,
+                  int32_t n_split_total, int32_t groups, float eps, const float* gamma,
+                  const float* beta, int32_t silu, void* y, int64_t ldy, int64_t rows_per_blk,
+                  vd_stream_t stream);
 
 /* ---------------------------------------------------------------- LayerNorm
  * BasicTransformerBlock.norm1/2/3 (eps 1e-5) over the last dim of bf16 rows,

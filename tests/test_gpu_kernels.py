@@ -369,6 +369,31 @@ def test_group_norm(cuda, kind):
     close_bf16(got, want)
 
 
+@pytest.mark.parametrize("n_inst,pix,C,c0,silu", [(4, 64, 1280, 1280, True), (2, 4096, 320, 320, False),
+                                                   (4, 64, 2560, 1280, True), (3, 100, 640, 640, True),
+                                                   (1, 7, 64, 32, False), (32, 1024, 640, 640, True)])
+@pytest.mark.parametrize("path", ["2pass", "4pass"])
+def test_group_norm_paths(cuda, n_inst, pix, C, c0, silu, path):
+    """The two-launch image GroupNorm (per-group records, finalize in the apply prologue) and
+    the partial/finalize/apply path the motion module takes (forced by an identity `gather`),
+    over L4-like small instances, a whole 64x64 image, the 2560-channel up-block concat,
+    ragged row blocks and a 7-pixel instance."""
+    torch.manual_seed(3)
+    x = rnd(n_inst * pix, c0) * 3 + 1.5
+    x1 = rnd(n_inst * pix, C - c0) - 0.7 if c0 < C else None
+    g = torch.rand(C, device=cuda) + 0.5
+    be = torch.randn(C, device=cuda)
+    if path == "2pass":  # the two-launch kernels directly (the policy picks them for large norms only)
+        got = ops.group_norm_2pass(x, n_inst, pix, 32, 1e-6, g, be, silu=silu, x1=x1)
+    else:
+        got = ops.group_norm(x, n_inst, pix, 32, 1e-6, g, be, silu=silu, x1=x1, two_pass=False)
+    xx = x if x1 is None else torch.cat([x, x1], 1)
+    t = xx.double().reshape(n_inst, pix, C).permute(0, 2, 1)
+    want = F.group_norm(t, 32, g.double(), be.double(), 1e-6)
+    want = (F.silu(want) if silu else want).permute(0, 2, 1).reshape(-1, C)
+    close_bf16(got, want)
+
+
 def test_layer_norm_pe(cuda):
     rows, C, frames, pos = 4 * 16 * 24, 320, 16, 24
     x = rnd(rows, C) * 2 + 0.3

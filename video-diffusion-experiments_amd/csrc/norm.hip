@@ -22,11 +22,21 @@ __device__ __forceinline__ const bf16_t* gn_src(const bf16_t* x0, int64_t ldx0, 
   return c < c0 ? x0 + row * ldx0 + c : x1 + row * ldx1 + (c - c0);
 }
 
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float n2, float mean2,
+                                           float m22);
+
+// GREC = false: records per (instance, split, channel) (the motion-module norm, whose
+// records are all-gathered across ranks and combined by gn_finalize).  GREC = true: the
+// channels of each group are Chan-merged in LDS and ONE record per (instance, split,
+// group) is written, few enough for gn_apply_g to finalize in its prologue.
+constexpr int GN_CMAX = 2560;  // channels (incl. the up-block concat) of a group-record partial
+template <bool GREC>
 __global__ __launch_bounds__(NT) void gn_partial_kernel(const bf16_t* x0, int64_t ldx0, int64_t c0,
                                                         const bf16_t* x1, int64_t ldx1, int64_t C,
                                                         int64_t pix_per_inst, int n_split,
-                                                        float4* ws) {
+                                                        float4* ws, int groups) {
   __shared__ float4 red[NT * 8];  // [task][8 channels] {n, mean, M2, -}
+  __shared__ float4 chrec[GREC ? GN_CMAX : 1];
   const int inst = blockIdx.x / n_split;
   const int split = blockIdx.x % n_split;
   const int64_t pb = pix_per_inst * split / n_split;
@@ -35,7 +45,7 @@ __global__ __launch_bounds__(NT) void gn_partial_kernel(const bf16_t* x0, int64_
   const int nch = (int)(C / 8);
   const int PL = nch >= NT ? 1 : NT / nch;
   const int ntask = PL * nch;
-  float4* out = ws + ((int64_t)inst * n_split + split) * C;
+  float4* out = GREC ? chrec : ws + ((int64_t)inst * n_split + split) * C;
 
   for (int task = threadIdx.x; task < ((ntask + NT - 1) / NT) * NT; task += NT) {
     const bool active = task < ntask;
@@ -121,6 +131,29 @@ __global__ __launch_bounds__(NT) void gn_partial_kernel(const bf16_t* x0, int64_
         out[c] = make_float4(n, mean, m2, 0.f);
       }
       break;
+    }
+  }
+  if constexpr (GREC) {
+    // merge each group's cpg channel records: NT / groups threads per group, then a
+    // per-group pass over their partials (red is free again)
+    __syncthreads();
+    const int cpg = (int)(C / groups), tpg = NT / groups;
+    const int g = threadIdx.x / tpg, sub = threadIdx.x % tpg;
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    if (g < groups)
+      for (int q = sub; q < cpg; q += tpg) {
+        const float4 r = chrec[g * cpg + q];
+        chan_merge(n, mean, m2, r.x, r.y, r.z);
+      }
+    red[threadIdx.x] = make_float4(n, mean, m2, 0.f);
+    __syncthreads();
+    if (threadIdx.x < groups) {
+      float gn = 0.f, gm = 0.f, g2 = 0.f;
+      for (int i = 0; i < tpg; ++i) {
+        const float4 r = red[threadIdx.x * tpg + i];
+        chan_merge(gn, gm, g2, r.x, r.y, r.z);
+      }
+      ws[((int64_t)inst * n_split + split) * groups + threadIdx.x] = make_float4(gn, gm, g2, 0.f);
     }
   }
 }
@@ -212,6 +245,73 @@ __global__ __launch_bounds__(NT) void gn_apply_kernel(const bf16_t* x0, int64_t 
   }
 }
 
+// GroupNorm apply that finalizes its own statistics: one workgroup per (instance, row
+// block); the prologue Chan-merges the instance's n_split x groups records (NT / groups
+// threads per group, then one thread per group), forms {a, b} for every channel in LDS,
+// and the body is gn_apply's 16-byte vector pass over the block's rows.  Removes the
+// separate finalize launch (and its ~5 us floor) from every image-instance GroupNorm.
+__global__ __launch_bounds__(NT) void gn_apply_g_kernel(const bf16_t* x0, int64_t ldx0, int64_t c0,
+                                                        const bf16_t* x1, int64_t ldx1, int64_t C,
+                                                        int64_t pix_per_inst, int64_t rows_per_blk, int bpi,
+                                                        const float4* ws, int n_split, int groups, float eps,
+                                                        const float* gamma, const float* beta, int silu,
+                                                        bf16_t* y, int64_t ldy) {
+  __shared__ float4 part[NT];
+  __shared__ float2 gst[NT];
+  __shared__ float2 ab[GN_CMAX];
+  const int inst = blockIdx.x / bpi, blk = blockIdx.x % bpi;
+  const int tpg = NT / groups;
+  {
+    const int g = threadIdx.x % groups, s0 = threadIdx.x / groups;
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    const float4* rec = ws + (int64_t)inst * n_split * groups + g;
+    for (int sp = s0; sp < n_split; sp += tpg) {
+      const float4 r = rec[(int64_t)sp * groups];
+      chan_merge(n, mean, m2, r.x, r.y, r.z);
+    }
+    part[threadIdx.x] = make_float4(n, mean, m2, 0.f);
+  }
+  __syncthreads();
+  if (threadIdx.x < groups) {
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    for (int i = 0; i < tpg; ++i) {
+      const float4 r = part[threadIdx.x + i * groups];
+      chan_merge(n, mean, m2, r.x, r.y, r.z);
+    }
+    const float var = n > 0.f ? m2 / n : 0.f;
+    gst[threadIdx.x] = make_float2(mean, rsqrtf(var + eps));
+  }
+  __syncthreads();
+  const int cpg = (int)(C / groups);
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const float2 st = gst[c / cpg];
+    const float a = st.y * gamma[c];
+    ab[c] = make_float2(a, beta[c] - st.x * a);
+  }
+  __syncthreads();
+  const int64_t nch = C / 8;
+  const int64_t r0 = (int64_t)inst * pix_per_inst + (int64_t)blk * rows_per_blk;
+  const int64_t r1 = min((int64_t)inst * pix_per_inst + pix_per_inst, r0 + rows_per_blk);
+  const int64_t total = (r1 - r0) * nch;
+  for (int64_t idx = threadIdx.x; idx < total; idx += NT) {
+    const int64_t row = r0 + idx / nch;
+    const int64_t c = (idx % nch) * 8;
+    const uint4 u = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row, c);
+    float f[8];
+    unpack8(u, f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float2 t = ab[c + q];
+      f[q] = fmaf(f[q], t.x, t.y);
+    }
+    if (silu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = silu_f(f[e]);
+    }
+    *(uint4*)(y + row * ldy + c) = pack8(f);
+  }
+}
+
 // One wave per row; up to LNCH 16-byte chunks per lane (C <= 64*8*LNCH).
 constexpr int LNCH = 4;
 __global__ __launch_bounds__(NT) void layernorm_kernel(const bf16_t* x, int64_t ldx, int64_t rows,
@@ -280,9 +380,41 @@ extern "C" int vd_gn_partial(const void* x0, int64_t ldx0, int64_t c0, const voi
   if (c0 < C) VD_CHECK_ARG(x1 && ldx1 % 8 == 0 && al16(x1));
   VD_CHECK_ARG(n_inst > 0 && pix_per_inst > 0 && n_split > 0 && n_split <= pix_per_inst);
   VD_CHECK_ARG(n_inst * n_split < 0x7fffffff);
-  hipLaunchKernelGGL(gn_partial_kernel, dim3((unsigned)(n_inst * n_split)), dim3(NT), 0,
+  hipLaunchKernelGGL(gn_partial_kernel<false>, dim3((unsigned)(n_inst * n_split)), dim3(NT), 0,
                      (hipStream_t)stream, (const bf16_t*)x0, ldx0, c0, (const bf16_t*)x1, ldx1, C,
-                     pix_per_inst, n_split, (float4*)ws);
+                     pix_per_inst, n_split, (float4*)ws, 1);
+  return vd_launch_status();
+}
+
+extern "C" int vd_gn_partial_g(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1, int64_t C,
+                               int64_t n_inst, int64_t pix_per_inst, int32_t n_split, int32_t groups, float* ws,
+                               vd_stream_t stream) {
+  VD_CHECK_ARG(x0 && ws && C > 0 && C % 8 == 0 && C <= GN_CMAX && c0 % 8 == 0 && c0 > 0 && c0 <= C);
+  VD_CHECK_ARG(groups > 0 && NT % groups == 0 && C % groups == 0);
+  VD_CHECK_ARG(ldx0 % 8 == 0 && al16(x0) && al16(ws));
+  if (c0 < C) VD_CHECK_ARG(x1 && ldx1 % 8 == 0 && al16(x1));
+  VD_CHECK_ARG(n_inst > 0 && pix_per_inst > 0 && n_split > 0 && n_split <= pix_per_inst);
+  VD_CHECK_ARG(n_inst * n_split < 0x7fffffff);
+  hipLaunchKernelGGL(gn_partial_kernel<true>, dim3((unsigned)(n_inst * n_split)), dim3(NT), 0,
+                     (hipStream_t)stream, (const bf16_t*)x0, ldx0, c0, (const bf16_t*)x1, ldx1, C,
+                     pix_per_inst, n_split, (float4*)ws, groups);
+  return vd_launch_status();
+}
+
+extern "C" int vd_gn_apply_g(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1, int64_t C,
+                             int64_t n_inst, int64_t pix_per_inst, const float* ws, int32_t n_split_total,
+                             int32_t groups, float eps, const float* gamma, const float* beta, int32_t silu,
+                             void* y, int64_t ldy, int64_t rows_per_blk, vd_stream_t stream) {
+  VD_CHECK_ARG(x0 && y && ws && gamma && beta && C > 0 && C % 8 == 0 && C <= GN_CMAX);
+  VD_CHECK_ARG(c0 % 8 == 0 && c0 > 0 && c0 <= C && groups > 0 && NT % groups == 0 && C % groups == 0);
+  VD_CHECK_ARG(ldx0 % 8 == 0 && ldy % 8 == 0 && al16(x0) && al16(y) && al16(ws));
+  if (c0 < C) VD_CHECK_ARG(x1 && ldx1 % 8 == 0 && al16(x1));
+  VD_CHECK_ARG(n_inst > 0 && pix_per_inst > 0 && n_split_total > 0 && rows_per_blk > 0);
+  const int64_t bpi = (pix_per_inst + rows_per_blk - 1) / rows_per_blk;
+  VD_CHECK_ARG(n_inst * bpi < 0x7fffffff);
+  hipLaunchKernelGGL(gn_apply_g_kernel, dim3((unsigned)(n_inst * bpi)), dim3(NT), 0, (hipStream_t)stream,
+                     (const bf16_t*)x0, ldx0, c0, (const bf16_t*)x1, ldx1, C, pix_per_inst, rows_per_blk, (int)bpi,
+                     (const float4*)ws, n_split_total, groups, eps, gamma, beta, silu, (bf16_t*)y, ldy);
   return vd_launch_status();
 }
 

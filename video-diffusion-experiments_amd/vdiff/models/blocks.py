@@ -189,7 +189,7 @@ class AnimateDiffTransformer3D(nn.Module):
         B, Fl = ctx.batch, ctx.frames
         dist = ctx.dist
         gather = dist.gather_gn_partials if dist is not None else None
-        hn = ops.group_norm(x.t, B, Fl * hw, self.groups, 1e-6, self._g, self._b, gather=gather)
+        hn = ops.group_norm(x.t, B, Fl * hw, self.groups, 1e-6, self._g, self._b, gather=gather, two_pass=False)
         h = ops.gemm(hn, self._wi, bias=self._bi)
         blk = self.transformer_blocks[0]
         if dist is None:

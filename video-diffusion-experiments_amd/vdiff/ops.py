@@ -146,15 +146,44 @@ def gn_apply(x, ss, pix, silu, x1=None, out=None):
     return out
 
 
-def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, gather=None):
+def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, gather=None, two_pass=True):
     """GroupNorm(+SiLU) over NHWC rows; instance = `pix` consecutive rows.
-    `gather(ws) -> ws'` (optional) merges partial statistics across ranks."""
+    Image-instance norms (two_pass): per-group partial records, and an apply that finalizes
+    them itself (two launches).  The motion-module norm (two_pass=False: its instance is a
+    whole video, so it needs hundreds of splits) runs partial / [gather] / finalize / apply,
+    where `gather(ws) -> ws'` merges the partial statistics across frame-sharded ranks."""
     C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
+    # two launches win by 2-5 us per norm at 16+ instances or 16k+ rows; on the few small
+    # instances of a 2-frame rank's deep levels the four-launch path is 1-2 us faster
+    # (tools/gn_bench.py)
+    big = n_inst >= 16 or n_inst * pix >= 16384
+    if two_pass and big and gather is None and C <= 2560 and 256 % groups == 0:
+        return group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=silu, x1=x1)
     ws = gn_partial(x, C, n_inst, pix, gn_splits(n_inst, pix), x1=x1)
     if gather is not None:
         ws = gather(ws)
     ss = gn_finalize(ws, groups, eps, gamma, beta)
     return gn_apply(x, ss, pix, silu, x1=x1)
+
+
+def group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, out=None):
+    """vd_gn_partial_g + vd_gn_apply_g.  Splits: <= 32 per instance (the apply prologue reads
+    splits x groups records), ~2048 partial blocks in all; ~1024 apply blocks in all (tools/gn_bench.py)."""
+    _dev(x, x1, gamma, beta, out)
+    C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
+    n_split = max(1, min(pix // 16, math.ceil(2048 / n_inst), 32))
+    ws = torch.empty(n_inst, n_split, groups, 4, device=x.device, dtype=torch.float32)
+    x1p, ld1 = (_p(x1), _rows(x1)) if x1 is not None else (None, 0)
+    check(lib().vd_gn_partial_g(_p(x), _rows(x), x.shape[1], x1p, ld1, C, n_inst, pix, n_split, groups, _p(ws),
+                                _stream()), "vd_gn_partial_g")
+    if out is None:
+        out = torch.empty(x.shape[0], C, device=x.device, dtype=BF16)
+    bpi = max(1, min(pix, math.ceil(1024 / n_inst)))
+    rows_per_blk = math.ceil(pix / bpi)
+    check(lib().vd_gn_apply_g(_p(x), _rows(x), x.shape[1], x1p, ld1, C, n_inst, pix, _p(ws), n_split, groups, eps,
+                              _p(gamma), _p(beta), int(silu), _p(out), _rows(out), rows_per_blk, _stream()),
+          "vd_gn_apply_g")
+    return out
 
 
 def layer_norm(x, gamma, beta, eps=1e-5, pe=None, pe_div=1, pe_period=1, out=None):
