@@ -93,6 +93,16 @@ def pmc_traffic(n_img):
     return t["traffic_bytes_per_launch"] * n_img / 32.0, files[-1].name
 
 
+def pmc_mfma_busy():
+    """MFMA-busy share of the roofline kernel (SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x
+    GRBM_GUI_ACTIVE/8) from the newest committed profiles/rNN_mfma_busy.json (tools/mfma_busy.sh:
+    one PMC pass over a bench.py run).  Counts padded MFMA work, unlike `frac`."""
+    files = sorted((ROOT / "profiles").glob("r*_mfma_busy.json"))
+    if not files:
+        return None, None
+    return json.loads(files[-1].read_text()).get("mfma_busy_frac"), files[-1].name
+
+
 def cpu_baseline(unet_gpu, cfg_name, frames_sample, frames_full):
     """Oracle (oracle/unet_ref.py, fp32 PyTorch-CPU) on `frames_sample` frames of the
     same CFG-batch step; scaled to steps/s of the full `frames_full`-frame video."""
@@ -212,6 +222,7 @@ def main():
 
     roof = time_attention(2 * fl, args.attn_reps, torch.cuda.current_stream())
     roof["traffic"], roof["traffic_source"] = pmc_traffic(2 * fl)
+    roof["mfma_busy"], roof["mfma_busy_source"] = pmc_mfma_busy()
     step_tf = STEP_TFLOP[cfg_name] * (frames / (16 if cfg_name == "full" else 4)) / (ms * 1e-3) / world
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
