@@ -877,7 +877,11 @@ __global__ __launch_bounds__(NT) void temporal_mfma_kernel(
   const int64_t stride = (int64_t)gridDim.x * 4;
   const bool unitc = c == 1.0f;
   const int vtr = (4 * fq + (fr >> 2)) * C::VS + 4 * (fr & 3);  // tr-read lane offset in a column block
-  for (int64_t item = (int64_t)blockIdx.x * 4 + wave; item < nitems; item += stride) {
+  // XCD-aware (T1): the blocks holding the other heads of the same position (whose 80-byte
+  // head slices share 128-byte lines of the Q/K/V/O rows) get adjacent logical ids, which
+  // xcd_remap keeps on one XCD, so a shared line is fetched into one L2, not two
+  const int64_t lblk = xcd_remap(blockIdx.x, gridDim.x);
+  for (int64_t item = lblk * 4 + wave; item < nitems; item += stride) {
     const int h = (int)(item % heads);
     const int64_t bp = item / heads;
     const int64_t p = bp % positions, b = bp / positions;
