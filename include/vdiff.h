@@ -142,6 +142,9 @@ int vd_gn_apply_g(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int6
 int vd_layernorm(const void* x, int64_t ldx, int64_t rows, int64_t C, const float* gamma,
                  const float* beta, float eps, const float* pe, int64_t pe_div,
                  int64_t pe_period, void* y, int64_t ldy, vd_stream_t stream);
+/* Test/benchmark hook: multi_row = 0 forces the one-row-per-wave LayerNorm kernel (default 1:
+ * several rows per wave for C in {320, 640, 1280}). */
+int vd_layernorm_select(int32_t multi_row);
 
 /* ---------------------------------------------------------------- attention
  * softmax(q k^T * scale) v per (batch b, head h): replaces

@@ -394,6 +394,27 @@ def test_group_norm_paths(cuda, n_inst, pix, C, c0, silu, path):
     close_bf16(got, want)
 
 
+@pytest.mark.parametrize("C,rows", [(320, 4 * 16 * 24 + 5), (640, 1000), (1280, 333), (64, 77)])
+@pytest.mark.parametrize("multi_row", [1, 0])
+def test_layer_norm_kernels(cuda, C, rows, multi_row):
+    """Both LayerNorm kernels (several rows per wave for C in 320/640/1280, one row per wave
+    otherwise) with ragged row counts and the motion block's sinusoidal PE."""
+    from vdiff._lib import lib
+    x = rnd(rows, C) * 2 + 0.3
+    g, b = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda)
+    pe = torch.randn(16, C, device=cuda)
+    lib().vd_layernorm_select(multi_row)
+    try:
+        got = ops.layer_norm(x, g, b, pe=pe, pe_div=24, pe_period=16)
+        plain = ops.layer_norm(x, g, b)
+    finally:
+        lib().vd_layernorm_select(1)
+    f = (torch.arange(rows, device=cuda) // 24) % 16
+    ref = F.layer_norm(x.double(), (C,), g.double(), b.double(), 1e-5)
+    close_bf16(got, ref + pe.double()[f])
+    close_bf16(plain, ref)
+
+
 def test_layer_norm_pe(cuda):
     rows, C, frames, pos = 4 * 16 * 24, 320, 16, 24
     x = rnd(rows, C) * 2 + 0.3

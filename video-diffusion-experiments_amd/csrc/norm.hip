@@ -368,6 +368,69 @@ __global__ __launch_bounds__(NT) void layernorm_kernel(const bf16_t* x, int64_t 
   }
 }
 
+// Several rows per wave for C = 8 * LPR * CH (320 / 640 / 1280 with CH = 5): LPR lanes per
+// row, CH 16-byte chunks per lane, all issued before the first use, so a wave keeps
+// 64 x CH x 16 bytes in flight (the one-row-per-wave kernel leaves 24 of 64 lanes idle at
+// C = 320 and has one 16-byte load per lane outstanding).  Row sums by xor shuffles inside
+// each LPR-lane group; lane l of a group holds chunks l, l + LPR, ... (coalesced rows).
+template <int LPR, int CH>
+__global__ __launch_bounds__(NT) void layernorm_rows_kernel(const bf16_t* x, int64_t ldx, int64_t rows,
+                                                            const float* gamma, const float* beta, float eps,
+                                                            const float* pe, int64_t pe_div, int64_t pe_period,
+                                                            bf16_t* y, int64_t ldy) {
+  constexpr int C = 8 * LPR * CH, RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool ok = row < rows;
+  const int64_t rr = ok ? row : 0;
+  uint4 u[CH];
+#pragma unroll
+  for (int q = 0; q < CH; ++q) u[q] = *(const uint4*)(x + rr * ldx + (sub + q * LPR) * 8);
+  float v[CH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < CH; ++q) {
+    unpack8(u[q], v[q]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[q][e];
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / (float)C;
+  float s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < CH; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float t = v[q][e] - mean;
+      s2 = fmaf(t, t, s2);
+    }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+  const float rstd = rsqrtf(s2 / (float)C + eps);
+  if (!ok) return;
+  const float* per = pe ? pe + ((row / pe_div) % pe_period) * C : nullptr;
+#pragma unroll
+  for (int q = 0; q < CH; ++q) {
+    const int j = sub + q * LPR;
+    const float4 g0 = *(const float4*)(gamma + j * 8), g1 = *(const float4*)(gamma + j * 8 + 4);
+    const float4 b0 = *(const float4*)(beta + j * 8), b1 = *(const float4*)(beta + j * 8 + 4);
+    const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = fmaf((v[q][e] - mean) * rstd, gg[e], bb[e]);
+    if (per) {
+      const float4 p0 = *(const float4*)(per + j * 8), p1 = *(const float4*)(per + j * 8 + 4);
+      o[0] += p0.x; o[1] += p0.y; o[2] += p0.z; o[3] += p0.w;
+      o[4] += p1.x; o[5] += p1.y; o[6] += p1.z; o[7] += p1.w;
+    }
+    *(uint4*)(y + row * ldy + j * 8) = pack8(o);
+  }
+}
+
+int g_ln_rows = 1;  // 0: always the one-row-per-wave kernel (vd_layernorm_select)
+
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
@@ -453,9 +516,29 @@ extern "C" int vd_layernorm(const void* x, int64_t ldx, int64_t rows, int64_t C,
   VD_CHECK_ARG(ldx % 8 == 0 && ldy % 8 == 0 && al16(x) && al16(y) && al16(gamma) && al16(beta));
   if (pe) VD_CHECK_ARG(al16(pe) && pe_div > 0 && pe_period > 0);
   if (rows == 0) return VD_OK;
+#define LN_ROWS(LPR, CH)                                                                                   \
+  {                                                                                                        \
+    const int64_t rpb = (NT / 64) * (64 / LPR);                                                            \
+    hipLaunchKernelGGL((layernorm_rows_kernel<LPR, CH>), dim3((unsigned)((rows + rpb - 1) / rpb)), dim3(NT), 0, \
+                       (hipStream_t)stream, (const bf16_t*)x, ldx, rows, gamma, beta, eps, pe, pe_div,     \
+                       pe_period, (bf16_t*)y, ldy);                                                        \
+    return vd_launch_status();                                                                             \
+  }
+  if (g_ln_rows) {
+    if (C == 320) LN_ROWS(8, 5)
+    if (C == 640) LN_ROWS(16, 5)
+    if (C == 1280) LN_ROWS(32, 5)
+  }
+#undef LN_ROWS
   const int64_t blocks = (rows + 3) / 4;
   hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream,
                      (const bf16_t*)x, ldx, rows, (int)C, gamma, beta, eps, pe, pe_div, pe_period,
                      (bf16_t*)y, ldy);
   return vd_launch_status();
+}
+
+// Test/benchmark hook: 0 forces the one-row-per-wave LayerNorm kernel for every C.
+extern "C" int vd_layernorm_select(int32_t multi_row) {
+  g_ln_rows = multi_row != 0;
+  return VD_OK;
 }

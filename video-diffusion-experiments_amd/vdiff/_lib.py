@@ -34,6 +34,7 @@ SIGNATURES = {
     "vd_gn_partial_g": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp], c_i32),
     "vd_gn_apply_g": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64, c_i64, c_vp], c_i32),
     "vd_layernorm": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
+    "vd_layernorm_select": ([c_i32], c_i32),
     "vd_attention": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_i64, c_f32, c_vp], c_i32),
     "vd_temporal_attention": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
     "vd_softmax_rows": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
