@@ -293,22 +293,33 @@ __global__ __launch_bounds__(NT) void gn_apply_g_kernel(const bf16_t* x0, int64_
   const int64_t r0 = (int64_t)inst * pix_per_inst + (int64_t)blk * rows_per_blk;
   const int64_t r1 = min((int64_t)inst * pix_per_inst + pix_per_inst, r0 + rows_per_blk);
   const int64_t total = (r1 - r0) * nch;
-  for (int64_t idx = threadIdx.x; idx < total; idx += NT) {
-    const int64_t row = r0 + idx / nch;
-    const int64_t c = (idx % nch) * 8;
-    const uint4 u = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row, c);
-    float f[8];
-    unpack8(u, f);
+  constexpr int U = 4;  // 16-byte loads in flight per thread before the first store
+  for (int64_t base = threadIdx.x; base < total; base += U * NT) {
+    uint4 u[U];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float2 t = ab[c + q];
-      f[q] = fmaf(f[q], t.x, t.y);
+    for (int k = 0; k < U; ++k) {
+      const int64_t idx = base + k * NT;
+      if (idx < total) u[k] = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, r0 + idx / nch, (idx % nch) * 8);
     }
-    if (silu) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = silu_f(f[e]);
+    for (int k = 0; k < U; ++k) {
+      const int64_t idx = base + k * NT;
+      if (idx >= total) break;
+      const int64_t row = r0 + idx / nch;
+      const int64_t c = (idx % nch) * 8;
+      float f[8];
+      unpack8(u[k], f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float2 t = ab[c + q];
+        f[q] = fmaf(f[q], t.x, t.y);
+      }
+      if (silu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = silu_f(f[e]);
+      }
+      *(uint4*)(y + row * ldy + c) = pack8(f);
     }
-    *(uint4*)(y + row * ldy + c) = pack8(f);
   }
 }
 
