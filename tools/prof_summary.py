@@ -46,5 +46,5 @@ if len(after) > 3:
     timed = after[3:]
     d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed]
     print(f"roofline kernel (bench time_attention): {len(d)} timed launches of "
-          f"{timed[0]['Kernel_Name'].split('(')[0].replace('void ', '')[:60]} "
+          f"{timed[0]['Kernel_Name'].replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0][:60]} "
           f"grid={timed[0]['Grid_Size_X']}, avg {sum(d) / len(d) / 1e3:.1f} us")
