@@ -1,9 +1,9 @@
-"""Two ranks of the frame-sharded denoise loop on ONE MI355X, with real cross-rank data.
+"""Several ranks (2, 4, 8) of the frame-sharded denoise loop on ONE MI355X, with real cross-rank data.
 
 tests/test_gpu_dist.py runs the RCCL path at world size 1 (every collective an identity);
 tests/test_dist.py checks the 2-rank decomposition on CPU with oracle primitives.  This
-test closes the gap between them: two processes share cuda:0, each holds 2 of the 4 frames
-of both CFG halves and runs the product path (HIP kernels, GroupNorm partials merged across
+test closes the gap between them: 2/4/8 processes share cuda:0, each holds 8/world of the 8 frames
+of both CFG halves (one frame per rank at world 8, the driver's 8-GPU layout) and runs the product path (HIP kernels, GroupNorm partials merged across
 ranks, vd_block_transpose re-shards around every motion module) with the collectives staged
 through gloo on the host (RCCL refuses two ranks on one device); the gathered latents must
 match the unsharded single-process loop.  Tolerance: rel-L2 1e-2 over 2 DDIM steps (the
@@ -29,9 +29,12 @@ def _port():
     return p
 
 
+FRAMES = 8
+
+
 def _inputs():
     g = torch.Generator().manual_seed(0)
-    lat = torch.randn(1, 4, 4, 64, 64, generator=g)
+    lat = torch.randn(1, 4, FRAMES, 64, 64, generator=g)
     ehs = torch.randn(2, 77, 64, generator=g)
     return lat, ehs
 
@@ -72,7 +75,7 @@ def _worker(rank, world, port, out_path):
         fs = HostStagedShard()
         unet.dist = fs
         lat, ehs = _inputs()
-        fl = 4 // world
+        fl = FRAMES // world
         local = lat[:, :, rank * fl:(rank + 1) * fl].cuda()
         loop = DenoiseLoop(unet, _sched(), local, ehs.cuda(), 7.5, use_graph=False).prime()
         out = fs.all_gather_frames(loop.run(2))
@@ -82,13 +85,19 @@ def _worker(rank, world, port, out_path):
         dist.destroy_process_group()
 
 
-def test_two_ranks_on_one_gpu_match_unsharded(cuda):
+@pytest.fixture(scope="module")
+def unsharded_ref(cuda):
     from vdiff import DenoiseLoop
     lat, ehs = _inputs()
-    ref = DenoiseLoop(_model(), _sched(), lat.cuda(), ehs.cuda(), 7.5, use_graph=False).prime().run(2).cpu()
+    return DenoiseLoop(_model(), _sched(), lat.cuda(), ehs.cuda(), 7.5, use_graph=False).prime().run(2).cpu()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ranks_on_one_gpu_match_unsharded(unsharded_ref, world):
+    ref = unsharded_ref
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "out.pt")
-        mp.start_processes(_worker, args=(2, _port(), path), nprocs=2, join=True, start_method="spawn")
+        mp.start_processes(_worker, args=(world, _port(), path), nprocs=world, join=True, start_method="spawn")
         got = torch.load(path, weights_only=True)
     assert got.shape == ref.shape
     err = ((got.double() - ref.double()).norm() / ref.double().norm()).item()
