@@ -141,17 +141,16 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--attn-reps", type=int, default=20)
     ap.add_argument("--no-nocfg", action="store_true", help="skip the B=1 (no-CFG) variant")
+    ap.add_argument("--layout", default="auto", choices=["auto", "frame", "cfg-frame"],
+                    help="N>1 placement (vdiff.dist.layout): auto = cfg-frame at 2 GPUs, frame otherwise")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    fs = None
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        from vdiff.dist import FrameShard
-        fs = FrameShard()
 
     import vdiff
     from vdiff import DDIMScheduler, DenoiseLoop
@@ -160,21 +159,25 @@ def main():
     cfg_name = args.config
     frames = args.frames or (16 if cfg_name == "full" else 4)
     t0 = time.time()
+    from vdiff.dist import NodeLayout
+    lay = NodeLayout(args.layout, frames, cfg=True, world=world, rank=rank)
     unet = materialize_synthetic(cfg_name, device="cuda", seed=0)
-    unet.dist = fs
+    unet.dist = lay.frame_shard
     unet.prepare()
-    log(f"[bench] model ready in {time.time() - t0:.1f}s; world={world}")
+    log(f"[bench] model ready in {time.time() - t0:.1f}s; world={world} layout={lay.describe()}")
     cfg = unet.config
-    fl = frames // world
+    fl = lay.frames_local
     g = torch.Generator().manual_seed(42)
-    lat = torch.randn((1, 4, frames, 64, 64), generator=g)[:, :, rank * fl:(rank + 1) * fl].cuda()
+    lat_all = torch.randn((1, 4, frames, 64, 64), generator=g)
+    lat = lat_all[:, :, lay.frame_slice()].cuda()
     ehs = torch.randn((2, 77, cfg["cross_attention_dim"]), generator=torch.Generator().manual_seed(1))
     sched = DDIMScheduler.from_config(DDIMScheduler().config, beta_schedule="linear", steps_offset=1,
                                       clip_sample=False)
     sched.set_timesteps(50)
     total = args.warmup + args.steps
     ts = sched.timesteps.repeat((total + 49) // 50)[:max(total, 50)]
-    loop = DenoiseLoop(unet, sched, lat, ehs.cuda(), 7.5, timesteps=ts, use_graph=not args.no_graph)
+    loop = DenoiseLoop(unet, sched, lat, ehs.cuda(), 7.5, timesteps=ts, use_graph=not args.no_graph,
+                       cfg_shard=lay.cfg_shard)
     loop.prime()
     log(f"[bench] primed: graph={'yes' if loop.graph is not None else 'no'} {loop.graph_error or ''}")
     loop.run(args.warmup)
@@ -194,13 +197,19 @@ def main():
         elapsed = tt.item()
     assert torch.isfinite(loop.lat).all(), "non-finite latents"
     sps = args.steps / elapsed
+    graph_ok = loop.graph is not None
     ms = 1e3 * elapsed / args.steps
 
     # the B=1 (no-CFG, guidance 1) variant, labelled — same graph-captured
     # loop on the conditional half only
     nocfg = None
     if not args.no_nocfg:
-        loop1 = DenoiseLoop(unet, sched, lat, ehs[1:].cuda(), 1.0, timesteps=ts, use_graph=not args.no_graph)
+        # no CFG pair to split: frame-shard over all ranks
+        del loop
+        lay1 = lay if lay.layout == "frame" else NodeLayout("frame", frames, cfg=False, world=world, rank=rank)
+        unet.dist = lay1.frame_shard
+        lat1 = lat_all[:, :, lay1.frame_slice()].cuda()
+        loop1 = DenoiseLoop(unet, sched, lat1, ehs[1:].cuda(), 1.0, timesteps=ts, use_graph=not args.no_graph)
         loop1.prime()
         loop1.run(args.warmup)
         torch.cuda.synchronize()
@@ -220,8 +229,9 @@ def main():
                  "config": "guidance_scale 1 (no CFG): UNet batch 1 per step, same frames/latents"}
         del loop1
 
-    roof = time_attention(2 * fl, args.attn_reps, torch.cuda.current_stream())
-    roof["traffic"], roof["traffic_source"] = pmc_traffic(2 * fl)
+    imgs = (2 // lay.cfg_ranks) * fl  # images per rank in the CFG run
+    roof = time_attention(imgs, args.attn_reps, torch.cuda.current_stream())
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(imgs)
     roof["mfma_busy"], roof["mfma_busy_source"] = pmc_mfma_busy()
     step_tf = STEP_TFLOP[cfg_name] * (frames / (16 if cfg_name == "full" else 4)) / (ms * 1e-3) / world
     cpu = None
@@ -250,8 +260,8 @@ def main():
                 if cfg_name == "full" else "BASELINE config 2: tiny UNetMotionModel, 4 frames x 64x64",
                 "model": f"UNetMotionModel[{cfg_name}]",
                 "frames": frames, "latent_hw": 64, "global_batch": 2, "seq_len": 4096,
-                "parallelism": f"frame-shard x{world}" if world > 1 else "single-GPU",
-                "hipgraph": loop.graph is not None,
+                "parallelism": lay.describe(),
+                "hipgraph": graph_ok,
             },
             "roofline": roof,
             "step_mfma": {"algorithmic_tflop_per_step_per_gpu": round(STEP_TFLOP[cfg_name] * frames /

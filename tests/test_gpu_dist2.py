@@ -1,5 +1,6 @@
 """Several ranks (2, 4, 8) of the frame-sharded denoise loop on ONE MI355X, with real cross-rank data.
 
+The cfg-frame cases split the CFG halves over two rank groups (vdiff.dist.layout).
 tests/test_gpu_dist.py runs the RCCL path at world size 1 (every collective an identity);
 tests/test_dist.py checks the 2-rank decomposition on CPU with oracle primitives.  This
 test closes the gap between them: 2/4/8 processes share cuda:0, each holds 8/world of the 8 frames
@@ -51,12 +52,12 @@ def _sched():
     return s
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, layout="frame"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from vdiff import DenoiseLoop
-    from vdiff.dist import FrameShard
+    from vdiff.dist import CfgShard, FrameShard, NodeLayout
 
     class HostStagedShard(FrameShard):
         """The product FrameShard with its two data collectives staged through host memory."""
@@ -70,17 +71,27 @@ def _worker(rank, world, port, out_path):
         def all_gather_frames(self, x):
             return super().all_gather_frames(x.cpu())
 
+    class HostStagedCfg(CfgShard):
+        def gather_eps(self, eps):
+            return super().gather_eps(eps.cpu()).to(eps.device)
+
     try:
         unet = _model()
-        fs = HostStagedShard()
+        lay = NodeLayout(layout, FRAMES, world=world, rank=rank)
+        fs = HostStagedShard(lay.frame_shard.group) if lay.frame_shard is not None else None
+        cs = HostStagedCfg(lay.cfg_shard.group) if lay.cfg_shard is not None else None
         unet.dist = fs
         lat, ehs = _inputs()
-        fl = FRAMES // world
-        local = lat[:, :, rank * fl:(rank + 1) * fl].cuda()
-        loop = DenoiseLoop(unet, _sched(), local, ehs.cuda(), 7.5, use_graph=False).prime()
-        out = fs.all_gather_frames(loop.run(2))
+        local = lat[:, :, lay.frame_slice()].cuda()
+        loop = DenoiseLoop(unet, _sched(), local, ehs.cuda(), 7.5, use_graph=False, cfg_shard=cs).prime()
+        mine = loop.run(2).cpu()
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
         if rank == 0:
-            torch.save(out.cpu(), out_path)
+            # ranks of the cond half hold bitwise copies of the uncond half's latents
+            for r in range(lay.frame_ranks, world):
+                assert torch.equal(parts[r], parts[r - lay.frame_ranks]), f"rank {r} diverged from its CFG pair"
+            torch.save(torch.cat(parts[:lay.frame_ranks], dim=2), out_path)
     finally:
         dist.destroy_process_group()
 
@@ -92,12 +103,16 @@ def unsharded_ref(cuda):
     return DenoiseLoop(_model(), _sched(), lat.cuda(), ehs.cuda(), 7.5, use_graph=False).prime().run(2).cpu()
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_ranks_on_one_gpu_match_unsharded(unsharded_ref, world):
+@pytest.mark.parametrize("world,layout", [(2, "frame"), (4, "frame"), (8, "frame"),
+                                          (2, "cfg-frame"), (4, "cfg-frame"), (8, "cfg-frame")])
+def test_ranks_on_one_gpu_match_unsharded(unsharded_ref, world, layout):
+    """layout "cfg-frame" (SURVEY §8e (ii)): the two CFG halves on two rank groups, eps
+    swapped between CFG pairs before the update; at world 2 no motion-module collective."""
     ref = unsharded_ref
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "out.pt")
-        mp.start_processes(_worker, args=(world, _port(), path), nprocs=world, join=True, start_method="spawn")
+        mp.start_processes(_worker, args=(world, _port(), path, layout), nprocs=world, join=True,
+                           start_method="spawn")
         got = torch.load(path, weights_only=True)
     assert got.shape == ref.shape
     err = ((got.double() - ref.double()).norm() / ref.double().norm()).item()

@@ -1,1 +1,2 @@
 from .frame_shard import FrameShard, block_transpose_reference  # noqa: F401
+from .layout import CfgShard, NodeLayout  # noqa: F401

@@ -58,7 +58,11 @@ class DenoiseLoop:
 
     def __init__(self, unet: UNetMotionModel, scheduler, latents: torch.Tensor,
                  prompt_embeds: torch.Tensor, guidance_scale: float, timesteps=None,
-                 use_graph: bool = True):
+                 use_graph: bool = True, cfg_shard=None):
+        """cfg_shard (vdiff.dist.CfgShard, CFG only): this rank runs the UNet on ONE half
+        (cfg_shard.index: 0 uncond, 1 cond) and swaps eps rows with its pair before the
+        fused CFG+scheduler update, which both ranks apply to their replicated latents
+        (SURVEY.md §8e (ii)).  prompt_embeds still holds both halves, uncond first."""
         if not unet._prepared:
             unet.prepare()
         dev = unet.device
@@ -68,6 +72,7 @@ class DenoiseLoop:
         self.lat = latents.to(dev, torch.float32).contiguous().clone()
         self.B, _, self.F, self.H, self.W = self.lat.shape
         self.Bt = self.ncfg * self.B
+        self.cfg_shard = cfg_shard if self.ncfg == 2 else None
         ts = scheduler.timesteps if timesteps is None else timesteps
         self.n_steps = len(ts)
         self.ts = torch.as_tensor(ts).to(dev, torch.float32)
@@ -84,8 +89,17 @@ class DenoiseLoop:
         if pe.shape[0] != self.Bt:
             raise ValueError(f"prompt_embeds batch {pe.shape[0]} != {self.Bt} (uncond first when CFG)")
         self.L = pe.shape[1]
-        self.ehs_rows = pe.reshape(self.Bt * self.L, -1)
-        self.x_in = ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD, in_div=self.in_div0)
+        # the UNet batch: both CFG halves, or this rank's half under cfg_shard
+        self.Bu = self.Bt
+        if self.cfg_shard is not None:
+            h = self.cfg_shard.index
+            pe = pe[h * self.B:(h + 1) * self.B].contiguous()
+            self.Bu = self.B
+        self.ehs_rows = pe.reshape(self.Bu * self.L, -1)
+        # the CFG step kernel writes the next input for both halves; under cfg_shard the
+        # UNet reads only the first copy (the latents are replicated over the pair)
+        self.x_in2 = ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD, in_div=self.in_div0)
+        self.x_in = self.x_in2[:self.Bu * self.F * self.H * self.W]
         self.kv_cache = {}
         self.use_graph = use_graph
         self.graph = None
@@ -93,17 +107,19 @@ class DenoiseLoop:
 
     def step(self):
         u = self.unet
-        te = ops.timestep_embed(self.ts, u.time_proj.num_channels, step_idx=self.step_idx, batch=self.Bt)
-        ctx = u.make_ctx(te, self.ehs_rows, self.Bt, self.F, self.L, kv_cache=self.kv_cache)
+        te = ops.timestep_embed(self.ts, u.time_proj.num_channels, step_idx=self.step_idx, batch=self.Bu)
+        ctx = u.make_ctx(te, self.ehs_rows, self.Bu, self.F, self.L, kv_cache=self.kv_cache)
         eps = u.forward_rows(self.x_in, self.H, self.W, ctx)
+        if self.cfg_shard is not None:
+            eps = self.cfg_shard.gather_eps(eps)
         self.sched_step(eps, self.ncfg, self.g, self.lat, self.coef, step_idx=self.step_idx,
-                        next_in=self.x_in)
+                        next_in=self.x_in2)
         ops.step_advance(self.step_idx)
 
     def reset(self, latents):
         self.lat.copy_(latents)
         self.step_idx.zero_()
-        ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD, out=self.x_in, in_div=self.in_div0)
+        ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD, out=self.x_in2, in_div=self.in_div0)
 
     def prime(self):
         """One eager step (loads kernels, fills the cross-attention K/V cache,
