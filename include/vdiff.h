@@ -63,7 +63,8 @@ int vd_version(void);
  *   gate); out has N/2 columns: h * gelu_erf(g)  (diffusers GEGLU, a10).
  */
 enum { VD_A_DENSE = 0, VD_A_CONV3X3 = 1 };
-enum { VD_ACT_NONE = 0, VD_ACT_SILU = 1, VD_ACT_GEGLU = 2 };
+enum { VD_ACT_NONE = 0, VD_ACT_SILU = 1, VD_ACT_GEGLU = 2, VD_ACT_GELU = 3 };
+/* VD_ACT_GELU: pointwise gelu (erf form) — the DiT MLP (build-defined, §8f rank 3). */
 
 typedef struct vd_gemm_desc {
   const void* a0; int64_t lda0; int64_t k0;
@@ -230,6 +231,29 @@ int vd_step_advance(int32_t* step_idx, vd_stream_t stream);
  * elements (a transpose of the [nb][na] grid of row blocks, nc rows each). */
 int vd_block_transpose(const void* src, void* dst, int64_t nb, int64_t na, int64_t nc,
                        int64_t width, vd_stream_t stream);
+
+/* ---- DiT-style denoiser (BASELINE config 5; build-defined model,
+ * no reference counterpart — oracle/dit_ref.py is its restatement) ----
+ * vd_patchify: latents fp32 (B,C,F,H,W) / in_div -> token rows bf16 [(b,f,hp,wp)][kpad],
+ *   k = (c*p + ph)*p + pw (Conv3d (1,p,p) patch-embed flattening), zero-padded; dup = 2
+ *   writes the CFG copy after the first B*F*(H/p)*(W/p) rows.
+ * vd_unpatchify: token rows fp32 [(n,hp,wp)][(ph,pw,c)] -> NHWC pixel rows fp32 [(n,h,w)][c].
+ * vd_rope_qk: rotary embedding (rotate-half pairs) in place on columns [0, ncols) of token
+ *   rows, head width d; mode 0 = spatial 2-D (first d/2 dims by row h, last d/2 by column
+ *   w), mode 1 = temporal 1-D (frame f); token r = ((b*F + f)*Hp + h)*Wp + w.
+ * vd_res_ln_mod: per row (b = row / rows_per_b): xn = x + gate[b]*y (y, gate optional),
+ *   x_out = xn (optional, may alias x), h = LN(xn, eps; no affine)*(1 + scale[b]) + shift[b]
+ *   (shift/scale optional); C <= 2048, C % 8 == 0; gate/shift/scale fp32 rows of ld_mod. */
+int vd_patchify(const float* lat, int64_t B, int64_t C, int64_t F, int64_t H, int64_t W,
+                int32_t p, int32_t dup, float in_div, void* out, int64_t kpad, vd_stream_t stream);
+int vd_unpatchify(const float* src, int64_t ld_src, int64_t n_img, int64_t H, int64_t W,
+                  int32_t p, int32_t C, float* dst, vd_stream_t stream);
+int vd_rope_qk(void* x, int64_t ld, int64_t rows, int32_t ncols, int32_t d, int32_t mode,
+               int64_t F, int64_t Hp, int64_t Wp, float theta, vd_stream_t stream);
+int vd_res_ln_mod(const void* x, int64_t ldx, const void* y, int64_t ldy, const float* gate,
+                  const float* shift, const float* scale, int64_t ld_mod, int64_t rows_per_b,
+                  void* x_out, int64_t ldxo, void* h, int64_t ldh, int64_t rows, int64_t C,
+                  float eps, vd_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -63,6 +63,8 @@ __device__ __forceinline__ float erf_fast(float x) {
 }
 // diffusers GEGLU/FeedForward gelu(approximate="none"): 0.5 x (1 + erf(x / sqrt 2))
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+// pointwise GEMM epilogue activation: VD_ACT_SILU or VD_ACT_GELU (erf form)
+__device__ __forceinline__ float act_pw(int act, float x) { return act == VD_ACT_GELU ? gelu_erf(x) : silu_f(x); }
 
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

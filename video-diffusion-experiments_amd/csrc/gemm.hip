@@ -153,9 +153,9 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
           o[0] += t0.x; o[1] += t0.y; o[2] += t0.z; o[3] += t0.w;
           o[4] += t1.x; o[5] += t1.y; o[6] += t1.z; o[7] += t1.w;
         }
-        if (d.act == VD_ACT_SILU) {
+        if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = silu_f(o[j]);
+          for (int j = 0; j < 8; ++j) o[j] = act_pw(d.act, o[j]);
         }
         if (d.res) {
           float rf[8];
@@ -189,9 +189,9 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
         const float4 t = *(const float4*)(d.rowbias + (int64_t)(mrow_ / (int)d.rb_div) * d.ld_rb + n);
         o[0] += t.x; o[1] += t.y; o[2] += t.z; o[3] += t.w;
       }
-      if (d.act == VD_ACT_SILU) {
+      if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = silu_f(o[j]);
+        for (int j = 0; j < 4; ++j) o[j] = act_pw(d.act, o[j]);
       }
       if (d.res) {
         const uint2 r = *(const uint2*)((const bf16_t*)d.res + (uint32_t)(mrow_ * (int)d.ld_res + n));
@@ -945,9 +945,9 @@ __device__ __forceinline__ int epi_fast(const vd_gemm_desc& d, f32x4 (&acc)[NB][
         o[j] = __uint_as_float(r[0]) + bv[j];
         o[4 + j] = __uint_as_float(r[1]) + bv[4 + j];
       }
-      if (d.act == VD_ACT_SILU) {
+      if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = silu_f(o[j]);
+        for (int j = 0; j < 8; ++j) o[j] = act_pw(d.act, o[j]);
       }
       const uint4 pk = pack8(o);
       const bool ok = m < M && n < N;
@@ -1449,8 +1449,8 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
       const float4 a4 = *(const float4*)(d.rowbias + (m / d.rb_div) * d.ld_rb + o);
       v[0] += a4.x; v[1] += a4.y; v[2] += a4.z; v[3] += a4.w;
     }
-    if (d.act == VD_ACT_SILU)
-      for (int j = 0; j < 4; ++j) v[j] = silu_f(v[j]);
+    if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU)
+      for (int j = 0; j < 4; ++j) v[j] = act_pw(d.act, v[j]);
     if (d.res) {
       const uint2 r2 = *(const uint2*)((const bf16_t*)d.res + m * d.ld_res + o);
       v[0] += bf_lo(r2.x); v[1] += bf_hi(r2.x); v[2] += bf_lo(r2.y); v[3] += bf_hi(r2.y);
@@ -1503,8 +1503,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
         const float4 a = *(const float4*)(d.rowbias + (m / d.rb_div) * d.ld_rb + o);
         v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
       }
-      if (d.act == VD_ACT_SILU)
-        for (int j = 0; j < 4; ++j) v[j] = silu_f(v[j]);
+      if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU)
+        for (int j = 0; j < 4; ++j) v[j] = act_pw(d.act, v[j]);
       if (d.res) {
         const uint2 r = *(const uint2*)((const bf16_t*)d.res + m * d.ld_res + o);
         v[0] += bf_lo(r.x); v[1] += bf_hi(r.x); v[2] += bf_lo(r.y); v[3] += bf_hi(r.y);
@@ -1750,7 +1750,7 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   if (d.bias) VD_CHECK_ARG(al16(d.bias));
   if (d.rowbias) VD_CHECK_ARG(al16(d.rowbias) && d.ld_rb % 4 == 0 && d.rb_div > 0);
   if (d.res) VD_CHECK_ARG(al8(d.res) && d.ld_res % 4 == 0);
-  VD_CHECK_ARG(d.act == VD_ACT_NONE || d.act == VD_ACT_SILU || d.act == VD_ACT_GEGLU);
+  VD_CHECK_ARG(d.act == VD_ACT_NONE || d.act == VD_ACT_SILU || d.act == VD_ACT_GEGLU || d.act == VD_ACT_GELU);
   if (d.a_mode == VD_A_CONV3X3) {
     VD_CHECK_ARG(d.K % 9 == 0);
     const int64_t cin = d.K / 9;

@@ -46,6 +46,10 @@ SIGNATURES = {
     "vd_euler_cfg_step": ([c_vp, c_i64, c_i32, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
     "vd_step_advance": ([c_vp, c_vp], c_i32),
     "vd_block_transpose": ([c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp], c_i32),
+    "vd_patchify": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_i64, c_vp], c_i32),
+    "vd_unpatchify": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp], c_i32),
+    "vd_rope_qk": ([c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_vp], c_i32),
+    "vd_res_ln_mod": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_f32, c_vp], c_i32),
 }
 
 

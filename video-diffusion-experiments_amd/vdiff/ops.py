@@ -13,7 +13,7 @@ import torch
 
 from ._lib import GemmDesc, check, lib
 
-ACT_NONE, ACT_SILU, ACT_GEGLU = 0, 1, 2
+ACT_NONE, ACT_SILU, ACT_GEGLU, ACT_GELU = 0, 1, 2, 3
 A_DENSE, A_CONV3X3 = 0, 1
 BF16 = torch.bfloat16
 
@@ -300,4 +300,58 @@ def block_transpose(src, nb, na, nc, out=None):
     if out is None:
         out = torch.empty_like(src)
     check(lib().vd_block_transpose(_p(src), _p(out), nb, na, nc, width, _stream()), "vd_block_transpose")
+    return out
+
+
+# ---------------------------------------------------------------- DiT (§8f rank 3)
+def patchify(lat, p, kpad, dup=1, in_div=1.0, out=None):
+    """latents fp32 (B,C,F,H,W) -> bf16 token rows [(b,f,hp,wp)][kpad] (x dup for CFG)."""
+    _dev(lat, out)
+    if lat.dtype != torch.float32 or not lat.is_contiguous():
+        raise ValueError("patchify expects contiguous fp32 latents")
+    B, Cc, F, H, W = lat.shape
+    rows = B * F * (H // p) * (W // p)
+    if out is None:
+        out = torch.empty(dup * rows, kpad, device=lat.device, dtype=BF16)
+    check(lib().vd_patchify(_p(lat), B, Cc, F, H, W, p, dup, in_div, _p(out), kpad, _stream()), "vd_patchify")
+    return out
+
+
+def unpatchify(src, n_img, H, W, p, Cc, out=None):
+    """fp32 token rows [(n,hp,wp)][(ph,pw,c)] -> fp32 NHWC pixel rows [(n,h,w)][c]."""
+    _dev(src, out)
+    if src.dtype != torch.float32:
+        raise ValueError("unpatchify expects fp32 rows")
+    if out is None:
+        out = torch.empty(n_img * H * W, Cc, device=src.device, dtype=torch.float32)
+    check(lib().vd_unpatchify(_p(src), _rows(src, torch.float32), n_img, H, W, p, Cc, _p(out), _stream()),
+          "vd_unpatchify")
+    return out
+
+
+def rope_qk(x, ncols, d, mode, F, Hp, Wp, theta=10000.0):
+    """In-place rotary embedding on columns [0, ncols) of bf16 token rows x."""
+    _dev(x)
+    check(lib().vd_rope_qk(_p(x), _rows(x), x.shape[0], ncols, d, mode, F, Hp, Wp, theta, _stream()),
+          "vd_rope_qk")
+    return x
+
+
+def res_ln_mod(x, *, y=None, gate=None, shift=None, scale=None, rows_per_b=None, x_out=None,
+               eps=1e-6, out=None):
+    """h = LN(x + gate*y) * (1 + scale) + shift per row group b = row // rows_per_b;
+    x_out (may be x) receives x + gate*y.  gate/shift/scale: fp32 [B, >= C] row views."""
+    _dev(x, y, gate, shift, scale, x_out, out)
+    rows, Cc = x.shape
+    mods = [t for t in (gate, shift, scale) if t is not None]
+    ld_mod = mods[0].stride(0) if mods else 0
+    for t in mods:
+        if t.dtype != torch.float32 or t.stride(1) != 1 or t.stride(0) != ld_mod:
+            raise ValueError("gate/shift/scale must be fp32 row views sharing one row stride")
+    if out is None:
+        out = torch.empty(rows, Cc, device=x.device, dtype=BF16)
+    check(lib().vd_res_ln_mod(_p(x), _rows(x), _p(y), _rows(y) if y is not None else 0, _p(gate), _p(shift),
+                              _p(scale), ld_mod, rows_per_b or rows, _p(x_out),
+                              _rows(x_out) if x_out is not None else 0, _p(out), _rows(out), rows, Cc, eps,
+                              _stream()), "vd_res_ln_mod")
     return out
