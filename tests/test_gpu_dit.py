@@ -115,10 +115,13 @@ def test_gemm_gelu_epilogue(cuda):
         torch.testing.assert_close(out, want, rtol=2 ** -6, atol=2e-2)
 
 
-def test_temporal_attention_32_frames_d64(cuda):
-    """The full DiT config attends over 32 frames with d = 64 (the VALU temporal kernel)."""
-    g = torch.Generator().manual_seed(5)
-    B, F, P, heads, d = 2, 32, 12, 3, 64
+@pytest.mark.parametrize("F", [4, 16, 17, 27, 32])
+@pytest.mark.parametrize("d", [40, 64, 80, 160])
+def test_temporal_attention_mfma_up_to_32_frames(cuda, F, d):
+    """The full DiT config attends over 32 frames with d = 64: temporal_mfma32_kernel for
+    17..32 frames, temporal_mfma_kernel (now also d = 64) up to 16, ragged frame counts."""
+    g = torch.Generator().manual_seed(5 + F + d)
+    B, P, heads = 2, 12, 3
     D = heads * d
     qkv = torch.randn(B * F * P, 3 * D, generator=g).to(torch.bfloat16)
     c = qkv.cuda()

@@ -950,6 +950,118 @@ __global__ __launch_bounds__(NT) void temporal_mfma_kernel(
   }
 }
 
+// 17..32 frames (the DiT's 32-frame temporal blocks): the 16-frame kernel's scheme on two
+// key blocks and two query blocks.  Per query block, S^T blocks (keys 16kb + 4fq + j,
+// query 16qb + fr) give each lane 8 keys of its query; P^T's k-slot (fq, j) is key
+// 4fq + j for j < 4 and 16 + 4fq + (j - 4) for j >= 4, and V^T's fragment takes the
+// same keys from two tr reads 16 LDS rows apart, so one 16x16x32 MFMA per d-block sums
+// all 32 keys.  The V^T fragments are read once per item and reused by both query blocks.
+template <int D>
+__global__ __launch_bounds__(NT) void temporal_mfma32_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
+    bf16_t* __restrict__ o, int64_t ldo, int64_t batch, int frames, int64_t positions, int heads,
+    float c) {
+  using C = TmCfg<D>;
+  __shared__ __attribute__((aligned(16))) bf16_t vimg[4][32 * C::VS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16_t* vl = vimg[wave];
+  for (int idx = lane; idx < 32 * C::VS / 8; idx += 64) *(uint4*)(vl + idx * 8) = make_uint4(0, 0, 0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane < 32) vl[lane * C::VS + D] = (bf16_t)0x3F80;
+  const int64_t nitems = batch * positions * heads;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  const bool unitc = c == 1.0f;
+  const int vtr = (4 * fq + (fr >> 2)) * C::VS + 4 * (fr & 3);
+  const int64_t lblk = xcd_remap(blockIdx.x, gridDim.x);
+  for (int64_t item = lblk * 4 + wave; item < nitems; item += stride) {
+    const int h = (int)(item % heads);
+    const int64_t bp = item / heads;
+    const int64_t p = bp % positions, b = bp / positions;
+    const int64_t row0 = b * frames * positions + p;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous item's tr reads done
+    for (int idx = lane; idx < frames * C::DCH; idx += 64) {
+      const int f = idx / C::DCH, cc = idx - f * C::DCH;
+      *(uint4*)(vl + f * C::VS + cc * 8) =
+          *(const uint4*)(v + (row0 + (int64_t)f * positions) * ld + (int64_t)h * D + cc * 8);
+    }
+    // ---- S^T blocks: [qb][kb]
+    f32x4 s[2][2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) s[qb][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < C::KSTEPS; ++ks) {
+      const int dd = ks * 32 + 8 * fq;
+      uint4 kq[2], qq[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int f = 16 * t + fr;
+        kq[t] = qq[t] = make_uint4(0, 0, 0, 0);
+        if (dd < D && f < frames) {
+          const int64_t rf = (row0 + (int64_t)f * positions) * ld + (int64_t)h * D + dd;
+          kq[t] = *(const uint4*)(k + rf);
+          qq[t] = *(const uint4*)(q + rf);
+        }
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          s[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kq[kb]),
+                                                              __builtin_bit_cast(bf16x8, qq[qb]), s[qb][kb], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // V image written
+    __builtin_amdgcn_wave_barrier();
+    bf16x8 vf[C::DB];
+#pragma unroll
+    for (int a = 0; a < C::DB; ++a) {
+      const bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (bf16x4 __attribute__((address_space(3)))*)(vl + vtr + 16 * a));
+      const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (bf16x4 __attribute__((address_space(3)))*)(vl + 16 * C::VS + vtr + 16 * a));
+      vf[a] = bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+    }
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (16 * kb + 4 * fq + j >= frames) s[qb][kb][j] = -INFINITY;
+          else if (!unitc) s[qb][kb][j] *= c;
+          mx = fmaxf(mx, s[qb][kb][j]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pf[j] = (__bf16)__builtin_amdgcn_exp2f(s[qb][0][j] - mx);
+        pf[4 + j] = (__bf16)__builtin_amdgcn_exp2f(s[qb][1][j] - mx);
+      }
+      f32x4 ot[C::DB];
+#pragma unroll
+      for (int a = 0; a < C::DB; ++a)
+        ot[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[a], pf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const float l = __shfl(ot[D / 16][(D % 16) % 4], ((D % 16) / 4) * 16 + fr, 64);
+      const float inv = __builtin_amdgcn_rcpf(l);
+      const int f = 16 * qb + fr;
+      if (f < frames) {
+        bf16_t* orow = o + (row0 + (int64_t)f * positions) * ldo + (int64_t)h * D;
+#pragma unroll
+        for (int a = 0; a < C::DB; ++a) {
+          const int dd = 16 * a + 4 * fq;
+          if (dd + 4 <= D)
+            *(uint2*)(orow + dd) = make_uint2(pack2(ot[a][0] * inv, ot[a][1] * inv), pack2(ot[a][2] * inv, ot[a][3] * inv));
+        }
+      }
+    }
+  }
+}
+
 // Row softmax for the materialised-score attention of the VAE mid block (one head,
 // d = 512: S = 4096 keys per frame fits HBM easily, the flash kernels stop at d = 160).
 // Scores arrive fp32 in log2 units (the caller folded d^-1/2 * log2(e) into q):
@@ -1038,15 +1150,23 @@ extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v
   const unsigned grid = (unsigned)((items + 3) / 4);
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  if (frames <= 16 && !g_temporal_valu && (d == 40 || d == 80 || d == 160) && ld % 8 == 0 && ldo % 4 == 0) {
+  if (!g_temporal_valu && (d == 40 || d == 64 || d == 80 || d == 160) && ld % 8 == 0 && ldo % 4 == 0) {
     const int64_t g = (items + 3) / 4;
     const unsigned grid2 = (unsigned)(g < 8192 ? g : 8192);
-#define TM_LAUNCH(DD)                                                                                           \
-    hipLaunchKernelGGL(temporal_mfma_kernel<DD>, dim3(grid2), dim3(NT), 0, s, (const bf16_t*)q, (const bf16_t*)k, \
+#define TM_LAUNCH(KERN, DD)                                                                                 \
+    hipLaunchKernelGGL(KERN<DD>, dim3(grid2), dim3(NT), 0, s, (const bf16_t*)q, (const bf16_t*)k,           \
                        (const bf16_t*)v, ld, (bf16_t*)o, ldo, batch, frames, positions, heads, sl2)
-    if (d == 40) TM_LAUNCH(40);
-    else if (d == 80) TM_LAUNCH(80);
-    else TM_LAUNCH(160);
+    if (frames <= 16) {
+      if (d == 40) TM_LAUNCH(temporal_mfma_kernel, 40);
+      else if (d == 64) TM_LAUNCH(temporal_mfma_kernel, 64);
+      else if (d == 80) TM_LAUNCH(temporal_mfma_kernel, 80);
+      else TM_LAUNCH(temporal_mfma_kernel, 160);
+    } else {
+      if (d == 40) TM_LAUNCH(temporal_mfma32_kernel, 40);
+      else if (d == 64) TM_LAUNCH(temporal_mfma32_kernel, 64);
+      else if (d == 80) TM_LAUNCH(temporal_mfma32_kernel, 80);
+      else TM_LAUNCH(temporal_mfma32_kernel, 160);
+    }
 #undef TM_LAUNCH
     return vd_launch_status();
   }

@@ -1702,8 +1702,11 @@ Plan plan(const vd_gemm_desc& d) {
   // measured (tools/kbench.py): v3 wins on the wide projections (qkv, GEGLU) once the
   // grid fills the chip without split-K; v2's persistent stream wins on N <= 640 and
   // on few-tile shapes
-  const bool v3auto = v3ok && d.N >= 768 && (p256 - d.N) * 16 <= d.N &&
-                      ((d.M + G3_BM - 1) / G3_BM) * (p256 / 256) >= 256;
+  // DiT (tools/dit_kbench.py, M 147456): N 1152 = 4.5 tiles still wins on v3 at K >= 1024
+  // (426 vs 500 us at K 1152, 1431 vs 1666 us at K 4608), so the padding bound loosens to
+  // 1/8 there; no UNet shape has N >= 768 with K >= 1024 at M >= 65536
+  const bool v3pad = (p256 - d.N) * 16 <= d.N || (d.K >= 1024 && d.M >= 65536 && (p256 - d.N) * 8 <= d.N);
+  const bool v3auto = v3ok && d.N >= 768 && v3pad && ((d.M + G3_BM - 1) / G3_BM) * (p256 / 256) >= 256;
   if (g_path == 3 ? v3ok : v3auto) {
     p.ver = 3;
     p.bn = 256;
