@@ -255,6 +255,23 @@ int vd_res_ln_mod(const void* x, int64_t ldx, const void* y, int64_t ldy, const 
                   void* x_out, int64_t ldxo, void* h, int64_t ldh, int64_t rows, int64_t C,
                   float eps, vd_stream_t stream);
 
+/* fp8 spatial self-attention, d = 64 (BASELINE config 5 "fp8 MFMA QK^T/PV"; the DiT's
+ * spatial blocks): block-scaled v_mfma_scale_f32_32x32x64_f8f6f4, OCP e4m3 operands.
+ * vd_attention_fp8_quant: q/k/v bf16 rows (column slices of the fused QKV buffer) ->
+ *   q8/k8 fp8 rows [batch*s][ld8] (ld8 >= heads*64, % 16) with one E8M0 scale byte per
+ *   (row, head) in qs/ks [batch*s][heads]; vt8 = V^T fp8 [batch*heads][64][skv] with the keys
+ *   of every 64-key tile in the MFMA's k-slot order, vs = one E8M0 per (image, head, tile).
+ * vd_attention_fp8: softmax(scale * Q K^T) V from those operands -> bf16 rows o (column h*64
+ *   of head h).  sq % 32 == 0, skv % 64 == 0. */
+int vd_attention_fp8_quant(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                           int64_t ldv, int64_t batch, int32_t heads, int64_t sq, int64_t skv,
+                           int32_t d, void* q8, void* k8, int64_t ld8, void* vt8, void* qs, void* ks,
+                           void* vs, vd_stream_t stream);
+int vd_attention_fp8(const void* q8, const void* k8, int64_t ld8, const void* qs, const void* ks,
+                     const void* vt8, const void* vs, void* o, int64_t ldo, int64_t batch,
+                     int32_t heads, int64_t sq, int64_t skv, int32_t d, float scale,
+                     vd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

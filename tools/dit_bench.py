@@ -48,11 +48,12 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="spatial self-attention on the fp8 MFMA kernel")
     args = ap.parse_args()
     cfg = dict(DIT_FULL, num_frames=args.frames, sample_size=args.size)
     t0 = time.time()
     sd = init_dit_state_dict(cfg, seed=0, device="cuda")
-    model = DiT3DModel(cfg, sd, device="cuda")
+    model = DiT3DModel(cfg, sd, device="cuda", attn_fp8=args.fp8)
     del sd
     torch.cuda.empty_cache()
     F, H = args.frames, args.size
@@ -82,6 +83,26 @@ def main():
     ev[1].record()
     torch.cuda.synchronize()
     at = ev[0].elapsed_time(ev[1]) / 5
+    # the fp8 kernel on the same data: operand quantization and the attention launch apart
+    ws = ops.attention_fp8_quant(q, k, v, 2 * F, cfg["num_heads"], S, S, d)
+    from vdiff._lib import lib
+    fp8_call = lambda: lib().vd_attention_fp8(ws["q8"].data_ptr(), ws["k8"].data_ptr(), ws["ld8"], ws["qs"].data_ptr(),  # noqa: E731
+                                              ws["ks"].data_ptr(), ws["vt8"].data_ptr(), ws["vs"].data_ptr(),
+                                              o.data_ptr(), o.stride(0), 2 * F, cfg["num_heads"], S, S, d, d ** -0.5,
+                                              torch.cuda.current_stream().cuda_stream)
+    fp8_call()
+    ev[0].record()
+    for _ in range(5):
+        fp8_call()
+    ev[1].record()
+    torch.cuda.synchronize()
+    at8 = ev[0].elapsed_time(ev[1]) / 5
+    ev[0].record()
+    for _ in range(5):
+        ops.attention_fp8_quant(q, k, v, 2 * F, cfg["num_heads"], S, S, d)
+    ev[1].record()
+    torch.cuda.synchronize()
+    qt8 = ev[0].elapsed_time(ev[1]) / 5
     res = {
         "metric": "DiT denoising steps/s (BASELINE config 5 shapes, CFG batch 2, 1 GPU)",
         "value": round(1.0 / dt, 4), "unit": "denoising steps/s", "ms_per_step": round(dt * 1e3, 3),
@@ -94,6 +115,12 @@ def main():
         "spatial_attention": {"kernel": f"flash_attn_kernel<{d}> S={S} batch={2 * F} heads={cfg['num_heads']}",
                               "ms": round(at, 4), "achieved": round(sp_flop / at / 1e9, 1),
                               "unit": "TFLOP/s", "frac": round(sp_flop / at / 1e9 / PEAK, 4)},
+        "spatial_attention_fp8": {"kernel": "flash_fp8_kernel (v_mfma_scale_f32_32x32x64_f8f6f4, e4m3)",
+                                  "ms": round(at8, 4), "achieved": round(sp_flop / at8 / 1e9, 1), "unit": "TFLOP/s",
+                                  "frac_of_fp8_peak": round(sp_flop / at8 / 1e9 / (2 * PEAK), 4),
+                                  "frac_of_bf16_peak": round(sp_flop / at8 / 1e9 / PEAK, 4),
+                                  "quant_ms": round(qt8, 4)},
+        "attn_fp8_in_step": bool(args.fp8),
     }
     if args.cpu:
         from oracle import dit_ref

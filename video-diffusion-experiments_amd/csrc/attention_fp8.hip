@@ -1,0 +1,309 @@
+// fp8 (OCP e4m3) spatial self-attention for d = 64 on the block-scaled MFMA
+// v_mfma_scale_f32_32x32x64_f8f6f4 (2x the bf16 MFMA rate on gfx950): the "fp8 MFMA
+// QK^T/PV" of BASELINE config 5 (the DiT's spatial blocks).
+//
+// Operand map (lane l, r = l & 31, h = l >> 5; checked with exact integer data by
+// tools/mb/fp8_probe.py): A row r / B column r, 32 bytes per lane = k-slots (h, j),
+// j < 32; C/D as every 32x32 MFMA: column r, row (i & 3) + 8 (i >> 2) + 4 h for
+// accumulator register i.  The E8M0 scale a lane passes applies to its 32 k-slots.
+//
+//   S^T = K . Q^T   A = K rows (key r), B = Q^T (query r), k-slot (h, j) = d 32h + j:
+//                   both are plain 32-byte slices of the fp8 rows, scaled per token
+//                   (the lane's own key / query scale).
+//   O^T = V^T . P^T B = P^T: the two S^T accumulators of a 64-key tile, converted to fp8
+//                   in register order, ARE the operand: k-slot (h, j) = key
+//                   32 (j >> 4) + (j & 3) + 8 ((j & 15) >> 2) + 4 h.  A = V^T rows (d r)
+//                   must hold the same keys in the same slots: the pre-pass writes V^T
+//                   with the keys of every 64-key tile permuted that way, so a lane's
+//                   32 bytes are contiguous.  V's scale is one E8M0 per (image, head, tile).
+//
+// Pre-pass (attn_fp8_quant_*): per (token, head) power-of-two scale 2^ceil(log2(amax/448))
+// for Q and K; V per 64-key tile.  Softmax: fp32 scores * (d^-1/2 log2 e), running max per
+// query (lanes r and r+32 share a query: one permlane32 swap), P = exp2(s - m) <= 1 in
+// fp8 with unit scale, row sum in fp32 (halves summed at the end), lazy O rescale when a
+// query's max grows.  Block = 4 waves x 32 queries sharing double-buffered LDS tiles.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int FD = 64;        // head dim
+constexpr int KT8 = 64;       // keys per tile
+constexpr int KROW = 80;      // LDS bytes per K row (64 + 16 pad: conflict-light b128 reads)
+constexpr int VROW = 80;      // LDS bytes per V^T row
+constexpr int STAGE8 = KT8 * KROW + FD * VROW + KT8;  // K, V^T, K scales
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+__device__ __forceinline__ float partner32f(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
+
+__device__ __forceinline__ int e8m0_for(float amax) {
+  // smallest e with amax / 2^e <= 448 (OCP e4m3 max); zero rows get 2^0
+  if (!(amax > 0.f)) return 127;
+  int e = (int)ceilf(log2f(amax * (1.0f / 448.0f)));
+  e = e < -126 ? -126 : (e > 127 ? 127 : e);
+  return e + 127;
+}
+__device__ __forceinline__ float e8m0_inv(int b) { return exp2f((float)(127 - b)); }
+
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+  const float L = 448.f;
+  a = __builtin_amdgcn_fmed3f(a, L, -L); b = __builtin_amdgcn_fmed3f(b, L, -L);
+  c = __builtin_amdgcn_fmed3f(c, L, -L); d = __builtin_amdgcn_fmed3f(d, L, -L);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+
+// Q or K rows: one thread per (row, head): 64 bf16 -> 64 fp8 + one E8M0 byte.
+__global__ void quant_rows_kernel(const bf16_t* __restrict__ x, int64_t ldx, int64_t rows, int heads,
+                                  uint8_t* __restrict__ x8, int64_t ld8, uint8_t* __restrict__ sc) {
+  const int64_t total = rows * heads;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int64_t r = i / heads;
+    const int h = (int)(i % heads);
+    const bf16_t* src = x + r * ldx + h * FD;
+    float v[FD];
+    float amax = 0.f;
+#pragma unroll
+    for (int c = 0; c < FD / 8; ++c) {
+      unpack8(*(const uint4*)(src + 8 * c), v + 8 * c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[8 * c + j]));
+    }
+    const int e = e8m0_for(amax);
+    const float inv = e8m0_inv(e);
+    uint8_t* dst = x8 + r * ld8 + h * FD;
+#pragma unroll
+    for (int c = 0; c < FD / 16; ++c) {
+      const float* s = v + 16 * c;
+      *(uint4*)(dst + 16 * c) =
+          make_uint4(pack4_fp8(s[0] * inv, s[1] * inv, s[2] * inv, s[3] * inv),
+                     pack4_fp8(s[4] * inv, s[5] * inv, s[6] * inv, s[7] * inv),
+                     pack4_fp8(s[8] * inv, s[9] * inv, s[10] * inv, s[11] * inv),
+                     pack4_fp8(s[12] * inv, s[13] * inv, s[14] * inv, s[15] * inv));
+    }
+    sc[r * heads + h] = (uint8_t)e;
+  }
+}
+
+// slot p = 32h + j of a 64-key tile holds key 32 (j >> 4) + (j & 3) + 8 ((j & 15) >> 2) + 4h
+__device__ __forceinline__ int slot_key(int p) {
+  const int h = p >> 5, j = p & 31;
+  return 32 * (j >> 4) + (j & 3) + 8 * ((j & 15) >> 2) + 4 * h;
+}
+
+// V -> V^T fp8, keys permuted per tile; one workgroup per (image, head, 64-key tile).
+__global__ __launch_bounds__(NT) void quant_vt_kernel(const bf16_t* __restrict__ v, int64_t ldv, int heads,
+                                                     int64_t skv, uint8_t* __restrict__ vt8,
+                                                     uint8_t* __restrict__ vs) {
+  __shared__ float tile[KT8][FD + 1];
+  __shared__ float red[NT / 64];
+  const int64_t ntiles = skv / KT8;
+  const int64_t t = blockIdx.x % ntiles;
+  const int64_t bh = blockIdx.x / ntiles;
+  const int h = (int)(bh % heads);
+  const int64_t b = bh / heads;
+  const int tid = threadIdx.x;
+  // 64 keys x 64 d bf16 = 512 chunks of 8: two per thread
+  float amax = 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = tid + u * NT;
+    const int key = c >> 3, dc = (c & 7) * 8;
+    float f[8];
+    unpack8(*(const uint4*)(v + (b * skv + t * KT8 + key) * ldv + h * FD + dc), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      tile[key][dc + j] = f[j];
+      amax = fmaxf(amax, fabsf(f[j]));
+    }
+  }
+  amax = wave_max(amax);
+  if ((tid & 63) == 0) red[tid >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const int e = e8m0_for(amax);
+  const float inv = e8m0_inv(e);
+  // write V^T: row d (64 bytes per tile), 16 slots per thread
+  const int d = tid >> 2, q = (tid & 3) * 16;
+  uint32_t w[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int p = q + 4 * g;
+    w[g] = pack4_fp8(tile[slot_key(p)][d] * inv, tile[slot_key(p + 1)][d] * inv, tile[slot_key(p + 2)][d] * inv,
+                     tile[slot_key(p + 3)][d] * inv);
+  }
+  *(uint4*)(vt8 + (bh * FD + d) * skv + t * KT8 + q) = make_uint4(w[0], w[1], w[2], w[3]);
+  if (tid == 0) vs[bh * ntiles + t] = (uint8_t)e;
+}
+
+__global__ __launch_bounds__(NT, 2) void flash_fp8_kernel(
+    const uint8_t* __restrict__ q8, const uint8_t* __restrict__ k8, int64_t ld8,
+    const uint8_t* __restrict__ qs, const uint8_t* __restrict__ ks, const uint8_t* __restrict__ vt8,
+    const uint8_t* __restrict__ vs, bf16_t* __restrict__ o, int64_t ldo, int heads, int64_t sq, int64_t skv,
+    float c, int unit_scale) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = (int)((sq + 127) / 128);
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qblk = lid % nqb;
+  const int h = (lid / nqb) % heads;
+  const int64_t b = lid / (nqb * heads);
+  const int64_t bh = b * heads + h;
+  const int64_t q0 = (int64_t)qblk * 128 + wave * 32;
+  const bool qvalid = q0 < sq;
+  const int64_t qrow = b * sq + (qvalid ? q0 + r : 0);
+  // Q^T fragment: d = 32 hh + j of this lane's query, and its scale
+  const i32x8 qf = *(const i32x8*)(q8 + qrow * ld8 + h * FD + 32 * hh);
+  const int qsc = qs[qrow * heads + h];
+  const int64_t ntiles = skv / KT8;
+  const uint8_t* kbase = k8 + b * skv * ld8 + h * FD;
+  const uint8_t* vbase = vt8 + bh * FD * skv;
+  // cooperative tile load: K 64 rows x 64 B (256 x 16 B), V^T 64 rows x 64 B (256 x 16 B)
+  const int lr = tid >> 2, lc = (tid & 3) * 16;
+  uint4 kreg, vreg;
+  uint8_t sreg = 0;
+  auto gload = [&](int64_t t) {
+    kreg = *(const uint4*)(kbase + (t * KT8 + lr) * ld8 + lc);
+    vreg = *(const uint4*)(vbase + (int64_t)lr * skv + t * KT8 + lc);
+    if (tid < KT8) sreg = ks[(b * skv + t * KT8 + tid) * heads + h];
+  };
+  auto sstore = [&](int buf) {
+    uint8_t* st = lds + buf * STAGE8;
+    *(uint4*)(st + lr * KROW + lc) = kreg;
+    *(uint4*)(st + KT8 * KROW + lr * VROW + lc) = vreg;
+    if (tid < KT8) st[KT8 * KROW + FD * VROW + tid] = sreg;
+  };
+  f32x16 ot[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ot[a][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int buf = (int)(t & 1);
+    if (t + 1 < ntiles) gload(t + 1);
+    const uint8_t* st = lds + buf * STAGE8;
+    // ---- S^T for the two 32-key blocks
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const uint8_t* kr = st + (32 * kb + r) * KROW + 32 * hh;
+      const uint4 k0 = *(const uint4*)kr, k1 = *(const uint4*)(kr + 16);
+      const i32x8 kf = {(int)k0.x, (int)k0.y, (int)k0.z, (int)k0.w, (int)k1.x, (int)k1.y, (int)k1.z, (int)k1.w};
+      const int ksc = st[KT8 * KROW + FD * VROW + 32 * kb + r];
+      f32x16 z;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) z[i] = 0.f;
+      s[kb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, z, 0, 0, 0, ksc, 0, qsc);
+    }
+    // V^T fragments (d rows r and 32 + r, this lane's 32 slots)
+    i32x8 vf[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const uint8_t* vr = st + KT8 * KROW + (32 * a + r) * VROW + 32 * hh;
+      const uint4 v0 = *(const uint4*)vr, v1 = *(const uint4*)(vr + 16);
+      vf[a] = i32x8{(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+    }
+    const int vsc = vs[bh * ntiles + t];
+    // ---- online softmax over this lane's 32 scores (its query; the other half in lane ^ 32)
+    float mt = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kb][i]);
+    mt = fmaxf(mt, partner32f(mt)) * c;
+    if (mt > m) {
+      const float alpha = exp2f(m - mt);
+      l *= alpha;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ot[a][i] *= alpha;
+      m = mt;
+    }
+    uint32_t pw[8];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float p0 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 0], c, -m));
+        const float p1 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 1], c, -m));
+        const float p2 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 2], c, -m));
+        const float p3 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 3], c, -m));
+        l += (p0 + p1) + (p2 + p3);
+        pw[4 * kb + g] = pack4_fp8(p0, p1, p2, p3);
+      }
+    const i32x8 pf = {(int)pw[0], (int)pw[1], (int)pw[2], (int)pw[3], (int)pw[4], (int)pw[5], (int)pw[6], (int)pw[7]};
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+      ot[a] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf[a], pf, ot[a], 0, 0, 0, vsc, 0, unit_scale);
+    if (t + 1 < ntiles) {
+      sstore(buf ^ 1);
+    }
+    __syncthreads();
+  }
+  const float lt = l + partner32f(l);
+  const float inv = 1.0f / lt;
+  if (qvalid) {
+    bf16_t* orow = o + (b * sq + q0 + r) * ldo + h * FD;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = 32 * a + 8 * g + 4 * hh;
+        *(uint2*)(orow + dd) = make_uint2(pack2(ot[a][4 * g] * inv, ot[a][4 * g + 1] * inv),
+                                          pack2(ot[a][4 * g + 2] * inv, ot[a][4 * g + 3] * inv));
+      }
+  }
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" int vd_attention_fp8_quant(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                                      int64_t ldv, int64_t batch, int32_t heads, int64_t sq, int64_t skv,
+                                      int32_t d, void* q8, void* k8, int64_t ld8, void* vt8, void* qs,
+                                      void* ks, void* vs, vd_stream_t stream) {
+  VD_CHECK_ARG(d == FD && heads > 0 && batch > 0 && sq > 0 && skv > 0 && skv % KT8 == 0);
+  VD_CHECK_ARG(q && k && v && q8 && k8 && vt8 && qs && ks && vs && al16(q) && al16(k) && al16(v));
+  VD_CHECK_ARG(al16(q8) && al16(k8) && al16(vt8) && ld8 % 16 == 0 && ld8 >= (int64_t)heads * FD);
+  VD_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0);
+  hipStream_t s = (hipStream_t)stream;
+  auto grid = [](int64_t n) { const int64_t b = (n + NT - 1) / NT; return (unsigned)(b < 16384 ? b : 16384); };
+  hipLaunchKernelGGL(quant_rows_kernel, dim3(grid(batch * sq * heads)), dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                     batch * sq, (int)heads, (uint8_t*)q8, ld8, (uint8_t*)qs);
+  hipLaunchKernelGGL(quant_rows_kernel, dim3(grid(batch * skv * heads)), dim3(NT), 0, s, (const bf16_t*)k, ldk,
+                     batch * skv, (int)heads, (uint8_t*)k8, ld8, (uint8_t*)ks);
+  const int64_t nblk = batch * heads * (skv / KT8);
+  VD_CHECK_ARG(nblk < 0x7fffffff);
+  hipLaunchKernelGGL(quant_vt_kernel, dim3((unsigned)nblk), dim3(NT), 0, s, (const bf16_t*)v, ldv, (int)heads, skv,
+                     (uint8_t*)vt8, (uint8_t*)vs);
+  return vd_launch_status();
+}
+
+extern "C" int vd_attention_fp8(const void* q8, const void* k8, int64_t ld8, const void* qs, const void* ks,
+                                const void* vt8, const void* vs, void* o, int64_t ldo, int64_t batch,
+                                int32_t heads, int64_t sq, int64_t skv, int32_t d, float scale,
+                                vd_stream_t stream) {
+  VD_CHECK_ARG(d == FD && heads > 0 && batch > 0 && sq > 0 && sq % 32 == 0 && skv > 0 && skv % KT8 == 0);
+  VD_CHECK_ARG(q8 && k8 && qs && ks && vt8 && vs && o && al16(q8) && al16(k8) && al16(vt8));
+  VD_CHECK_ARG(ld8 % 16 == 0 && ld8 >= (int64_t)heads * FD && ldo % 4 == 0 && ((uintptr_t)o & 7) == 0);
+  const int64_t nblk = (sq + 127) / 128 * heads * batch;
+  VD_CHECK_ARG(nblk < 0x7fffffff);
+  const float c = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(flash_fp8_kernel, dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream, (const uint8_t*)q8,
+                     (const uint8_t*)k8, ld8, (const uint8_t*)qs, (const uint8_t*)ks, (const uint8_t*)vt8,
+                     (const uint8_t*)vs, (bf16_t*)o, ldo, (int)heads, sq, skv, c, 127);
+  return vd_launch_status();
+}

@@ -74,7 +74,10 @@ def init_dit_state_dict(cfg: dict, seed: int = 0, device="cpu", dtype=torch.floa
 class DiT3DModel:
     """Build-defined DiT video denoiser over HIP kernels (see module docstring)."""
 
-    def __init__(self, cfg: dict, state_dict: dict, device="cuda"):
+    def __init__(self, cfg: dict, state_dict: dict, device="cuda", attn_fp8: bool = False):
+        """attn_fp8: spatial self-attention on the block-scaled fp8 MFMA (vd_attention_fp8,
+        d = 64, frames of a multiple of 64 tokens); text cross- and temporal attention stay bf16."""
+        self.attn_fp8 = attn_fp8
         self.config = dict(cfg)
         self.device = torch.device(device)
         self.dtype = torch.bfloat16
@@ -140,7 +143,10 @@ class DiT3DModel:
             q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
             if i % 2 == 0:
                 ops.rope_qk(qkv, 2 * D, d, 0, F, Hp, Wp, theta)
-                a = ops.attention(q, k, v, B * F, heads, S, S, d)
+                if self.attn_fp8 and d == 64 and S % 64 == 0:
+                    a = ops.attention_fp8(q, k, v, B * F, heads, S, S, d)
+                else:
+                    a = ops.attention(q, k, v, B * F, heads, S, S, d)
             else:
                 ops.rope_qk(qkv, 2 * D, d, 1, F, Hp, Wp, theta)
                 a = ops.temporal_attention(q, k, v, B, F, S, heads, d)

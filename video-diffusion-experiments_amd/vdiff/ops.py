@@ -355,3 +355,35 @@ def res_ln_mod(x, *, y=None, gate=None, shift=None, scale=None, rows_per_b=None,
                               _rows(x_out) if x_out is not None else 0, _p(out), _rows(out), rows, Cc, eps,
                               _stream()), "vd_res_ln_mod")
     return out
+
+
+def attention_fp8_quant(q, k, v, batch, heads, sq, skv, d=64):
+    """bf16 q/k/v row views -> the fp8 operands of vd_attention_fp8 (a dict of buffers)."""
+    _dev(q, k, v)
+    dev = q.device
+    ld8 = (heads * d + 15) // 16 * 16
+    u8 = torch.uint8
+    ws = {"q8": torch.empty(batch * sq, ld8, device=dev, dtype=u8),
+          "k8": torch.empty(batch * skv, ld8, device=dev, dtype=u8),
+          "vt8": torch.empty(batch * heads * d, skv, device=dev, dtype=u8),
+          "qs": torch.empty(batch * sq, heads, device=dev, dtype=u8),
+          "ks": torch.empty(batch * skv, heads, device=dev, dtype=u8),
+          "vs": torch.empty(batch * heads, max(1, skv // 64), device=dev, dtype=u8),
+          "ld8": ld8, "batch": batch, "heads": heads, "sq": sq, "skv": skv, "d": d}
+    check(lib().vd_attention_fp8_quant(_p(q), q.stride(0), _p(k), k.stride(0), _p(v), v.stride(0), batch, heads,
+                                       sq, skv, d, _p(ws["q8"]), _p(ws["k8"]), ld8, _p(ws["vt8"]), _p(ws["qs"]),
+                                       _p(ws["ks"]), _p(ws["vs"]), _stream()), "vd_attention_fp8_quant")
+    return ws
+
+
+def attention_fp8(q, k, v, batch, heads, sq, skv, d=64, scale=None, out=None):
+    """fp8 (e4m3, block-scaled MFMA) self-attention, d = 64: quantize, then attend."""
+    ws = attention_fp8_quant(q, k, v, batch, heads, sq, skv, d)
+    if out is None:
+        out = torch.empty(batch * sq, heads * d, device=q.device, dtype=BF16)
+    _dev(out)
+    scale = d ** -0.5 if scale is None else scale
+    check(lib().vd_attention_fp8(_p(ws["q8"]), _p(ws["k8"]), ws["ld8"], _p(ws["qs"]), _p(ws["ks"]), _p(ws["vt8"]),
+                                 _p(ws["vs"]), _p(out), out.stride(0), batch, heads, sq, skv, d, scale, _stream()),
+          "vd_attention_fp8")
+    return out
