@@ -1,0 +1,51 @@
+"""fp8 vs bf16 spatial self-attention at the DiT's shape (S = 2304, d = 64, 64 images x 18
+heads), timed with HIP events; used under rocprofv3 --pmc for the kernel's counters.
+
+    python tools/attn_fp8_bench.py [--reps 10] [--images 64]
+"""
+import argparse
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "video-diffusion-experiments_amd")]
+import torch  # noqa: E402
+
+from vdiff import ops  # noqa: E402
+from vdiff._lib import lib  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--images", type=int, default=64)
+ap.add_argument("--seq", type=int, default=2304)
+a = ap.parse_args()
+n, heads, S, d = a.images, 18, a.seq, 64
+D = heads * d
+qkv = torch.randn(n * S, 3 * D, device="cuda").to(torch.bfloat16)
+q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+o = torch.empty(n * S, D, device="cuda", dtype=torch.bfloat16)
+ws = ops.attention_fp8_quant(q, k, v, n, heads, S, S, d)
+st = torch.cuda.current_stream().cuda_stream
+
+
+def fp8():
+    lib().vd_attention_fp8(ws["q8"].data_ptr(), ws["k8"].data_ptr(), ws["ld8"], ws["qs"].data_ptr(), ws["ks"].data_ptr(),
+                           ws["vt8"].data_ptr(), ws["vs"].data_ptr(), o.data_ptr(), o.stride(0), n, heads, S, S, d,
+                           d ** -0.5, st)
+
+
+def bf16():
+    ops.attention(q, k, v, n, heads, S, S, d, out=o)
+
+
+flop = 4.0 * n * heads * S * S * d
+for name, fn in (("fp8", fp8), ("bf16", bf16)):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / a.reps
+    print(f"{name}: {ms:.4f} ms  {flop / ms / 1e9:.1f} TFLOP/s", flush=True)
