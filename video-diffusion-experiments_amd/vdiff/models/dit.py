@@ -124,45 +124,68 @@ class DiT3DModel:
         """Per-block cross-attention K/V of the (constant) text rows [B*L, Dt]."""
         return [ops.gemm(ehs_rows, blk["cross.to_kv"][0], bias=blk["cross.to_kv"][1]) for blk in self.blocks]
 
-    def forward_rows(self, x_tok, B, F, Hp, Wp, mod, kv, L):
-        """x_tok: bf16 patch rows [B*F*Hp*Wp, kpad] -> fp32 token rows [.., p*p*C_out]."""
+    def _block(self, i, blk, x, y, gate, mod, B, F, P, rope, kv, L, rpb, spatial):
+        """One block over rows (b, f, p) of F frames x P positions; the previous MLP's gated
+        residual (y, gate) is folded into the first row pass.  Returns the new x and the
+        block's own pending (y, gate)."""
         D, d, heads = self.D, self.d, self.heads
+        base = 6 * D * i
+        sh1, sc1, g1, sh2, sc2, g2 = (mod[:, base + j * D: base + (j + 1) * D] for j in range(6))
+        h = ops.res_ln_mod(x, y=y, gate=gate, x_out=x if y is not None else None, shift=sh1, scale=sc1,
+                           rows_per_b=rpb)
+        qkv = ops.gemm(h, blk["attn.to_qkv"][0], bias=blk["attn.to_qkv"][1])
+        q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+        ops.rope_qk(qkv, 2 * D, d, 0 if spatial else 1, *rope, self.config["rope_theta"])
+        if not spatial:
+            a = ops.temporal_attention(q, k, v, B, F, P, heads, d)
+        elif self.attn_fp8 and d == 64 and P % 64 == 0:
+            a = ops.attention_fp8(q, k, v, B * F, heads, P, P, d)
+        else:
+            a = ops.attention(q, k, v, B * F, heads, P, P, d)
+        y = ops.gemm(a, blk["attn.to_out"][0], bias=blk["attn.to_out"][1])
+        h = ops.res_ln_mod(x, y=y, gate=g1, x_out=x, rows_per_b=rpb)
+        qc = ops.gemm(h, blk["cross.to_q"][0], bias=blk["cross.to_q"][1])
+        a = ops.attention(qc, kv[i][:, :D], kv[i][:, D:], B * F, heads, P, L, d, kv_div=F)
+        x = ops.gemm(a, blk["cross.to_out"][0], bias=blk["cross.to_out"][1], res=x)
+        h = ops.res_ln_mod(x, shift=sh2, scale=sc2, rows_per_b=rpb)
+        m = ops.gemm(h, blk["mlp.fc1"][0], bias=blk["mlp.fc1"][1], act=ops.ACT_GELU)
+        y = ops.gemm(m, blk["mlp.fc2"][0], bias=blk["mlp.fc2"][1])
+        return x, y, g2
+
+    def forward_rows(self, x_tok, B, F, Hp, Wp, mod, kv, L, dist=None):
+        """x_tok: bf16 patch rows [B*F*Hp*Wp, kpad] -> fp32 token rows [.., p*p*C_out].
+
+        dist (vdiff.dist.FrameShard): this rank holds F of the world*F frames (both CFG
+        halves).  Spatial blocks are frame-local; each temporal block re-shards the residual
+        stream frame -> position shards with one all-to-all, runs on all frames of
+        Hp*Wp/world positions, and re-shards back (as the UNet's motion
+        modules)."""
+        D = self.D
         S = Hp * Wp
-        rows = B * F * S
-        rpb = F * S
-        theta = self.config["rope_theta"]
+        rpb = F * S  # rows per video: the same in the frame and the position layout
         x = ops.gemm(x_tok, self.w_pe, bias=self.b_pe)
-        x_alt = torch.empty_like(x)
         y = gate = None
         for i, blk in enumerate(self.blocks):
-            base = 6 * D * i
-            sh1, sc1, g1, sh2, sc2, g2 = (mod[:, base + j * D: base + (j + 1) * D] for j in range(6))
-            h = ops.res_ln_mod(x, y=y, gate=gate, x_out=x if y is not None else None, shift=sh1,
-                               scale=sc1, rows_per_b=rpb)
-            qkv = ops.gemm(h, blk["attn.to_qkv"][0], bias=blk["attn.to_qkv"][1])
-            q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
             if i % 2 == 0:
-                ops.rope_qk(qkv, 2 * D, d, 0, F, Hp, Wp, theta)
-                if self.attn_fp8 and d == 64 and S % 64 == 0:
-                    a = ops.attention_fp8(q, k, v, B * F, heads, S, S, d)
-                else:
-                    a = ops.attention(q, k, v, B * F, heads, S, S, d)
+                x, y, gate = self._block(i, blk, x, y, gate, mod, B, F, S, (F, Hp, Wp), kv, L, rpb, True)
+            elif dist is None:
+                x, y, gate = self._block(i, blk, x, y, gate, mod, B, F, S, (F, Hp, Wp), kv, L, rpb, False)
             else:
-                ops.rope_qk(qkv, 2 * D, d, 1, F, Hp, Wp, theta)
-                a = ops.temporal_attention(q, k, v, B, F, S, heads, d)
-            y = ops.gemm(a, blk["attn.to_out"][0], bias=blk["attn.to_out"][1])
-            h = ops.res_ln_mod(x, y=y, gate=g1, x_out=x, rows_per_b=rpb)
-            qc = ops.gemm(h, blk["cross.to_q"][0], bias=blk["cross.to_q"][1])
-            a = ops.attention(qc, kv[i][:, :D], kv[i][:, D:], B * F, heads, S, L, d, kv_div=F)
-            ops.gemm(a, blk["cross.to_out"][0], bias=blk["cross.to_out"][1], res=x, out=x_alt)
-            x, x_alt = x_alt, x
-            h = ops.res_ln_mod(x, shift=sh2, scale=sc2, rows_per_b=rpb)
-            m = ops.gemm(h, blk["mlp.fc1"][0], bias=blk["mlp.fc1"][1], act=ops.ACT_GELU)
-            y = ops.gemm(m, blk["mlp.fc2"][0], bias=blk["mlp.fc2"][1])
-            gate = g2
+                W = dist.world
+                if S % W:
+                    raise ValueError(f"{S} positions do not shard over {W} ranks")
+                if y is not None:  # finish the pending residual before the re-shard
+                    ops.res_ln_mod(x, y=y, gate=gate, x_out=x, rows_per_b=rpb)
+                xp = dist.to_position_shards(x, B, F, S, ops.block_transpose)
+                Fg, Pl = F * W, S // W
+                xp, y, gate = self._block(i, blk, xp, None, None, mod, B, Fg, Pl, (Fg, 1, Pl), kv, L, rpb, False)
+                ops.res_ln_mod(xp, y=y, gate=gate, x_out=xp, rows_per_b=rpb)
+                x = dist.to_frame_shards(xp, B, F, S, ops.block_transpose)
+                y = gate = None
         base = 6 * D * len(self.blocks)
         shf, scf = mod[:, base:base + D], mod[:, base + D:base + 2 * D]
-        h = ops.res_ln_mod(x, y=y, gate=gate, x_out=x, shift=shf, scale=scf, rows_per_b=rpb)
+        h = ops.res_ln_mod(x, y=y, gate=gate, x_out=x if y is not None else None, shift=shf, scale=scf,
+                           rows_per_b=rpb)
         return ops.gemm(h, self.w_fin, bias=self.b_fin, out_f32=True)
 
     # ------------------------------------------------------------------ call surface
@@ -193,7 +216,10 @@ class DiTDenoiseLoop:
     unpatchify, the fused CFG + scheduler kernel, re-patchify of the new latents."""
 
     def __init__(self, model: DiT3DModel, scheduler, latents, prompt_embeds, guidance_scale,
-                 use_graph=True):
+                 use_graph=True, dist=None):
+        """dist (vdiff.dist.FrameShard): latents hold this rank's frames only (the CFG
+        update and patchify are per frame); temporal blocks re-shard (forward_rows)."""
+        self.dist = dist
         dev = model.device
         self.m = model
         self.ncfg = 2 if guidance_scale > 1 else 1
@@ -224,7 +250,8 @@ class DiTDenoiseLoop:
         te = ops.timestep_embed(self.ts, m.config["freq_dim"], step_idx=self.step_idx, batch=self.Bt)
         mod = m.modulation(te)
         p = m.p
-        out = m.forward_rows(self.x_tok, self.Bt, self.F, self.H // p, self.W // p, mod, self.kv, self.L)
+        out = m.forward_rows(self.x_tok, self.Bt, self.F, self.H // p, self.W // p, mod, self.kv, self.L,
+                             dist=self.dist)
         eps = ops.unpatchify(out, self.Bt * self.F, self.H, self.W, p, m.config["out_channels"])
         self.sched_step(eps, self.ncfg, self.g, self.lat, self.coef, step_idx=self.step_idx)
         ops.patchify(self.lat, p, m.kpad, dup=self.ncfg, out=self.x_tok)
