@@ -2,7 +2,10 @@
 denoiser (patchified 3D latents) … 32 frames × 768×768"), 1x MI355X, bf16, CFG batch 2,
 hipGraph-captured DDIM step (vdiff.models.dit.DiTDenoiseLoop), synthetic N(0, 0.02^2) weights.
 
-    python tools/dit_bench.py [--frames 32] [--size 96] [--steps 5] [--warmup 2] [--cpu]
+    python tools/dit_bench.py [--frames 32] [--size 96] [--steps 5] [--warmup 2] [--cpu] [--fp8]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/dit_bench.py
+        (frame sharding over N GPUs: F/N frames of both CFG halves per rank, an RCCL all-to-all
+        around every temporal block; barrier + max-over-ranks timing, whole-node steps/s)
 
 Prints one JSON line: denoising steps/s, ms/step, the algorithmic TFLOP per step (2*M*N*K
 over every linear and attention product) and its MFMA fraction, the spatial-attention
@@ -50,6 +53,16 @@ def main():
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="spatial self-attention on the fp8 MFMA kernel")
     args = ap.parse_args()
+    import os
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    fs = None
+    if world > 1:
+        import torch.distributed as tdist
+        from vdiff.dist import FrameShard
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        tdist.init_process_group("nccl")
+        fs = FrameShard()
     cfg = dict(DIT_FULL, num_frames=args.frames, sample_size=args.size)
     t0 = time.time()
     sd = init_dit_state_dict(cfg, seed=0, device="cuda")
@@ -61,14 +74,29 @@ def main():
     ehs = torch.randn((2, 77, cfg["text_dim"]), generator=torch.Generator().manual_seed(1))
     s = DDIMScheduler(beta_schedule="linear", steps_offset=1, clip_sample=False)
     s.set_timesteps(50)
-    loop = DiTDenoiseLoop(model, s, lat.cuda(), ehs.cuda(), 7.5).prime()
-    print(f"[dit_bench] ready in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    fl = F // world
+    local = lat[:, :, rank * fl:(rank + 1) * fl]
+    loop = DiTDenoiseLoop(model, s, local.cuda(), ehs.cuda(), 7.5, dist=fs).prime()
+    print(f"[dit_bench] rank {rank}/{world} ready in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     loop.run(args.warmup)
-    torch.cuda.synchronize()
+
+    def barrier():
+        if fs is not None:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
     t1 = time.perf_counter()
     loop.run(args.steps)
-    torch.cuda.synchronize()
+    barrier()
     dt = (time.perf_counter() - t1) / args.steps
+    if fs is not None:
+        t = torch.tensor([dt], device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+        if rank != 0:
+            torch.distributed.destroy_process_group()
+            return
     S = (H // 2) ** 2
     flop, sp_flop = step_flop(cfg, 2, F, S)
     # the spatial attention kernel alone (one launch = all 2F frames x 18 heads)
@@ -107,7 +135,8 @@ def main():
         "metric": "DiT denoising steps/s (BASELINE config 5 shapes, CFG batch 2, 1 GPU)",
         "value": round(1.0 / dt, 4), "unit": "denoising steps/s", "ms_per_step": round(dt * 1e3, 3),
         "dtype": "bf16", "data": "synthetic (weights N(0,0.02^2) seed 0, latents randn seed 42)",
-        "config": {"frames": F, "latent_hw": H, "pixels": H * 8, "tokens_per_frame": S,
+        "n_gpus": world, "scaling": "strong",
+        "config": {"frames": F, "latent_hw": H, "parallelism": f"frame-shard x{world}" if world > 1 else "single-GPU", "pixels": H * 8, "tokens_per_frame": S,
                    "hidden": D, "heads": cfg["num_heads"], "depth": cfg["depth"], "hipgraph": True},
         "step_mfma": {"algorithmic_tflop": round(flop / 1e12, 3),
                       "achieved": round(flop / dt / 1e12, 1), "peak": PEAK,
@@ -135,6 +164,8 @@ def main():
                                "cores": torch.get_num_threads(), "kind": "port",
                                "sample": f"oracle fp32, 1 frame x CFG 2, {ct:.1f} s, scaled x{F}"}
     print(json.dumps(res), flush=True)
+    if fs is not None:
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":
