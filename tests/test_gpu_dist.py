@@ -54,3 +54,19 @@ def test_sharded_loop_world1_matches_unsharded(pg):
     finally:
         unet.dist = None
     assert torch.equal(out, ref)
+
+
+def test_dit_sharded_loop_world1_matches_unsharded(pg):
+    """The DiT's frame-sharded path (an all-to-all re-shard around every temporal block,
+    tools/dit_bench.py's multi-GPU mode) on RCCL, captured into the step's hipGraph."""
+    from vdiff.models.dit import DIT_TINY, DiT3DModel, DiTDenoiseLoop, init_dit_state_dict
+    torch.manual_seed(0)
+    m = DiT3DModel(DIT_TINY, init_dit_state_dict(DIT_TINY, seed=3), device="cuda")
+    lat = torch.randn(1, 4, 4, 16, 16, device="cuda")
+    ehs = torch.randn(2, 77, 64, device="cuda")
+    s = DDIMScheduler(beta_schedule="linear", steps_offset=1, clip_sample=False)
+    s.set_timesteps(50)
+    ref = DiTDenoiseLoop(m, s, lat, ehs, 7.5, use_graph=True).prime().run(2).clone()
+    loop = DiTDenoiseLoop(m, s, lat, ehs, 7.5, use_graph=True, dist=FrameShard()).prime()
+    assert loop.graph is not None
+    assert torch.equal(loop.run(2), ref)
