@@ -79,3 +79,31 @@ def test_gemm_workspace_policy():
     small = L.GemmDesc(M=2048, N=1280, K=11520, k0=11520, lda0=11520, ldw=11520, a_mode=0)
     nbytes = L.lib().vd_gemm_ws_bytes(ctypes.byref(small))
     assert nbytes > 0 and nbytes % (2048 * 1280 * 4) == 0
+
+
+def test_dit_entry_points_validate_before_launch():
+    """The DiT / fp8 entry points (§8f rank 3) reject bad arguments with VD_EINVAL before any
+    launch (null operands, unsupported head width, unaligned shapes) — no GPU needed."""
+    h = L.lib()
+    assert h.vd_patchify(None, 1, 4, 4, 16, 16, 2, 1, 1.0, None, 16, None) == 1000
+    assert h.vd_unpatchify(None, 16, 4, 16, 16, 2, 4, None, None) == 1000
+    assert h.vd_rope_qk(None, 384, 64, 256, 64, 0, 4, 8, 8, 10000.0, None) == 1000
+    assert h.vd_res_ln_mod(None, 128, None, 0, None, None, None, 0, 64, None, 0, None, 128, 64, 128, 1e-6,
+                           None) == 1000
+    assert h.vd_attention_fp8(None, None, 64, None, None, None, None, None, 64, 1, 1, 64, 64, 64, 0.125,
+                              None) == 1000
+    buf = ctypes.create_string_buffer(64)
+    p = ctypes.addressof(buf)
+    # d = 80 is not an fp8 kernel variant; skv must be a multiple of 64
+    assert h.vd_attention_fp8(p, p, 64, p, p, p, p, p, 64, 1, 1, 64, 64, 80, 0.1, None) == 1000
+    assert h.vd_attention_fp8_quant(p, 64, p, 64, p, 64, 1, 1, 64, 70, 64, p, p, 64, p, p, p, p, None) == 1000
+
+
+def test_dit_ops_refuse_cpu_tensors():
+    x = torch.zeros(64, 128, dtype=torch.bfloat16)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ops.res_ln_mod(x)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ops.patchify(torch.zeros(1, 4, 2, 8, 8), 2, 16)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ops.attention_fp8(x, x, x, 1, 2, 64, 64)
