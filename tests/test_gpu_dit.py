@@ -189,6 +189,50 @@ def test_attention_fp8_quant_layout(cuda):
     torch.testing.assert_close(v, vref, rtol=2 ** -4, atol=vsc.max().item() * 2 ** -9)
 
 
+def test_attention_fp8_quant_rope_fused(cuda):
+    """vd_attention_fp8_quant_rope: the spatial 2-D RoPE applied in fp32 inside the quantization
+    pass.  Dequantized Q/K within e4m3 rounding of the fp32 oracle RoPE (dit_ref.rope) of the
+    un-rotated rows; q/k/v rows left untouched; V^T bytes and scales identical to the unfused
+    quantization; attention output within 1 % of rope_qk -> attention_fp8 (which rounds the
+    rotated rows to bf16 first)."""
+    g = torch.Generator().manual_seed(11)
+    B, heads, Hp, Wp, d = 2, 3, 8, 16, 64  # non-square grid: the h and w sections differ
+    S, D = Hp * Wp, heads * d
+    qkv = (torch.randn(B * S, 3 * D + 8, generator=g) * 1.5).to(torch.bfloat16)
+    c = qkv.cuda()
+    ws = ops.attention_fp8_quant(c[:, :D], c[:, D:2 * D], c[:, 2 * D:3 * D], B, heads, S, S, d,
+                                 rope=(Hp, Wp, 10000.0))
+    assert torch.equal(c.cpu(), qkv)
+    r = torch.arange(B * S)
+    z = qkv.float()[:, :2 * D].reshape(B * S, 2 * heads, d)
+    zh = dit_ref.rope(z[..., :d // 2].transpose(0, 1), (r // Wp) % Hp, 10000.0).transpose(0, 1)
+    zw = dit_ref.rope(z[..., d // 2:].transpose(0, 1), r % Wp, 10000.0).transpose(0, 1)
+    want = torch.cat([zh, zw], -1)
+    f8 = torch.float8_e4m3fn
+    for j, (x8, xs) in enumerate(((ws["q8"], ws["qs"]), (ws["k8"], ws["ks"]))):
+        sc = torch.exp2(xs.cpu().float() - 127)
+        dq = x8.cpu()[:, :D].contiguous().view(f8).float().reshape(B * S, heads, d) * sc[..., None]
+        ref = want[:, j * heads:(j + 1) * heads]
+        torch.testing.assert_close(dq, ref, rtol=2 ** -4, atol=sc.max().item() * 2 ** -9)
+        assert float((ref.abs().amax(-1) / sc).max()) <= 448.0
+    plain = ops.attention_fp8_quant(c[:, :D], c[:, D:2 * D], c[:, 2 * D:3 * D], B, heads, S, S, d)
+    assert torch.equal(ws["vt8"].cpu(), plain["vt8"].cpu()) and torch.equal(ws["vs"].cpu(), plain["vs"].cpu())
+    fused = ops.attention_fp8(c[:, :D], c[:, D:2 * D], c[:, 2 * D:3 * D], B, heads, S, S, d,
+                              rope=(Hp, Wp, 10000.0)).float().cpu()
+    ops.rope_qk(c, 2 * D, d, 0, 1, Hp, Wp, 10000.0)
+    unfused = ops.attention_fp8(c[:, :D], c[:, D:2 * D], c[:, 2 * D:3 * D], B, heads, S, S, d).float().cpu()
+    # both are one e4m3 quantization of (nearly) the same rotated values; values near an e4m3
+    # rounding boundary flip with the bf16 rounding the unfused path adds, so compare both with
+    # exact fp32 SDPA of the fp32-rotated operands: the fused path is no less accurate
+    qh = want[:, :heads].reshape(B, S, heads, d).transpose(1, 2)
+    kh = want[:, heads:].reshape(B, S, heads, d).transpose(1, 2)
+    vh = qkv.float()[:, 2 * D:3 * D].reshape(B, S, heads, d).transpose(1, 2)
+    exact = torch.nn.functional.scaled_dot_product_attention(qh, kh, vh).transpose(1, 2).reshape(B * S, D)
+    err_f, err_u = rel_l2(fused, exact), rel_l2(unfused, exact)
+    print(f"fused RoPE+fp8 vs fp32 {err_f:.4f}, unfused {err_u:.4f}, fused vs unfused {rel_l2(fused, unfused):.4f}")
+    assert err_f < 0.10 and err_f <= 1.1 * err_u + 0.005, (err_f, err_u)
+
+
 def _fp8_emulated_attention(qkv, B, heads, S, d):
     """fp32 torch restatement of vd_attention_fp8's arithmetic: Q/K rounded to e4m3 with
     per-(token, head) power-of-two scales, V per (image, head, 64-key tile), P = exp2(s - max)

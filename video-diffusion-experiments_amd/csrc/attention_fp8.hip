@@ -91,6 +91,57 @@ __global__ void quant_rows_kernel(const bf16_t* __restrict__ x, int64_t ldx, int
   }
 }
 
+// Q or K rows with the DiT's spatial 2-D RoPE fused (vd_attention_fp8_quant_rope): eight
+// lanes per (row, head), lane c owns elements [8c, 8c + 8) and also loads its rotate-half
+// partner chunk c ^ 2 (same 32-wide section), so loads stay coalesced 16-byte chunks and
+// every lane evaluates only 8 angles; the head's amax is reduced over the 8 lanes with
+// xor shuffles.  Section 0 (chunks 0-3) rotates by h = (r / Wp) % Hp, section 1 by
+// w = r % Wp; pair (i, i + 16) of a section at angle pos * theta^(-2i/32) (dit.hip
+// rope_kernel mode 0).  Rotation in fp32, never rounded to bf16.
+__global__ __launch_bounds__(NT) void quant_rows_rope_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                             int64_t rows, int heads, uint8_t* __restrict__ x8,
+                                                             int64_t ld8, uint8_t* __restrict__ sc, int64_t Hp,
+                                                             int64_t Wp, float log2_theta) {
+  // 32-bit index math (the host checks rows * heads * 8 < 2^31): 64-bit divisions by heads,
+  // Wp and Hp would dominate this HBM pass.  total is a multiple of 8, so a lane group never
+  // straddles the grid stride.
+  const uint32_t total = (uint32_t)(rows * heads * 8);
+  const uint32_t uh = (uint32_t)heads, uw = (uint32_t)Wp, uhp = (uint32_t)Hp;
+  for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const int c = (int)(i & 7);
+    const uint32_t rh = i >> 3;
+    const uint32_t r = rh / uh;
+    const int h = (int)(rh - r * uh);
+    const bf16_t* src = x + (int64_t)r * ldx + h * FD;
+    float own[8], par[8];
+    unpack8(*(const uint4*)(src + 8 * c), own);
+    unpack8(*(const uint4*)(src + 8 * (c ^ 2)), par);
+    const uint32_t rw = r / uw;
+    const float pos = (float)(c < 4 ? rw % uhp : r - rw * uw);
+    const bool lo = (c & 2) == 0;  // holds the first half of its pairs
+    const int j0 = 8 * (c & 1);
+    float v[8];
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float inv_freq = exp2f(-log2_theta * (float)(2 * (j0 + j)) * (1.0f / (FD / 2)));
+      float sn, cs;
+      __sincosf(pos * inv_freq, &sn, &cs);
+      v[j] = lo ? own[j] * cs - par[j] * sn : own[j] * cs + par[j] * sn;
+      amax = fmaxf(amax, fabsf(v[j]));
+    }
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 8));
+    amax = fmaxf(amax, __shfl_xor(amax, 2, 8));
+    amax = fmaxf(amax, __shfl_xor(amax, 4, 8));
+    const int e = e8m0_for(amax);
+    const float inv = e8m0_inv(e);
+    *(uint2*)(x8 + (int64_t)r * ld8 + h * FD + 8 * c) =
+        make_uint2(pack4_fp8(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
+                   pack4_fp8(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv));
+    if (c == 0) sc[rh] = (uint8_t)e;
+  }
+}
+
 // slot p = 32h + j of a 64-key tile holds key 32 (j >> 4) + (j & 3) + 8 ((j & 15) >> 2) + 4h
 __device__ __forceinline__ int slot_key(int p) {
   const int h = p >> 5, j = p & 31;
@@ -269,27 +320,56 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_kernel(
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+int quant_operands(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                   int64_t batch, int32_t heads, int64_t sq, int64_t skv, int32_t d, bool rope, int64_t Hp,
+                   int64_t Wp, float theta, void* q8, void* k8, int64_t ld8, void* vt8, void* qs, void* ks,
+                   void* vs, vd_stream_t stream) {
+  VD_CHECK_ARG(d == FD && heads > 0 && batch > 0 && sq > 0 && skv > 0 && skv % KT8 == 0);
+  VD_CHECK_ARG(q && k && v && q8 && k8 && vt8 && qs && ks && vs && al16(q) && al16(k) && al16(v));
+  VD_CHECK_ARG(al16(q8) && al16(k8) && al16(vt8) && ld8 % 16 == 0 && ld8 >= (int64_t)heads * FD);
+  VD_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0);
+  if (rope) {
+    VD_CHECK_ARG(Hp > 0 && Wp > 0 && sq == Hp * Wp && skv == sq && theta > 1.f);
+    VD_CHECK_ARG(batch * sq * heads * 8 < 0x7fffffff);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  auto grid = [](int64_t n) { const int64_t b = (n + NT - 1) / NT; return (unsigned)(b < 16384 ? b : 16384); };
+  if (rope) {
+    const float l2t = log2f(theta);
+    hipLaunchKernelGGL(quant_rows_rope_kernel, dim3(grid(batch * sq * heads * 8)), dim3(NT), 0, s,
+                       (const bf16_t*)q, ldq, batch * sq, (int)heads, (uint8_t*)q8, ld8, (uint8_t*)qs, Hp, Wp, l2t);
+    hipLaunchKernelGGL(quant_rows_rope_kernel, dim3(grid(batch * skv * heads * 8)), dim3(NT), 0, s,
+                       (const bf16_t*)k, ldk, batch * skv, (int)heads, (uint8_t*)k8, ld8, (uint8_t*)ks, Hp, Wp, l2t);
+  } else {
+    hipLaunchKernelGGL(quant_rows_kernel, dim3(grid(batch * sq * heads)), dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                       batch * sq, (int)heads, (uint8_t*)q8, ld8, (uint8_t*)qs);
+    hipLaunchKernelGGL(quant_rows_kernel, dim3(grid(batch * skv * heads)), dim3(NT), 0, s, (const bf16_t*)k, ldk,
+                       batch * skv, (int)heads, (uint8_t*)k8, ld8, (uint8_t*)ks);
+  }
+  const int64_t nblk = batch * heads * (skv / KT8);
+  VD_CHECK_ARG(nblk < 0x7fffffff);
+  hipLaunchKernelGGL(quant_vt_kernel, dim3((unsigned)nblk), dim3(NT), 0, s, (const bf16_t*)v, ldv, (int)heads, skv,
+                     (uint8_t*)vt8, (uint8_t*)vs);
+  return vd_launch_status();
+}
+
 }  // namespace
 
 extern "C" int vd_attention_fp8_quant(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                                       int64_t ldv, int64_t batch, int32_t heads, int64_t sq, int64_t skv,
                                       int32_t d, void* q8, void* k8, int64_t ld8, void* vt8, void* qs,
                                       void* ks, void* vs, vd_stream_t stream) {
-  VD_CHECK_ARG(d == FD && heads > 0 && batch > 0 && sq > 0 && skv > 0 && skv % KT8 == 0);
-  VD_CHECK_ARG(q && k && v && q8 && k8 && vt8 && qs && ks && vs && al16(q) && al16(k) && al16(v));
-  VD_CHECK_ARG(al16(q8) && al16(k8) && al16(vt8) && ld8 % 16 == 0 && ld8 >= (int64_t)heads * FD);
-  VD_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0);
-  hipStream_t s = (hipStream_t)stream;
-  auto grid = [](int64_t n) { const int64_t b = (n + NT - 1) / NT; return (unsigned)(b < 16384 ? b : 16384); };
-  hipLaunchKernelGGL(quant_rows_kernel, dim3(grid(batch * sq * heads)), dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                     batch * sq, (int)heads, (uint8_t*)q8, ld8, (uint8_t*)qs);
-  hipLaunchKernelGGL(quant_rows_kernel, dim3(grid(batch * skv * heads)), dim3(NT), 0, s, (const bf16_t*)k, ldk,
-                     batch * skv, (int)heads, (uint8_t*)k8, ld8, (uint8_t*)ks);
-  const int64_t nblk = batch * heads * (skv / KT8);
-  VD_CHECK_ARG(nblk < 0x7fffffff);
-  hipLaunchKernelGGL(quant_vt_kernel, dim3((unsigned)nblk), dim3(NT), 0, s, (const bf16_t*)v, ldv, (int)heads, skv,
-                     (uint8_t*)vt8, (uint8_t*)vs);
-  return vd_launch_status();
+  return quant_operands(q, ldq, k, ldk, v, ldv, batch, heads, sq, skv, d, false, 0, 0, 0.f, q8, k8, ld8, vt8,
+                        qs, ks, vs, stream);
+}
+
+extern "C" int vd_attention_fp8_quant_rope(const void* q, int64_t ldq, const void* k, int64_t ldk,
+                                           const void* v, int64_t ldv, int64_t batch, int32_t heads,
+                                           int64_t s, int32_t d, int64_t Hp, int64_t Wp, float theta, void* q8,
+                                           void* k8, int64_t ld8, void* vt8, void* qs, void* ks, void* vs,
+                                           vd_stream_t stream) {
+  return quant_operands(q, ldq, k, ldk, v, ldv, batch, heads, s, s, d, true, Hp, Wp, theta, q8, k8, ld8, vt8, qs,
+                        ks, vs, stream);
 }
 
 extern "C" int vd_attention_fp8(const void* q8, const void* k8, int64_t ld8, const void* qs, const void* ks,

@@ -62,25 +62,28 @@ __global__ void unpatchify_kernel(const float* __restrict__ src, int64_t ld_src,
 // + h)*Wp + w.  mode 0 (spatial, 2-D): dims [0, d/2) rotate with position h, [d/2, d)
 // with w; mode 1 (temporal, 1-D): all d dims with position f.  Inside a section of
 // width S the pairs are (i, i + S/2) at angle pos * theta^(-2i/S).  One thread owns 8
-// consecutive pairs (two 16-byte loads / stores).
+// consecutive pairs (two 16-byte loads / stores).  I = uint32_t when rows * ncols fits
+// (index divisions in 32 bits: the 64-bit ones cost more than the pass's HBM time).
+template <typename I>
 __global__ void rope_kernel(bf16_t* __restrict__ x, int64_t ld, int64_t rows, int ncols, int d,
                             int mode, int64_t F, int64_t Hp, int64_t Wp, float log2_theta) {
   const int S = mode == 0 ? d / 2 : d;       // section width
   const int half = S / 2;
   const int chunks_per_row = ncols / 2 / 8;  // 8-pair chunks per row
   const int chunks_per_sec = half / 8;
-  const int64_t total = rows * chunks_per_row;
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
-    const int64_t r = i / chunks_per_row;
-    const int cj = (int)(i % chunks_per_row);
+  const I total = (I)(rows * chunks_per_row);
+  const I uF = (I)F, uHp = (I)Hp, uWp = (I)Wp, ucpr = (I)chunks_per_row;
+  for (I i = (I)blockIdx.x * NT + threadIdx.x; i < total; i += (I)gridDim.x * NT) {
+    const I r = i / ucpr;
+    const int cj = (int)(i - r * ucpr);
     const int sec_global = cj / chunks_per_sec;  // (head, section) index
     const int j0 = (cj % chunks_per_sec) * 8;    // first pair index inside the section
     const int col = sec_global * S + j0;
     const int sec = mode == 0 ? (sec_global % 2) : 0;
-    int64_t pos;
-    if (mode == 0) pos = sec == 0 ? (r / Wp) % Hp : r % Wp;
-    else pos = (r / (Wp * Hp)) % F;
-    bf16_t* p0 = x + r * ld + col;
+    I pos;
+    if (mode == 0) pos = sec == 0 ? (r / uWp) % uHp : r % uWp;
+    else pos = (r / (uWp * uHp)) % uF;
+    bf16_t* p0 = x + (int64_t)r * ld + col;
     bf16_t* p1 = p0 + half;
     float a[8], b[8];
     unpack8(*(const uint4*)p0, a);
@@ -207,7 +210,8 @@ extern "C" int vd_rope_qk(void* x, int64_t ld, int64_t rows, int32_t ncols, int3
   VD_CHECK_ARG(mode == 0 ? d % 32 == 0 : d % 16 == 0);
   VD_CHECK_ARG(F > 0 && Hp > 0 && Wp > 0 && theta > 1.f);
   const int64_t total = rows * (ncols / 16);
-  hipLaunchKernelGGL(rope_kernel, dim3(grid_of(total)), dim3(NT), 0, (hipStream_t)stream, (bf16_t*)x,
+  auto kern = total < 0x7fffffff && Hp * Wp < 0x7fffffff ? rope_kernel<uint32_t> : rope_kernel<int64_t>;
+  hipLaunchKernelGGL(kern, dim3(grid_of(total)), dim3(NT), 0, (hipStream_t)stream, (bf16_t*)x,
                      ld, rows, (int)ncols, (int)d, (int)mode, F, Hp, Wp, log2f(theta));
   return vd_launch_status();
 }

@@ -135,12 +135,15 @@ class DiT3DModel:
                            rows_per_b=rpb)
         qkv = ops.gemm(h, blk["attn.to_qkv"][0], bias=blk["attn.to_qkv"][1])
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
-        ops.rope_qk(qkv, 2 * D, d, 0 if spatial else 1, *rope, self.config["rope_theta"])
-        if not spatial:
+        theta = self.config["rope_theta"]
+        if spatial and self.attn_fp8 and d == 64 and P % 64 == 0:
+            # the spatial RoPE runs inside the fp8 quantization pass (q, k stay un-rotated)
+            a = ops.attention_fp8(q, k, v, B * F, heads, P, P, d, rope=(rope[1], rope[2], theta))
+        elif not spatial:
+            ops.rope_qk(qkv, 2 * D, d, 1, *rope, theta)
             a = ops.temporal_attention(q, k, v, B, F, P, heads, d)
-        elif self.attn_fp8 and d == 64 and P % 64 == 0:
-            a = ops.attention_fp8(q, k, v, B * F, heads, P, P, d)
         else:
+            ops.rope_qk(qkv, 2 * D, d, 0, *rope, theta)
             a = ops.attention(q, k, v, B * F, heads, P, P, d)
         y = ops.gemm(a, blk["attn.to_out"][0], bias=blk["attn.to_out"][1])
         h = ops.res_ln_mod(x, y=y, gate=g1, x_out=x, rows_per_b=rpb)

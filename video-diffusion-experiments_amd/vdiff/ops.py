@@ -357,8 +357,10 @@ def res_ln_mod(x, *, y=None, gate=None, shift=None, scale=None, rows_per_b=None,
     return out
 
 
-def attention_fp8_quant(q, k, v, batch, heads, sq, skv, d=64):
-    """bf16 q/k/v row views -> the fp8 operands of vd_attention_fp8 (a dict of buffers)."""
+def attention_fp8_quant(q, k, v, batch, heads, sq, skv, d=64, rope=None):
+    """bf16 q/k/v row views -> the fp8 operands of vd_attention_fp8 (a dict of buffers).
+    rope=(Hp, Wp, theta): apply the spatial 2-D RoPE (rope_qk mode 0) to q and k inside the
+    quantization pass (vd_attention_fp8_quant_rope); q and k are read un-rotated."""
     _dev(q, k, v)
     dev = q.device
     ld8 = (heads * d + 15) // 16 * 16
@@ -370,15 +372,25 @@ def attention_fp8_quant(q, k, v, batch, heads, sq, skv, d=64):
           "ks": torch.empty(batch * skv, heads, device=dev, dtype=u8),
           "vs": torch.empty(batch * heads, max(1, skv // 64), device=dev, dtype=u8),
           "ld8": ld8, "batch": batch, "heads": heads, "sq": sq, "skv": skv, "d": d}
+    if rope is not None:
+        if sq != skv:
+            raise ValueError("fused RoPE quantization needs sq == skv (self-attention)")
+        Hp, Wp, theta = rope
+        check(lib().vd_attention_fp8_quant_rope(
+            _p(q), q.stride(0), _p(k), k.stride(0), _p(v), v.stride(0), batch, heads, sq, d, Hp, Wp, theta,
+            _p(ws["q8"]), _p(ws["k8"]), ld8, _p(ws["vt8"]), _p(ws["qs"]), _p(ws["ks"]), _p(ws["vs"]), _stream()),
+            "vd_attention_fp8_quant_rope")
+        return ws
     check(lib().vd_attention_fp8_quant(_p(q), q.stride(0), _p(k), k.stride(0), _p(v), v.stride(0), batch, heads,
                                        sq, skv, d, _p(ws["q8"]), _p(ws["k8"]), ld8, _p(ws["vt8"]), _p(ws["qs"]),
                                        _p(ws["ks"]), _p(ws["vs"]), _stream()), "vd_attention_fp8_quant")
     return ws
 
 
-def attention_fp8(q, k, v, batch, heads, sq, skv, d=64, scale=None, out=None):
-    """fp8 (e4m3, block-scaled MFMA) self-attention, d = 64: quantize, then attend."""
-    ws = attention_fp8_quant(q, k, v, batch, heads, sq, skv, d)
+def attention_fp8(q, k, v, batch, heads, sq, skv, d=64, scale=None, out=None, rope=None):
+    """fp8 (e4m3, block-scaled MFMA) self-attention, d = 64: quantize (optionally with the
+    spatial RoPE fused, see attention_fp8_quant), then attend."""
+    ws = attention_fp8_quant(q, k, v, batch, heads, sq, skv, d, rope=rope)
     if out is None:
         out = torch.empty(batch * sq, heads * d, device=q.device, dtype=BF16)
     _dev(out)
