@@ -169,6 +169,13 @@ int vd_temporal_attention(const void* q, const void* k, const void* v, int64_t l
                           void* o, int64_t ldo, int64_t batch, int32_t frames,
                           int64_t positions, int32_t heads, int32_t d, float scale,
                           vd_stream_t stream);
+/* vd_temporal_attention for the DiT's temporal blocks (d = 64, 17..32 frames) with the 1-D
+ * temporal RoPE (vd_rope_qk mode 1, angle by frame) applied to q/k inside the kernel as they
+ * are loaded; q and k are read un-rotated and left unchanged. */
+int vd_temporal_attention_rope(const void* q, const void* k, const void* v, int64_t ld, void* o,
+                               int64_t ldo, int64_t batch, int32_t frames, int64_t positions,
+                               int32_t heads, int32_t d, float scale, float theta,
+                               vd_stream_t stream);
 /* Test/benchmark hook: on != 0 forces the VALU temporal kernel (default: the MFMA kernel
  * for frames <= 16 and d in {40, 80, 160}). */
 int vd_temporal_force_valu(int32_t on);

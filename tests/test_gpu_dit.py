@@ -132,6 +132,33 @@ def test_temporal_attention_mfma_up_to_32_frames(cuda, F, d):
     torch.testing.assert_close(o, want, rtol=2 ** -6, atol=1e-2)
 
 
+@pytest.mark.parametrize("F", [17, 27, 32])
+def test_temporal_attention_fused_rope(cuda, F):
+    """vd_temporal_attention_rope (d = 64, 17..32 frames): the temporal RoPE applied to the Q/K
+    fragments inside the 32-frame MFMA kernel equals rope_qk (mode 1) followed by the plain
+    kernel (same fp32 rotation, same bf16 rounding), and fp32 SDPA of the oracle-rotated
+    operands; q/k rows are left un-rotated."""
+    g = torch.Generator().manual_seed(40 + F)
+    B, P, heads, d = 2, 12, 3, 64
+    D = heads * d
+    qkv = torch.randn(B * F * P, 3 * D + 8, generator=g).to(torch.bfloat16)
+    c = qkv.cuda()
+    fused = ops.temporal_attention(c[:, :D], c[:, D:2 * D], c[:, 2 * D:3 * D], B, F, P, heads, d,
+                                   rope_theta=10000.0).float().cpu()
+    assert torch.equal(c.cpu(), qkv)
+    ops.rope_qk(c, 2 * D, d, 1, F, 1, P, 10000.0)
+    two_pass = ops.temporal_attention(c[:, :D], c[:, D:2 * D], c[:, 2 * D:3 * D], B, F, P, heads, d).float().cpu()
+    torch.testing.assert_close(fused, two_pass, rtol=2 ** -7, atol=4e-3)
+    rows = B * F * P
+    z = qkv.float()[:, :2 * D].reshape(rows, 2 * heads, d)
+    zr = dit_ref.rope(z.transpose(0, 1), (torch.arange(rows) // P) % F, 10000.0).transpose(0, 1)
+    t = torch.cat([zr.reshape(rows, 2 * D), qkv.float()[:, 2 * D:3 * D]], 1)
+    t = t.reshape(B, F, P, 3, heads, d).permute(3, 0, 2, 4, 1, 5)  # qkv b p h f d
+    want = torch.nn.functional.scaled_dot_product_attention(t[0], t[1], t[2])
+    want = want.permute(0, 3, 1, 2, 4).reshape(rows, D)
+    torch.testing.assert_close(fused, want, rtol=2 ** -6, atol=1e-2)
+
+
 @pytest.mark.parametrize("t", [961, 500])
 def test_tiny_dit_matches_oracle(tiny_dit, gold, t):
     lat = torch.from_numpy(gold["latents"]).cuda()

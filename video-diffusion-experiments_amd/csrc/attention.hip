@@ -956,11 +956,17 @@ __global__ __launch_bounds__(NT) void temporal_mfma_kernel(
 // 4fq + j for j < 4 and 16 + 4fq + (j - 4) for j >= 4, and V^T's fragment takes the
 // same keys from two tr reads 16 LDS rows apart, so one 16x16x32 MFMA per d-block sums
 // all 32 keys.  The V^T fragments are read once per item and reused by both query blocks.
-template <int D>
+// ROPE (D = 64, the DiT's temporal blocks): the 1-D temporal RoPE of vd_rope_qk mode 1 is
+// applied to the Q/K fragments as they are loaded — a lane's chunk at d-step 0 (dims
+// 8fq..8fq+7) and d-step 1 (dims 32 + 8fq..) are exactly a rotate-half pair set, rotated
+// by its frame f at angle f * theta^(-2i/64) in fp32 and rounded to bf16 as dit.hip's
+// rope_kernel does — so the separate in-place RoPE pass over the Q/K rows disappears.
+template <int D, bool ROPE = false>
 __global__ __launch_bounds__(NT) void temporal_mfma32_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
     bf16_t* __restrict__ o, int64_t ldo, int64_t batch, int frames, int64_t positions, int heads,
-    float c) {
+    float c, float log2_theta) {
+  static_assert(!ROPE || D == 64, "fused temporal RoPE: d = 64 only");
   using C = TmCfg<D>;
   __shared__ __attribute__((aligned(16))) bf16_t vimg[4][32 * C::VS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -991,6 +997,50 @@ __global__ __launch_bounds__(NT) void temporal_mfma32_kernel(
     for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) s[qb][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (ROPE) {
+      uint4 kq[2][2], qq[2][2];  // [d-step][frame block]
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int f = 16 * t + fr;
+          kq[ks][t] = qq[ks][t] = make_uint4(0, 0, 0, 0);
+          if (f < frames) {
+            const int64_t rf = (row0 + (int64_t)f * positions) * ld + (int64_t)h * D + ks * 32 + 8 * fq;
+            kq[ks][t] = *(const uint4*)(k + rf);
+            qq[ks][t] = *(const uint4*)(q + rf);
+          }
+        }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float pos = (float)(16 * t + fr);
+        float ka[8], kb8[8], qa[8], qb8[8];
+        unpack8(kq[0][t], ka); unpack8(kq[1][t], kb8);
+        unpack8(qq[0][t], qa); unpack8(qq[1][t], qb8);
+        float oka[8], okb[8], oqa[8], oqb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float inv_freq = exp2f(-log2_theta * (float)(2 * (8 * fq + j)) / (float)D);
+          float sn, cs;
+          __sincosf(pos * inv_freq, &sn, &cs);
+          oka[j] = ka[j] * cs - kb8[j] * sn;
+          okb[j] = kb8[j] * cs + ka[j] * sn;
+          oqa[j] = qa[j] * cs - qb8[j] * sn;
+          oqb[j] = qb8[j] * cs + qa[j] * sn;
+        }
+        kq[0][t] = pack8(oka); kq[1][t] = pack8(okb);
+        qq[0][t] = pack8(oqa); qq[1][t] = pack8(oqb);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+            s[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kq[ks][kb]),
+                                                                __builtin_bit_cast(bf16x8, qq[ks][qb]), s[qb][kb], 0, 0,
+                                                                0);
+    } else {
 #pragma unroll
     for (int ks = 0; ks < C::KSTEPS; ++ks) {
       const int dd = ks * 32 + 8 * fq;
@@ -1011,6 +1061,7 @@ __global__ __launch_bounds__(NT) void temporal_mfma32_kernel(
         for (int kb = 0; kb < 2; ++kb)
           s[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kq[kb]),
                                                               __builtin_bit_cast(bf16x8, qq[qb]), s[qb][kb], 0, 0, 0);
+    }
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // V image written
     __builtin_amdgcn_wave_barrier();
@@ -1162,10 +1213,15 @@ extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v
       else if (d == 80) TM_LAUNCH(temporal_mfma_kernel, 80);
       else TM_LAUNCH(temporal_mfma_kernel, 160);
     } else {
-      if (d == 40) TM_LAUNCH(temporal_mfma32_kernel, 40);
-      else if (d == 64) TM_LAUNCH(temporal_mfma32_kernel, 64);
-      else if (d == 80) TM_LAUNCH(temporal_mfma32_kernel, 80);
-      else TM_LAUNCH(temporal_mfma32_kernel, 160);
+#define TM32_LAUNCH(DD)                                                                                     \
+    hipLaunchKernelGGL(temporal_mfma32_kernel<DD>, dim3(grid2), dim3(NT), 0, s, (const bf16_t*)q,           \
+                       (const bf16_t*)k, (const bf16_t*)v, ld, (bf16_t*)o, ldo, batch, frames, positions,     \
+                       heads, sl2, 0.f)
+      if (d == 40) TM32_LAUNCH(40);
+      else if (d == 64) TM32_LAUNCH(64);
+      else if (d == 80) TM32_LAUNCH(80);
+      else TM32_LAUNCH(160);
+#undef TM32_LAUNCH
     }
 #undef TM_LAUNCH
     return vd_launch_status();
@@ -1182,6 +1238,20 @@ extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v
     hipLaunchKernelGGL(temporal_attn_kernel<32>, dim3(grid), dim3(NT), 0, s, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, ld, (bf16_t*)o, ldo, batch, frames,
                        positions, heads, d, sl2);
+  return vd_launch_status();
+}
+
+extern "C" int vd_temporal_attention_rope(const void* q, const void* k, const void* v, int64_t ld, void* o,
+                                          int64_t ldo, int64_t batch, int32_t frames, int64_t positions,
+                                          int32_t heads, int32_t d, float scale, float theta,
+                                          vd_stream_t stream) {
+  VD_CHECK_ARG(q && k && v && o && al16(q) && al16(k) && al16(v) && al16(o));
+  VD_CHECK_ARG(ld % 8 == 0 && ldo % 4 == 0 && d == 64 && theta > 1.f);
+  VD_CHECK_ARG(frames >= 17 && frames <= 32 && batch > 0 && positions > 0 && heads > 0);
+  const int64_t g = (batch * positions * heads + 3) / 4;
+  hipLaunchKernelGGL((temporal_mfma32_kernel<64, true>), dim3((unsigned)(g < 8192 ? g : 8192)), dim3(NT), 0,
+                     (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld, (bf16_t*)o, ldo,
+                     batch, frames, positions, heads, scale * 1.4426950408889634f, log2f(theta));
   return vd_launch_status();
 }
 

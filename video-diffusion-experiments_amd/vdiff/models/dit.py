@@ -139,6 +139,9 @@ class DiT3DModel:
         if spatial and self.attn_fp8 and d == 64 and P % 64 == 0:
             # the spatial RoPE runs inside the fp8 quantization pass (q, k stay un-rotated)
             a = ops.attention_fp8(q, k, v, B * F, heads, P, P, d, rope=(rope[1], rope[2], theta))
+        elif not spatial and d == 64 and 17 <= F <= 32:
+            # the temporal RoPE runs inside the 32-frame MFMA kernel's Q/K loads
+            a = ops.temporal_attention(q, k, v, B, F, P, heads, d, rope_theta=theta)
         elif not spatial:
             ops.rope_qk(qkv, 2 * D, d, 1, *rope, theta)
             a = ops.temporal_attention(q, k, v, B, F, P, heads, d)

@@ -209,13 +209,20 @@ def attention(q, k, v, batch, heads, sq, skv, d, kv_div=1, scale=None, out=None)
     return out
 
 
-def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, out=None):
+def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, out=None, rope_theta=None):
+    """rope_theta: apply the temporal 1-D RoPE (rope_qk mode 1) to q/k inside the kernel
+    (vd_temporal_attention_rope: d = 64, 17..32 frames); q and k are read un-rotated."""
     _dev(q, k, v, out)
     if not (q.stride(0) == k.stride(0) == v.stride(0)):
         raise ValueError("q/k/v must share a row stride")
     if out is None:
         out = torch.empty(q.shape[0], heads * d, device=q.device, dtype=BF16)
     scale = d ** -0.5 if scale is None else scale
+    if rope_theta is not None:
+        check(lib().vd_temporal_attention_rope(_p(q), _p(k), _p(v), q.stride(0), _p(out), out.stride(0), batch,
+                                               frames, positions, heads, d, scale, rope_theta, _stream()),
+              "vd_temporal_attention_rope")
+        return out
     check(lib().vd_temporal_attention(_p(q), _p(k), _p(v), q.stride(0), _p(out), out.stride(0), batch,
                                       frames, positions, heads, d, scale, _stream()),
           "vd_temporal_attention")
