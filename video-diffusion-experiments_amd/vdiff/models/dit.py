@@ -78,6 +78,9 @@ class DiT3DModel:
         """attn_fp8: spatial self-attention on the block-scaled fp8 MFMA (vd_attention_fp8,
         d = 64, frames of a multiple of 64 tokens); text cross- and temporal attention stay bf16."""
         self.attn_fp8 = attn_fp8
+        # RoPE inside the attention kernels' Q/K loads (fp8 quantization pass, 32-frame temporal
+        # kernel); False runs the separate in-place rope_qk pass everywhere (A/B hook)
+        self.fuse_rope = True
         self.config = dict(cfg)
         self.device = torch.device(device)
         self.dtype = torch.bfloat16
@@ -136,10 +139,14 @@ class DiT3DModel:
         qkv = ops.gemm(h, blk["attn.to_qkv"][0], bias=blk["attn.to_qkv"][1])
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
         theta = self.config["rope_theta"]
-        if spatial and self.attn_fp8 and d == 64 and P % 64 == 0:
+        fp8 = spatial and self.attn_fp8 and d == 64 and P % 64 == 0
+        if fp8 and self.fuse_rope:
             # the spatial RoPE runs inside the fp8 quantization pass (q, k stay un-rotated)
             a = ops.attention_fp8(q, k, v, B * F, heads, P, P, d, rope=(rope[1], rope[2], theta))
-        elif not spatial and d == 64 and 17 <= F <= 32:
+        elif fp8:
+            ops.rope_qk(qkv, 2 * D, d, 0, *rope, theta)
+            a = ops.attention_fp8(q, k, v, B * F, heads, P, P, d)
+        elif not spatial and self.fuse_rope and d == 64 and 17 <= F <= 32:
             # the temporal RoPE runs inside the 32-frame MFMA kernel's Q/K loads
             a = ops.temporal_attention(q, k, v, B, F, P, heads, d, rope_theta=theta)
         elif not spatial:
