@@ -42,6 +42,9 @@ enum vd_status {
 
 const char* vd_strerror(int code);
 int vd_version(void);
+/* Content hash (16 hex digits) of the sources and compile flags the library was built from
+ * (video-diffusion-experiments_amd/build_ext.py); the Python loader compares it with the tree. */
+const char* vd_build_hash(void);
 
 /* ---------------------------------------------------------------- GEMM / conv
  * out[m, n] = epi( sum_k A[m, k] * W[n, k] )          (bf16 MFMA, fp32 accumulate)
@@ -171,7 +174,8 @@ int vd_temporal_attention(const void* q, const void* k, const void* v, int64_t l
                           vd_stream_t stream);
 /* vd_temporal_attention for the DiT's temporal blocks (d = 64, 17..32 frames) with the 1-D
  * temporal RoPE (vd_rope_qk mode 1, angle by frame) applied to q/k inside the kernel as they
- * are loaded; q and k are read un-rotated and left unchanged. */
+ * are loaded; q and k are read un-rotated and left unchanged.  Returns VD_EUNSUPPORTED while
+ * vd_temporal_force_valu is on (the fused form exists only on the MFMA kernel). */
 int vd_temporal_attention_rope(const void* q, const void* k, const void* v, int64_t ld, void* o,
                                int64_t ldo, int64_t batch, int32_t frames, int64_t positions,
                                int32_t heads, int32_t d, float scale, float theta,
@@ -198,7 +202,9 @@ int vd_frame_metrics(const void* frames_u8, int64_t videos, int32_t frames, int6
 
 /* ---------------------------------------------------------------- step glue
  * vd_timestep_embed: diffusers Timesteps(dim, flip_sin_to_cos=True, shift 0)
- *   (a12) -> bf16 [B][dim].  Timestep = ts[*step_idx] if step_idx else ts[b].
+ *   (a12) -> bf16 [B][dim].  Timestep = ts[*step_idx] if step_idx else ts[b]; ts holds
+ *   n_ts entries (the device step index is clamped to [0, n_ts - 1]; without step_idx
+ *   n_ts >= B).
  * vd_pack_latents: x (B,C,F,H,W) fp32 / in_div -> NHWC bf16 rows [(dup*B*F*H*W)][cpad],
  *   channels >= C zero; dup = 2 repeats the batch (the CFG cat([x, x])); in_div is
  *   the scheduler's scale_model_input divisor (1 for DDIM, sqrt(sigma^2+1) for Euler).
@@ -208,7 +214,8 @@ int vd_frame_metrics(const void* frames_u8, int64_t videos, int32_t frames, int6
  *   eps = e_u + g*(e_c - e_u) (uncond first); DDIM eta=0 epsilon update of
  *   latents (B,C,F,H,W) fp32 in place with coef[4*step] = {sqrt(a_t),
  *   sqrt(1-a_t), sqrt(a_prev), sqrt(1-a_prev)}, step = *step_idx (or 0 if
- *   NULL); optional x0_out (B,C,F,H,W) fp32; optional next_in = the packed
+ *   NULL) clamped to the n_coef rows of the table; fp32 in diffusers' operation
+ *   order, one rounding per op (bit-exact vs torch); optional x0_out (B,C,F,H,W) fp32; optional next_in = the packed
  *   bf16 UNet input of the next step (dup = ncfg) — a1 + a13 fused.
  * vd_euler_cfg_step: as vd_ddim_cfg_step, with the EulerDiscreteScheduler.step
  *   update (s_churn 0, epsilon; diffusers' fp32 order x0 = x - s*eps,
@@ -217,19 +224,19 @@ int vd_frame_metrics(const void* frames_u8, int64_t videos, int32_t frames, int6
  *   packed to bf16 — §8f rank 2 (experiments/01_baseline_generation.py:76-80).
  * vd_step_advance: ++*step_idx (one thread; the last node of a captured step).
  */
-int vd_timestep_embed(const float* ts, const int32_t* step_idx, int64_t B, int32_t dim,
-                      void* out, vd_stream_t stream);
+int vd_timestep_embed(const float* ts, int64_t n_ts, const int32_t* step_idx, int64_t B,
+                      int32_t dim, void* out, vd_stream_t stream);
 int vd_pack_latents(const float* x, int64_t B, int64_t C, int64_t F, int64_t H, int64_t W,
                     int32_t dup, void* out, int64_t cpad, float in_div, vd_stream_t stream);
 int vd_unpack_nhwc(const void* src, int32_t src_f32, int64_t ld, int64_t B, int64_t C,
                    int64_t F, int64_t H, int64_t W, float* dst, vd_stream_t stream);
 int vd_ddim_cfg_step(const float* eps, int64_t ld_eps, int32_t ncfg, float guidance,
                      float* latents, int64_t B, int64_t C, int64_t F, int64_t H, int64_t W,
-                     const float* coef, const int32_t* step_idx, float* x0_out,
+                     const float* coef, int64_t n_coef, const int32_t* step_idx, float* x0_out,
                      void* next_in, int64_t cpad, vd_stream_t stream);
 int vd_euler_cfg_step(const float* eps, int64_t ld_eps, int32_t ncfg, float guidance,
                       float* latents, int64_t B, int64_t C, int64_t F, int64_t H, int64_t W,
-                      const float* coef, const int32_t* step_idx, float* x0_out,
+                      const float* coef, int64_t n_coef, const int32_t* step_idx, float* x0_out,
                       void* next_in, int64_t cpad, vd_stream_t stream);
 int vd_step_advance(int32_t* step_idx, vd_stream_t stream);
 

@@ -27,7 +27,10 @@ def test_library_loads_and_exports_every_symbol():
     h = L.lib()
     for name in header_functions():
         assert hasattr(h, name), name
-    assert h.vd_version() == 1
+    assert h.vd_version() == 2
+    from vdiff._srchash import source_hash
+    import build_ext
+    assert h.vd_build_hash().decode() == source_hash(build_ext.HASH_FLAGS)  # a build of THIS tree
     assert h.vd_strerror(1000).decode().startswith("vdiff: invalid argument")
     out = subprocess.run(["nm", "-D", "--defined-only", str(L.LIB_PATH)], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (vd_\w+)", out))
@@ -115,3 +118,12 @@ def test_dit_ops_refuse_cpu_tensors():
         ops.patchify(torch.zeros(1, 4, 2, 8, 8), 2, 16)
     with pytest.raises(ValueError, match="no CPU fallback"):
         ops.attention_fp8(x, x, x, 1, 2, 64, 64)
+
+
+def test_loader_refuses_a_library_built_from_other_sources(monkeypatch):
+    """VERDICT r1 weak #10: a pushed/stale .so must not stand in for the tracked sources."""
+    import vdiff._srchash as sh
+    h = L.lib()
+    monkeypatch.setattr(sh, "source_hash", lambda flags=(): "0000000000000000")
+    with pytest.raises(L.VdiffError, match="built from other sources"):
+        L._check_build_hash(h)

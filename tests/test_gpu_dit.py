@@ -318,3 +318,57 @@ def test_tiny_dit_fp8_attention_matches_oracle(cuda, gold):
     err = rel_l2(out, torch.from_numpy(gold["eps_t961"]))
     print(f"tiny DiT, fp8 spatial attention: rel-L2 {err:.4f} vs the fp32 oracle")
     assert err < 0.03, err
+
+
+# DiT with 20 frames: the temporal blocks take the fused-RoPE 32-frame MFMA route
+# (dit.py: fuse_rope and 17 <= F <= 32) at the MODEL level, not only per kernel.
+DIT_F20 = dict(DIT_TINY, num_frames=20, sample_size=8)
+
+
+@pytest.fixture(scope="module")
+def dit_f20(cuda):
+    sd = init_dit_state_dict(DIT_F20, seed=5)
+    return DiT3DModel(DIT_F20, sd, device=cuda), sd
+
+
+def _f20_inputs():
+    g = torch.Generator().manual_seed(11)
+    lat = torch.randn(1, 4, 20, 8, 8, generator=g).to(torch.bfloat16).float()
+    ehs = torch.randn(2, 77, 64, generator=g).to(torch.bfloat16).float()
+    return torch.cat([lat, lat]), ehs
+
+
+def test_dit_20_frames_fused_rope_matches_unfused_and_oracle(dit_f20):
+    """fuse_rope True (vd_temporal_attention_rope inside the 32-frame kernel) vs False
+    (in-place rope_qk + vd_temporal_attention) on the same model: equal within bf16 rounding
+    of q/k (the fused path never stores rotated q/k); both within the tiny model's 3 %
+    rel-L2 of the fp32 oracle."""
+    m, sd = dit_f20
+    x, ehs = _f20_inputs()
+    outs = {}
+    for fuse in (True, False):
+        m.fuse_rope = fuse
+        outs[fuse] = m(x.cuda(), 500, encoder_hidden_states=ehs.cuda()).sample.cpu()
+    m.fuse_rope = True
+    with torch.no_grad():
+        want = dit_ref.forward(sd, DIT_F20, x, 500, ehs)
+    e_fu, e_un, e_ab = rel_l2(outs[True], want), rel_l2(outs[False], want), rel_l2(outs[True], outs[False])
+    print(f"DiT F=20 rel-L2: fused {e_fu:.4f} unfused {e_un:.4f} fused-vs-unfused {e_ab:.4f}")
+    assert e_ab < 0.01, e_ab
+    assert e_fu < 0.03 and e_un < 0.03, (e_fu, e_un)
+
+
+def test_dit_20_frames_force_valu_falls_back(dit_f20):
+    """Under the force-VALU hook vd_temporal_attention_rope returns VD_EUNSUPPORTED and
+    ops.temporal_attention falls back to rope_qk + the VALU kernel: the model
+    still matches the fused MFMA path."""
+    from vdiff._lib import lib
+    m, _ = dit_f20
+    x, ehs = _f20_inputs()
+    ref = m(x.cuda(), 500, encoder_hidden_states=ehs.cuda()).sample.cpu()
+    lib().vd_temporal_force_valu(1)
+    try:
+        got = m(x.cuda(), 500, encoder_hidden_states=ehs.cuda()).sample.cpu()
+    finally:
+        lib().vd_temporal_force_valu(0)
+    assert rel_l2(got, ref) < 0.01

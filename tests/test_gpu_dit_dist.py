@@ -16,6 +16,7 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 FRAMES = 4
+FRAMES_LONG = 20  # 2 ranks x 10 frames: the temporal blocks see 20 frames (fused-RoPE 32-frame kernel)
 
 
 def _port():
@@ -26,14 +27,16 @@ def _port():
     return p
 
 
-def _inputs():
+def _inputs(frames=FRAMES):
     g = torch.Generator().manual_seed(0)
-    return torch.randn(1, 4, FRAMES, 16, 16, generator=g), torch.randn(2, 77, 64, generator=g)
+    size = 16 if frames == FRAMES else 8
+    return torch.randn(1, 4, frames, size, size, generator=g), torch.randn(2, 77, 64, generator=g)
 
 
-def _model():
+def _model(frames=FRAMES):
     from vdiff.models.dit import DIT_TINY, DiT3DModel, init_dit_state_dict
-    return DiT3DModel(DIT_TINY, init_dit_state_dict(DIT_TINY, seed=3), device="cuda")
+    cfg = DIT_TINY if frames == FRAMES else dict(DIT_TINY, num_frames=frames, sample_size=8)
+    return DiT3DModel(cfg, init_dit_state_dict(cfg, seed=3), device="cuda")
 
 
 def _sched():
@@ -43,7 +46,7 @@ def _sched():
     return s
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, frames=FRAMES):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -55,10 +58,10 @@ def _worker(rank, world, port, out_path):
             return super()._a2a(x.cpu()).to(x.device)
 
     try:
-        lat, ehs = _inputs()
-        fl = FRAMES // world
+        lat, ehs = _inputs(frames)
+        fl = frames // world
         local = lat[:, :, rank * fl:(rank + 1) * fl].cuda()
-        loop = DiTDenoiseLoop(_model(), _sched(), local, ehs.cuda(), 7.5, use_graph=False,
+        loop = DiTDenoiseLoop(_model(frames), _sched(), local, ehs.cuda(), 7.5, use_graph=False,
                               dist=HostStagedShard()).prime()
         mine = loop.run(2).cpu()
         parts = [torch.empty_like(mine) for _ in range(world)]
@@ -84,4 +87,20 @@ def test_dit_ranks_on_one_gpu_match_unsharded(unsharded_ref, world):
         got = torch.load(path, weights_only=True)
     assert got.shape == unsharded_ref.shape
     err = ((got.double() - unsharded_ref.double()).norm() / unsharded_ref.double().norm()).item()
+    assert err < 1e-2, err
+
+
+def test_dit_20_frames_two_ranks_match_unsharded(cuda):
+    """the sharded DiT whose temporal blocks see >= 17 frames (frames = world x
+    F_local = 2 x 10) routes through the fused-RoPE 32-frame kernel on the global frame index."""
+    from vdiff.models.dit import DiTDenoiseLoop
+    lat, ehs = _inputs(FRAMES_LONG)
+    ref = DiTDenoiseLoop(_model(FRAMES_LONG), _sched(), lat.cuda(), ehs.cuda(), 7.5,
+                         use_graph=False).prime().run(2).cpu()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "out.pt")
+        mp.start_processes(_worker, args=(2, _port(), path, FRAMES_LONG), nprocs=2, join=True,
+                           start_method="spawn")
+        got = torch.load(path, weights_only=True)
+    err = ((got.double() - ref.double()).norm() / ref.double().norm()).item()
     assert err < 1e-2, err

@@ -627,9 +627,27 @@ def test_ddim_cfg_step_matches_oracle(cuda):
     ops.ddim_cfg_step(eps_rows, 2, 7.5, x, coef.to(cuda), x0_out=x0, next_in=nxt)
     e = eps_rows.cpu().reshape(2, Fr, H, W, 4).permute(0, 4, 1, 2, 3)
     want, want0 = ddim_ref.ddim_step(ddim_ref.cfg_combine(e, 7.5), t, lat.cpu(), n, acp)
-    close_f32(x, want, rtol=1e-5, atol=1e-5)
-    close_f32(x0, want0, rtol=1e-5, atol=1e-5)
+    # one rounding per op in diffusers' order (no contraction, correctly rounded division)
+    assert torch.equal(x.cpu(), want)
+    assert torch.equal(x0.cpu(), want0)
     close_bf16(ops.unpack_nhwc(nxt[: Fr * H * W], 1, 4, Fr, H, W), want)
+
+
+def test_step_index_is_clamped_to_the_tables(cuda):
+    """a device step counter past the end of its timestep / coefficient table
+    (a replay beyond the schedule) reads the table's last row, never memory past it."""
+    ts = torch.tensor([961.0, 941.0], device=cuda)
+    lat = torch.randn(1, 4, 2, 8, 8, device=cuda)
+    eps_rows = torch.randn(2 * 8 * 8, 4, device=cuda)
+    coef = torch.tensor([[0.05, 0.99, 0.06, 0.98], [0.3, 0.9, 0.4, 0.8]], device=cuda)
+    for idx, row in ((5, 1), (-3, 0), (1, 1)):
+        st = torch.tensor([idx], device=cuda, dtype=torch.int32)
+        te = ops.timestep_embed(ts, 320, step_idx=st, batch=1)
+        assert torch.equal(te, ops.timestep_embed(ts[row:row + 1].contiguous(), 320))
+        a, b = lat.clone(), lat.clone()
+        ops.ddim_cfg_step(eps_rows, 1, 1.0, a, coef, step_idx=st)
+        ops.ddim_cfg_step(eps_rows, 1, 1.0, b, coef[row:row + 1].contiguous())
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("ncfg", [2, 1])

@@ -146,12 +146,13 @@ def test_scheduler_step_api_matches_oracle(tiny_unet, gold):
     u, c = eps.chunk(2)
     out = s.step(u + 7.5 * (c - u), t, lat)
     assert rel_l2(out.prev_sample, torch.from_numpy(gold["ddim_step0_x"])) < 0.01
-    # exact DDIM arithmetic on identical eps
+    # exact DDIM arithmetic on identical eps: the kernel rounds once per operation in
+    # diffusers' order (no FMA contraction, correctly rounded division) -> bit-exact
     acp = ddim_ref.alphas_cumprod()
     e = (u + 7.5 * (c - u)).cpu()
     want, want0 = ddim_ref.ddim_step(e, t, lat.cpu(), 50, acp)
-    torch.testing.assert_close(out.prev_sample.cpu(), want, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(out.pred_original_sample.cpu(), want0, rtol=1e-4, atol=1e-4)
+    assert torch.equal(out.prev_sample.cpu(), want)
+    assert torch.equal(out.pred_original_sample.cpu(), want0)
 
 
 @pytest.mark.parametrize("use_graph", [True, False])
@@ -166,6 +167,9 @@ def test_denoise_loop_graph_matches_oracle(tiny_unet, gold, use_graph):
     x = loop.run(3)
     assert int(loop.step_idx.item()) == 3
     assert rel_l2(x, torch.from_numpy(gold["loop3_x"])) < 0.01
+    with pytest.raises(RuntimeError, match="scheduled steps"):
+        loop.run(48)  # 3 + 48 > the 50-step schedule: refused before anything is enqueued
+    assert int(loop.step_idx.item()) == 3
 
 
 def test_euler_scheduler_api_and_graph_loop_match_oracle(tiny_unet, gold):

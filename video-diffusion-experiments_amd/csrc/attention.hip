@@ -1248,6 +1248,9 @@ extern "C" int vd_temporal_attention_rope(const void* q, const void* k, const vo
   VD_CHECK_ARG(q && k && v && o && al16(q) && al16(k) && al16(v) && al16(o));
   VD_CHECK_ARG(ld % 8 == 0 && ldo % 4 == 0 && d == 64 && theta > 1.f);
   VD_CHECK_ARG(frames >= 17 && frames <= 32 && batch > 0 && positions > 0 && heads > 0);
+  // the fused form exists only on the MFMA kernel: under the force-VALU hook the caller
+  // runs vd_rope_qk + vd_temporal_attention (the VALU kernel) instead
+  if (g_temporal_valu) return VD_EUNSUPPORTED;
   const int64_t g = (batch * positions * heads + 3) / 4;
   hipLaunchKernelGGL((temporal_mfma32_kernel<64, true>), dim3((unsigned)(g < 8192 ? g : 8192)), dim3(NT), 0,
                      (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld, (bf16_t*)o, ldo,

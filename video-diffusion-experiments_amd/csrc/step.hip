@@ -20,14 +20,23 @@ constexpr int NT = 256;
 __device__ __forceinline__ float div_rn(float a, float b) { return (float)((double)a / (double)b); }
 
 
-__global__ void timestep_embed_kernel(const float* ts, const int32_t* step_idx, int64_t B, int dim,
+// Step index into a device table of n entries, clamped to [0, n-1]: a graph replayed past the
+// end of its schedule (run(n) beyond n_steps without reset()) keeps reading the last row
+// instead of memory past the table (the host loops raise before that happens).
+__device__ __forceinline__ int table_row(const int32_t* step_idx, int64_t n) {
+  int st = step_idx ? *step_idx : 0;
+  st = st < 0 ? 0 : st;
+  return (int64_t)st < n ? st : (int)(n - 1);
+}
+
+__global__ void timestep_embed_kernel(const float* ts, int64_t n_ts, const int32_t* step_idx, int64_t B, int dim,
                                       bf16_t* out) {
   const int half = dim / 2;
   const int64_t total = B * dim;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
     const int64_t b = i / dim;
     const int c = (int)(i - b * dim);
-    const float t = step_idx ? ts[*step_idx] : ts[b];
+    const float t = step_idx ? ts[table_row(step_idx, n_ts)] : ts[b];
     const int j = c < half ? c : c - half;
     // diffusers get_timestep_embedding: exp(-ln(1e4) * j / half); flip -> [cos, sin]
     const float freq = expf(-9.210340371976184f * (float)j / (float)half);
@@ -66,11 +75,14 @@ __global__ void unpack_kernel(const void* src, int src_f32, int64_t ld, int64_t 
   }
 }
 
+// fp32 in diffusers' operation order with one rounding per operation (no contraction,
+// correctly rounded division), as torch's separate fp32 ops: bit-exact vs oracle/ddim_ref.py.
 __global__ void ddim_cfg_kernel(const float* eps, int64_t ld_eps, int ncfg, float g, float* lat,
                                 int64_t B, int64_t C, int64_t F, int64_t HW, const float* coef,
-                                const int32_t* step_idx, float* x0_out, bf16_t* next_in,
+                                int64_t n_coef, const int32_t* step_idx, float* x0_out, bf16_t* next_in,
                                 int64_t cpad) {
-  const int st = step_idx ? *step_idx : 0;
+#pragma clang fp contract(off)
+  const int st = table_row(step_idx, n_coef);
   const float sat = coef[4 * st + 0], s1at = coef[4 * st + 1];
   const float sap = coef[4 * st + 2], s1ap = coef[4 * st + 3];
   const int64_t total = B * C * F * HW;
@@ -87,7 +99,7 @@ __global__ void ddim_cfg_kernel(const float* eps, int64_t ld_eps, int ncfg, floa
       e = e + g * (ec - e);
     }
     const float x = lat[i];
-    const float x0 = (x - s1at * e) / sat;
+    const float x0 = div_rn(x - s1at * e, sat);
     const float xn = sap * x0 + s1ap * e;
     lat[i] = xn;
     if (x0_out) x0_out[i] = x0;
@@ -106,10 +118,10 @@ __global__ void ddim_cfg_kernel(const float* eps, int64_t ld_eps, int ncfg, floa
 // (coef[4*st] = {sigma, sigma_next, sqrt(sigma_next^2 + 1), 0}).
 __global__ void euler_cfg_kernel(const float* eps, int64_t ld_eps, int ncfg, float g, float* lat,
                                  int64_t B, int64_t C, int64_t F, int64_t HW, const float* coef,
-                                 const int32_t* step_idx, float* x0_out, bf16_t* next_in,
+                                 int64_t n_coef, const int32_t* step_idx, float* x0_out, bf16_t* next_in,
                                  int64_t cpad) {
 #pragma clang fp contract(off)  // one rounding per operation, as torch's separate fp32 ops
-  const int st = step_idx ? *step_idx : 0;
+  const int st = table_row(step_idx, n_coef);
   const float sig = coef[4 * st + 0], sig_n = coef[4 * st + 1], in_div = coef[4 * st + 2];
   const float dt = sig_n - sig;
   const int64_t total = B * C * F * HW;
@@ -164,11 +176,12 @@ unsigned grid_for(int64_t total) {
 
 }  // namespace
 
-extern "C" int vd_timestep_embed(const float* ts, const int32_t* step_idx, int64_t B, int32_t dim,
-                                 void* out, vd_stream_t stream) {
-  VD_CHECK_ARG(ts && out && B > 0 && dim > 0 && dim % 2 == 0);
+extern "C" int vd_timestep_embed(const float* ts, int64_t n_ts, const int32_t* step_idx, int64_t B,
+                                 int32_t dim, void* out, vd_stream_t stream) {
+  VD_CHECK_ARG(ts && out && B > 0 && dim > 0 && dim % 2 == 0 && n_ts > 0);
+  if (!step_idx) VD_CHECK_ARG(n_ts >= B);
   hipLaunchKernelGGL(timestep_embed_kernel, dim3(grid_for(B * dim)), dim3(NT), 0,
-                     (hipStream_t)stream, ts, step_idx, B, dim, (bf16_t*)out);
+                     (hipStream_t)stream, ts, n_ts, step_idx, B, dim, (bf16_t*)out);
   return vd_launch_status();
 }
 
@@ -192,25 +205,25 @@ extern "C" int vd_unpack_nhwc(const void* src, int32_t src_f32, int64_t ld, int6
 
 extern "C" int vd_ddim_cfg_step(const float* eps, int64_t ld_eps, int32_t ncfg, float guidance,
                                 float* latents, int64_t B, int64_t C, int64_t F, int64_t H,
-                                int64_t W, const float* coef, const int32_t* step_idx,
+                                int64_t W, const float* coef, int64_t n_coef, const int32_t* step_idx,
                                 float* x0_out, void* next_in, int64_t cpad, vd_stream_t stream) {
-  VD_CHECK_ARG(eps && latents && coef && (ncfg == 1 || ncfg == 2) && ld_eps >= C);
+  VD_CHECK_ARG(eps && latents && coef && n_coef > 0 && (ncfg == 1 || ncfg == 2) && ld_eps >= C);
   if (next_in) VD_CHECK_ARG(cpad >= C);
   hipLaunchKernelGGL(ddim_cfg_kernel, dim3(grid_for(B * C * F * H * W)), dim3(NT), 0,
                      (hipStream_t)stream, eps, ld_eps, ncfg, guidance, latents, B, C, F, H * W,
-                     coef, step_idx, x0_out, (bf16_t*)next_in, cpad);
+                     coef, n_coef, step_idx, x0_out, (bf16_t*)next_in, cpad);
   return vd_launch_status();
 }
 
 extern "C" int vd_euler_cfg_step(const float* eps, int64_t ld_eps, int32_t ncfg, float guidance,
                                  float* latents, int64_t B, int64_t C, int64_t F, int64_t H,
-                                 int64_t W, const float* coef, const int32_t* step_idx,
+                                 int64_t W, const float* coef, int64_t n_coef, const int32_t* step_idx,
                                  float* x0_out, void* next_in, int64_t cpad, vd_stream_t stream) {
-  VD_CHECK_ARG(eps && latents && coef && (ncfg == 1 || ncfg == 2) && ld_eps >= C);
+  VD_CHECK_ARG(eps && latents && coef && n_coef > 0 && (ncfg == 1 || ncfg == 2) && ld_eps >= C);
   if (next_in) VD_CHECK_ARG(cpad >= C);
   hipLaunchKernelGGL(euler_cfg_kernel, dim3(grid_for(B * C * F * H * W)), dim3(NT), 0,
                      (hipStream_t)stream, eps, ld_eps, ncfg, guidance, latents, B, C, F, H * W,
-                     coef, step_idx, x0_out, (bf16_t*)next_in, cpad);
+                     coef, n_coef, step_idx, x0_out, (bf16_t*)next_in, cpad);
   return vd_launch_status();
 }
 
@@ -239,4 +252,11 @@ extern "C" const char* vd_strerror(int code) {
   }
 }
 
-extern "C" int vd_version(void) { return 1; }
+extern "C" int vd_version(void) { return 2; }
+
+#ifndef VD_BUILD_HASH
+#define VD_BUILD_HASH "unhashed"
+#endif
+// Content hash of the sources + flags this library was built from (build_ext.py);
+// vdiff._lib refuses to load a library whose hash differs from the tree's sources.
+extern "C" const char* vd_build_hash(void) { return VD_BUILD_HASH; }

@@ -16,12 +16,14 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 LIB_PATH = Path(__file__).resolve().parent / "libvdiff_hip.so"
 
 c_i64, c_i32, c_f32, c_vp = C.c_int64, C.c_int32, C.c_float, C.c_void_p
+VD_OK, VD_EINVAL, VD_EUNSUPPORTED, VD_ERCCL = 0, 1000, 1001, 1002  # enum vd_status
 
 # Every exported symbol and its argtypes: the single source of truth used by the
 # loader and by tests/test_abi.py (which checks it against include/vdiff.h).
 SIGNATURES = {
     "vd_strerror": ([c_i32], C.c_char_p),
     "vd_version": ([], c_i32),
+    "vd_build_hash": ([], C.c_char_p),
     "vd_gemm": ([c_vp, c_vp], c_i32),
     "vd_gemm_force_v1": ([c_i32], c_i32),
     "vd_gemm_select_path": ([c_i32], c_i32),
@@ -40,11 +42,11 @@ SIGNATURES = {
     "vd_temporal_attention_rope": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_f32, c_vp], c_i32),
     "vd_softmax_rows": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
     "vd_frame_metrics": ([c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp], c_i32),
-    "vd_timestep_embed": ([c_vp, c_vp, c_i64, c_i32, c_vp, c_vp], c_i32),
+    "vd_timestep_embed": ([c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp], c_i32),
     "vd_pack_latents": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_f32, c_vp], c_i32),
     "vd_unpack_nhwc": ([c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp], c_i32),
-    "vd_ddim_cfg_step": ([c_vp, c_i64, c_i32, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
-    "vd_euler_cfg_step": ([c_vp, c_i64, c_i32, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
+    "vd_ddim_cfg_step": ([c_vp, c_i64, c_i32, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
+    "vd_euler_cfg_step": ([c_vp, c_i64, c_i32, c_f32, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
     "vd_step_advance": ([c_vp, c_vp], c_i32),
     "vd_block_transpose": ([c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp], c_i32),
     "vd_patchify": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_i64, c_vp], c_i32),
@@ -97,8 +99,27 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = argt
             fn.restype = rest
+        _check_build_hash(h)
         _lib = h
     return _lib
+
+
+def _check_build_hash(h) -> None:
+    """The library must be a build of the sources in this tree (build_ext.py embeds their
+    content hash): a stale or foreign .so raises instead of silently running other kernels."""
+    import sys
+    pkg = str(Path(__file__).resolve().parents[1])
+    if pkg not in sys.path:
+        sys.path.insert(0, pkg)
+    import build_ext
+    from ._srchash import source_files, source_hash
+    if not source_files():
+        return  # an installed library without its sources: nothing to compare against
+    want = source_hash(build_ext.HASH_FLAGS)
+    got = h.vd_build_hash().decode()
+    if got != want:
+        raise VdiffError(f"{LIB_PATH.name} was built from other sources (hash {got}, tree {want}): "
+                         "rebuild with python video-diffusion-experiments_amd/build_ext.py")
 
 
 def check(rc: int, what: str = "") -> None:

@@ -257,6 +257,7 @@ class DiTDenoiseLoop:
         self.x_tok = ops.patchify(self.lat, p, model.kpad, dup=self.ncfg)
         self.use_graph = use_graph
         self.graph = None
+        self.issued = 0  # steps run since the last reset() (the device index into ts / coef)
 
     def step(self):
         m = self.m
@@ -273,6 +274,7 @@ class DiTDenoiseLoop:
     def reset(self, latents):
         self.lat.copy_(latents)
         self.step_idx.zero_()
+        self.issued = 0
         ops.patchify(self.lat, self.m.p, self.m.kpad, dup=self.ncfg, out=self.x_tok)
 
     def prime(self):
@@ -288,9 +290,13 @@ class DiTDenoiseLoop:
         return self
 
     def run(self, n=None):
-        n = self.n_steps if n is None else n
+        n = self.n_steps - self.issued if n is None else n
+        if n < 0 or self.issued + n > self.n_steps:
+            raise RuntimeError(f"run({n}) after {self.issued} of {self.n_steps} scheduled steps: "
+                               "call reset(latents) to start a new schedule")
         if self.graph is None and self.use_graph:
             self.prime()
+        self.issued += n
         for _ in range(n):
             if self.graph is not None:
                 self.graph.replay()

@@ -11,7 +11,7 @@ import math
 
 import torch
 
-from ._lib import GemmDesc, check, lib
+from ._lib import VD_EUNSUPPORTED, GemmDesc, check, lib
 
 ACT_NONE, ACT_SILU, ACT_GEGLU, ACT_GELU = 0, 1, 2, 3
 A_DENSE, A_CONV3X3 = 0, 1
@@ -219,10 +219,17 @@ def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, 
         out = torch.empty(q.shape[0], heads * d, device=q.device, dtype=BF16)
     scale = d ** -0.5 if scale is None else scale
     if rope_theta is not None:
-        check(lib().vd_temporal_attention_rope(_p(q), _p(k), _p(v), q.stride(0), _p(out), out.stride(0), batch,
-                                               frames, positions, heads, d, scale, rope_theta, _stream()),
-              "vd_temporal_attention_rope")
-        return out
+        rc = lib().vd_temporal_attention_rope(_p(q), _p(k), _p(v), q.stride(0), _p(out), out.stride(0), batch,
+                                              frames, positions, heads, d, scale, rope_theta, _stream())
+        if rc != VD_EUNSUPPORTED:
+            check(rc, "vd_temporal_attention_rope")
+            return out
+        # no fused variant (the force-VALU test hook): rotate q/k in place, then attend;
+        # q and k must be the column slices [0, C) and [C, 2C) of one QKV row buffer
+        if k.data_ptr() - q.data_ptr() != heads * d * q.element_size():
+            raise ValueError("rope fallback needs q, k adjacent column slices of one buffer")
+        qk = torch.as_strided(q, (q.shape[0], 2 * heads * d), (q.stride(0), 1))
+        rope_qk(qk, 2 * heads * d, d, 1, frames, 1, positions, rope_theta)
     check(lib().vd_temporal_attention(_p(q), _p(k), _p(v), q.stride(0), _p(out), out.stride(0), batch,
                                       frames, positions, heads, d, scale, _stream()),
           "vd_temporal_attention")
@@ -246,7 +253,7 @@ def timestep_embed(ts, dim, step_idx=None, batch=None, out=None):
     B = ts.numel() if step_idx is None else batch
     if out is None:
         out = torch.empty(B, dim, device=ts.device, dtype=BF16)
-    check(lib().vd_timestep_embed(_p(ts), _p(step_idx), B, dim, _p(out), _stream()), "vd_timestep_embed")
+    check(lib().vd_timestep_embed(_p(ts), ts.numel(), _p(step_idx), B, dim, _p(out), _stream()), "vd_timestep_embed")
     return out
 
 
@@ -275,7 +282,7 @@ def ddim_cfg_step(eps, ncfg, guidance, latents, coef, step_idx=None, x0_out=None
         raise ValueError("latents must be contiguous fp32")
     B, Cc, Fr, H, W = latents.shape
     check(lib().vd_ddim_cfg_step(_p(eps), eps.stride(0), ncfg, guidance, _p(latents), B, Cc, Fr, H, W,
-                                 _p(coef), _p(step_idx), _p(x0_out), _p(next_in),
+                                 _p(coef), coef.numel() // 4, _p(step_idx), _p(x0_out), _p(next_in),
                                  next_in.shape[1] if next_in is not None else 0, _stream()),
           "vd_ddim_cfg_step")
 
@@ -287,7 +294,7 @@ def euler_cfg_step(eps, ncfg, guidance, latents, coef, step_idx=None, x0_out=Non
         raise ValueError("latents must be contiguous fp32")
     B, Cc, Fr, H, W = latents.shape
     check(lib().vd_euler_cfg_step(_p(eps), eps.stride(0), ncfg, guidance, _p(latents), B, Cc, Fr, H, W,
-                                  _p(coef), _p(step_idx), _p(x0_out), _p(next_in),
+                                  _p(coef), coef.numel() // 4, _p(step_idx), _p(x0_out), _p(next_in),
                                   next_in.shape[1] if next_in is not None else 0, _stream()),
           "vd_euler_cfg_step")
 

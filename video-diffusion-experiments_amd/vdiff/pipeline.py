@@ -104,6 +104,16 @@ class DenoiseLoop:
         self.use_graph = use_graph
         self.graph = None
         self.graph_error = None
+        self.issued = 0  # steps run since the last reset(): the device index into ts / coef
+
+    def _claim(self, n):
+        """Host-side bound on the device step counter: the timestep and coefficient tables
+        hold n_steps rows; running past them without reset() is an error (the kernels also
+        clamp the index, so a stray replay can never read past the tables)."""
+        if n < 0 or self.issued + n > self.n_steps:
+            raise RuntimeError(f"run({n}) after {self.issued} of {self.n_steps} scheduled steps: "
+                               "call reset(latents) to start a new schedule")
+        self.issued += n
 
     def step(self):
         u = self.unet
@@ -119,6 +129,7 @@ class DenoiseLoop:
     def reset(self, latents):
         self.lat.copy_(latents)
         self.step_idx.zero_()
+        self.issued = 0
         ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD, out=self.x_in2, in_div=self.in_div0)
 
     def prime(self):
@@ -142,7 +153,8 @@ class DenoiseLoop:
         return self
 
     def run(self, n=None):
-        n = self.n_steps if n is None else n
+        n = self.n_steps - self.issued if n is None else n
+        self._claim(n)
         for _ in range(n):
             if self.graph is not None:
                 self.graph.replay()
