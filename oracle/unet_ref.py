@@ -21,6 +21,15 @@ All functions take a state dict keyed by diffusers parameter names and a
 diffusers-style config dict.  `rnd` is an optional hook applied to every
 activation a fused HIP kernel would store to HBM (identity for pure fp32;
 bf16 rounding to emulate the device path's storage precision).
+
+act modes of unet_forward (test instrumentation for the device's precision):
+  "fp32" — the reference semantics in fp32 (what parity is measured against);
+  "bf16" — + bf16 rounding at every point the device stores an activation;
+  "dev"  — + the device's attention arithmetic: the softmax scale d^-1/2 * log2(e)
+           folded into a bf16 copy of to_q.weight (vdiff Attention.prepare), so q is
+           stored as bf16(x W_q'^T) and scores are in log2 units, and the probabilities
+           P = 2^(s - max) rounded to bf16 before P V, with the row sum taken over the
+           same bf16 P (the flash kernels' ones-column / row-sum arithmetic).
 """
 from __future__ import annotations
 
@@ -36,7 +45,13 @@ def _bf16_round(x):
     return x.to(torch.bfloat16).to(torch.float32)
 
 
-ROUNDERS = {"fp32": _ident, "bf16": _bf16_round}
+def _bf16_dev(x):
+    return x.to(torch.bfloat16).to(torch.float32)
+
+
+_bf16_dev.device_attention = True  # marks the "dev" mode (see module docstring)
+
+ROUNDERS = {"fp32": _ident, "bf16": _bf16_round, "dev": _bf16_dev}
 
 
 # ---------------------------------------------------------------- primitives
@@ -81,16 +96,31 @@ def attention(sd, p, x, ctx, heads, rnd=_ident):
     """diffusers:Attention + AttnProcessor2_0 (App. A.5): q/k/v without bias,
     softmax(q k^T / sqrt(d)) v, to_out.0 with bias, no residual inside."""
     ctx = x if ctx is None else ctx
-    q = rnd(linear(sd, p + ".to_q", x, bias=False))
+    dev = getattr(rnd, "device_attention", False)
+    wq = sd[p + ".to_q.weight"]
+    d = wq.shape[0] // heads
+    if dev:  # vdiff Attention.prepare: bf16(W_q * d^-1/2 * log2 e); scores in log2 units
+        wq = _bf16_round(wq * (d ** -0.5 * math.log2(math.e)))
+    q = rnd(F.linear(x, wq))
     k = rnd(linear(sd, p + ".to_k", ctx, bias=False))
     v = rnd(linear(sd, p + ".to_v", ctx, bias=False))
     b, s, c = q.shape
-    d = c // heads
     q = q.view(b, s, heads, d).transpose(1, 2)
     k = k.view(b, -1, heads, d).transpose(1, 2)
     v = v.view(b, -1, heads, d).transpose(1, 2)
-    w = torch.softmax((q @ k.transpose(-1, -2)) * (d ** -0.5), dim=-1)
-    o = (w @ v).transpose(1, 2).reshape(b, s, c)
+    # batch chunks bound the score matrix to ~2^28 floats (the full config's level-1
+    # self-attention would otherwise hold 32 x 8 x 4096^2 fp32 scores = 17 GB at once)
+    step = max(1, (1 << 28) // (heads * s * k.shape[2]))
+    outs = []
+    for i in range(0, b, step):
+        qi, ki, vi = q[i:i + step], k[i:i + step], v[i:i + step]
+        if dev:
+            sc = qi @ ki.transpose(-1, -2)
+            pr = _bf16_round(torch.exp2(sc - sc.amax(-1, keepdim=True)))
+            outs.append((pr @ vi) / pr.sum(-1, keepdim=True))
+        else:
+            outs.append(torch.softmax((qi @ ki.transpose(-1, -2)) * (d ** -0.5), dim=-1) @ vi)
+    o = torch.cat(outs).transpose(1, 2).reshape(b, s, c)
     return linear(sd, p + ".to_out.0", rnd(o))
 
 

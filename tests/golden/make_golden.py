@@ -6,7 +6,9 @@ tiny_unet.npz  — BASELINE config 1: tiny UNetMotionModel,
                  synthetic weights seed 0, latents randn seed 42
                  (1,4,4,64,64), encoder_hidden_states randn seed 1 (2,77,64),
                  CFG batch cat([x, x]); oracle (fp32) eps at t in {961, 500, 1},
-                 the bf16-storage-emulated oracle eps at t=961, the CFG+DDIM
+                 the bf16-storage-emulated oracle eps at t=961, the device-emulating
+                 oracle (act="dev": bf16 storage + the kernels' folded softmax scale and
+                 bf16 probabilities) at t in {961, 500, 1}, the CFG+DDIM
                  step from t=961 (50-step schedule), and a 3-step loop result.
 ddim_tables.npz — DDIM leading timesteps and {sqrt a_t, sqrt 1-a_t, sqrt a_p,
                  sqrt 1-a_p} tables for N in {15, 25, 50}.
@@ -57,6 +59,8 @@ def main():
         for t in (961, 500, 1):
             out[f"eps_t{t}"] = unet_ref.unet_forward(sd, TINY, x_in, t, ehs).numpy()
         out["eps_t961_bf16emu"] = unet_ref.unet_forward(sd, TINY, x_in, 961, ehs, act="bf16").numpy()
+        for t in (961, 500, 1):  # the oracle emulating the device's storage + attention arithmetic
+            out[f"eps_t{t}_dev"] = unet_ref.unet_forward(sd, TINY, x_in, t, ehs, act="dev").numpy()
         acp = ddim_ref.alphas_cumprod()
         ts50 = ddim_ref.timesteps_leading(50)
         x1, x0 = ddim_ref.ddim_step(ddim_ref.cfg_combine(

@@ -31,17 +31,22 @@ def _port():
 
 
 FRAMES = 8
+FULL_FRAMES = 16  # BASELINE config 4: the full model, 16 frames sharded 2 per rank over 8 ranks
 
 
-def _inputs():
+def _inputs(cfg="tiny"):
     g = torch.Generator().manual_seed(0)
-    lat = torch.randn(1, 4, FRAMES, 64, 64, generator=g)
-    ehs = torch.randn(2, 77, 64, generator=g)
+    frames, dim = (FRAMES, 64) if cfg == "tiny" else (FULL_FRAMES, 768)
+    lat = torch.randn(1, 4, frames, 64, 64, generator=g)
+    ehs = torch.randn(2, 77, dim, generator=g)
     return lat, ehs
 
 
-def _model():
+def _model(cfg="tiny"):
     from vdiff import UNetMotionModel, init_synthetic_
+    if cfg == "full":  # GPU-seeded synthetic weights: the same values in every process
+        from vdiff.weights import materialize_synthetic
+        return materialize_synthetic("full", device="cuda", seed=0).prepare()
     return init_synthetic_(UNetMotionModel("tiny"), seed=3).to("cuda", torch.bfloat16).prepare()
 
 
@@ -52,7 +57,7 @@ def _sched():
     return s
 
 
-def _worker(rank, world, port, out_path, layout="frame"):
+def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -76,15 +81,15 @@ def _worker(rank, world, port, out_path, layout="frame"):
             return super().gather_eps(eps.cpu()).to(eps.device)
 
     try:
-        unet = _model()
-        lay = NodeLayout(layout, FRAMES, world=world, rank=rank)
+        unet = _model(cfg)
+        lay = NodeLayout(layout, FRAMES if cfg == "tiny" else FULL_FRAMES, world=world, rank=rank)
         fs = HostStagedShard(lay.frame_shard.group) if lay.frame_shard is not None else None
         cs = HostStagedCfg(lay.cfg_shard.group) if lay.cfg_shard is not None else None
         unet.dist = fs
-        lat, ehs = _inputs()
+        lat, ehs = _inputs(cfg)
         local = lat[:, :, lay.frame_slice()].cuda()
         loop = DenoiseLoop(unet, _sched(), local, ehs.cuda(), 7.5, use_graph=False, cfg_shard=cs).prime()
-        mine = loop.run(2).cpu()
+        mine = loop.run(steps).cpu()
         parts = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(parts, mine)
         if rank == 0:
@@ -116,4 +121,24 @@ def test_ranks_on_one_gpu_match_unsharded(unsharded_ref, world, layout):
         got = torch.load(path, weights_only=True)
     assert got.shape == ref.shape
     err = ((got.double() - ref.double()).norm() / ref.double().norm()).item()
+    assert err < 1e-2, err
+
+
+def test_full_model_eight_ranks_two_frames_match_unsharded(cuda):
+    """BASELINE config 4 at its real shapes: the FULL 1.31B model, 16
+    frames sharded 2 per rank over 8 ranks sharing cuda:0 (collectives staged through gloo),
+    one CFG DDIM step after prime(), against the unsharded 16-frame loop."""
+    from vdiff import DenoiseLoop
+    lat, ehs = _inputs("full")
+    ref = DenoiseLoop(_model("full"), _sched(), lat.cuda(), ehs.cuda(), 7.5,
+                      use_graph=False).prime().run(1).cpu()
+    torch.cuda.empty_cache()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "out.pt")
+        mp.start_processes(_worker, args=(8, _port(), path, "frame", "full", 1), nprocs=8, join=True,
+                           start_method="spawn")
+        got = torch.load(path, weights_only=True)
+    assert got.shape == ref.shape == (1, 4, FULL_FRAMES, 64, 64)
+    err = ((got.double() - ref.double()).norm() / ref.double().norm()).item()
+    print(f"full model 8 ranks x 2 frames vs unsharded: rel-L2 {err:.2e}")
     assert err < 1e-2, err

@@ -372,3 +372,27 @@ def test_dit_20_frames_force_valu_falls_back(dit_f20):
     finally:
         lib().vd_temporal_force_valu(0)
     assert rel_l2(got, ref) < 0.01
+
+
+def test_full_config_dit_fp8_forward(cuda):
+    """BASELINE config 5 at its full shapes: the build-defined DiT at 32
+    frames x 96x96 latents (768x768 px; 73,728 tokens per video, CFG batch 2, depth 28, hidden
+    1152, 18 heads), one forward at t = 500 with the fp8 spatial attention and with the bf16
+    one on the same weights: finite, the right shape, and fp8 within 5 % rel-L2 of bf16 (the
+    measured value is printed; e4m3 has 3 mantissa bits, the tiny model lands at 0.5 %)."""
+    from vdiff.models.dit import DIT_FULL
+    cfg = dict(DIT_FULL)
+    m = DiT3DModel(cfg, init_dit_state_dict(cfg, seed=0, device="cuda"), device=cuda, attn_fp8=True)
+    F, H = cfg["num_frames"], cfg["sample_size"]
+    g = torch.Generator().manual_seed(42)
+    lat = torch.randn(1, 4, F, H, H, generator=g).cuda()
+    ehs = torch.randn(2, 77, cfg["text_dim"], generator=g).cuda()
+    x = torch.cat([lat, lat])
+    fp8 = m(x, 500, encoder_hidden_states=ehs).sample
+    m.attn_fp8 = False
+    bf = m(x, 500, encoder_hidden_states=ehs).sample
+    assert fp8.shape == bf.shape == (2, 4, F, H, H)
+    assert torch.isfinite(fp8).all() and torch.isfinite(bf).all()
+    err = rel_l2(fp8, bf)
+    print(f"full DiT (32 f x 96^2): fp8-vs-bf16 spatial attention rel-L2 {err:.4f}")
+    assert err < 0.05, err
