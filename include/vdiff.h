@@ -246,6 +246,23 @@ int vd_step_advance(int32_t* step_idx, vd_stream_t stream);
 int vd_block_transpose(const void* src, void* dst, int64_t nb, int64_t na, int64_t nc,
                        int64_t width, vd_stream_t stream);
 
+/* ---- module-level (diffusers-layout) path: csrc/rows.hip ----
+ * Elementwise ops a caller driving the modules one by one needs between HIP GEMM / norm /
+ * attention calls (forward-hook tracing, experiments/03_trace_forward_pass.py:105-113; a
+ * direct motion_modules[i](x, num_frames=F) call, 03:182).  bf16 rows, C % 8 == 0, 16-B
+ * aligned bases, row strides in elements.
+ * vd_rows_eltwise: op 0: out[r] = (x ? x[r] : 0) + y[(r / y_div) % y_period] (y bf16, or fp32
+ *   if y_f32) — residual adds, the ResnetBlock2D time-embedding broadcast, the sinusoidal
+ *   positional embedding, repeat_interleave, channel concat into column slices;
+ *   op 1: out[r] = silu(x[r]) (nn.SiLU).
+ * vd_upsample_nearest2x: rows of n_img h x w images -> rows of their nearest x2 upsample
+ *   (Upsample2D's F.interpolate(scale_factor=2.0, mode="nearest")). */
+int vd_rows_eltwise(int32_t op, const void* x, int64_t ldx, const void* y, int64_t ldy, int32_t y_f32,
+                    int64_t y_div, int64_t y_period, int64_t rows, int64_t C, void* out, int64_t ldo,
+                    vd_stream_t stream);
+int vd_upsample_nearest2x(const void* x, int64_t ldx, int64_t n_img, int64_t h, int64_t w, int64_t C,
+                          void* out, int64_t ldo, vd_stream_t stream);
+
 /* ---- DiT-style denoiser (BASELINE config 5; build-defined model,
  * no reference counterpart — oracle/dit_ref.py is its restatement) ----
  * vd_patchify: latents fp32 (B,C,F,H,W) / in_div -> token rows bf16 [(b,f,hp,wp)][kpad],

@@ -74,7 +74,7 @@ def test_resnet_block_concat_shortcut(cuda):
     temb_all = ops.gemm(temb_silu.to("cuda", torch.bfloat16), r.time_emb_proj.weight.to(torch.bfloat16),
                         bias=r.time_emb_proj.bias.float(), out_f32=True)
     ctx = Ctx(B, Fr, temb_all, None, 77)
-    out = r(Act(to_rows(x), B * Fr, H, W), ctx, skip=Act(to_rows(s), B * Fr, H, W))
+    out = r.run(Act(to_rows(x), B * Fr, H, W), ctx, skip=Act(to_rows(s), B * Fr, H, W))
     want = unet_ref.resnet(sd, "r", torch.cat([x, s], 1), temb_silu.repeat_interleave(Fr, 0), 32)
     assert rel_l2(from_rows(out.t, B * Fr, H, W), want) < 0.025
 
@@ -89,13 +89,13 @@ def test_transformer2d_with_cross_attention(cuda):
     x = torch.randn(B * Fr, C, H, W).to(torch.bfloat16).float()
     ehs = torch.randn(B, L, D).to(torch.bfloat16).float()
     ctx = Ctx(B, Fr, None, ehs.reshape(B * L, D).to("cuda", torch.bfloat16), L)
-    out = t(Act(to_rows(x), B * Fr, H, W), ctx)
+    out = t.run(Act(to_rows(x), B * Fr, H, W), ctx)
     want = unet_ref.transformer2d(sd, "t", x, ehs.repeat_interleave(Fr, 0), heads, 32)
     got = from_rows(out.t, B * Fr, H, W)
     assert rel_l2(got, want) < 0.025
     # the cross-attention path must matter at this weight scale
     ctx2 = Ctx(B, Fr, None, torch.zeros_like(ctx.ehs_rows), L)
-    other = from_rows(t(Act(to_rows(x), B * Fr, H, W), ctx2).t, B * Fr, H, W)
+    other = from_rows(t.run(Act(to_rows(x), B * Fr, H, W), ctx2).t, B * Fr, H, W)
     assert rel_l2(other, want) > 0.05
 
 
@@ -108,7 +108,7 @@ def test_motion_module(cuda):
     prepare_tree(m)
     x = (torch.randn(B * Fr, C, H, W) + 0.5).to(torch.bfloat16).float()
     ctx = Ctx(B, Fr, None, None, 77)
-    out = m(Act(to_rows(x), B * Fr, H, W), ctx)
+    out = m.run(Act(to_rows(x), B * Fr, H, W), ctx)
     want = unet_ref.motion_module(sd, "m", x, Fr, heads, 32, 32)
     assert rel_l2(from_rows(out.t, B * Fr, H, W), want) < 0.025
 

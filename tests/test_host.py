@@ -73,3 +73,18 @@ def test_text_encoder_stub_deterministic():
     e = SyntheticTextEncoder(64)
     assert torch.equal(e("a cat"), e("a cat")) and not torch.equal(e("a cat"), e("a dog"))
     assert e("").shape == (77, 64)
+
+
+def test_prepare_latents_follows_randn_tensor_cpu_fp16():
+    """SURVEY §8a a14 / VERDICT r1: the reference draws x_T with its CPU generator
+    (05_grid_search_ablation.py:156 torch.manual_seed(42)) in the pipeline dtype float16
+    (05:35, 05:130-134) through diffusers' randn_tensor (draw on the generator's device in
+    that dtype, then move); the pipeline restates exactly that, then keeps fp32."""
+    import torch
+    from vdiff import AnimateDiffPipeline, UNetMotionModel
+    with torch.device("meta"):
+        unet = UNetMotionModel("tiny")
+    pipe = AnimateDiffPipeline(unet.to_empty(device="cpu"))
+    x = pipe.prepare_latents(1, 16, 64, 64, generator=torch.manual_seed(42))
+    want = torch.randn((1, 4, 16, 64, 64), generator=torch.manual_seed(42), dtype=torch.float16)
+    assert x.dtype == torch.float32 and torch.equal(x, want.float())

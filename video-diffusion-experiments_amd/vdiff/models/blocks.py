@@ -2,30 +2,37 @@
 down/mid/up blocks of diffusers' UNetMotionModel,
 re-expressed over NHWC row activations and the HIP kernels of vdiff.ops.
 
-Fusions relative to the diffusers op sequence (same math):
-  * GroupNorm + SiLU in one apply pass; statistics in a split/finalize pair;
-  * the time-embedding broadcast add, the conv bias and the residual add are
-    GEMM epilogues of the convolution that produces them;
-  * up-block skip concatenation is read from both sources by GN and the conv
-    loaders (never materialised);
-  * Attention q/k/v are one fused GEMM; GEGLU is a GEMM epilogue; every
-    residual add (attention out, FF out, proj_out) is a GEMM epilogue;
-  * motion modules attend over frames directly on the NHWC rows (no permute).
+Every block has two entry points over the same kernels (see layers.py):
+  * `run(...)` — the fused fast path on `Act` rows.  Fusions relative to the diffusers
+    op sequence (same math): GroupNorm + SiLU in one apply pass; the time-embedding
+    broadcast add, the conv bias and the residual add are GEMM epilogues; up-block skip
+    concatenation is read from both sources by GN and the conv loaders (never
+    materialised); Attention q/k/v are one fused GEMM with the softmax scale folded into
+    q; GEGLU is a GEMM epilogue; every residual add (attention out, FF out, proj_out) is
+    a GEMM epilogue; motion modules attend over frames directly on the NHWC rows.
+  * `forward(...)` — diffusers' signature and control flow, module by module through
+    `__call__` (so forward hooks fire with the diffusers tensor shapes: spatial tokens
+    (B*F, H*W, C), temporal tokens (B*H*W, F, C) — experiments/03_trace_forward_pass.py:
+    160-169), each leaf on its HIP kernel.
 """
 from __future__ import annotations
 
+from collections import namedtuple
 from typing import Optional
 
 import torch
 import torch.nn as nn
 
 from .. import ops
-from .layers import (Act, Attention, Downsample2D, FeedForward, SinusoidalPositionalEmbedding,
-                     Upsample2D, bf, f32, pack_conv3x3)
+from .layers import (Act, Attention, Conv2d, Downsample2D, Dropout, FeedForward, GroupNorm, LayerNorm,
+                     Linear, SiLU, SinusoidalPositionalEmbedding, Upsample2D, add, bf, f32, fmap_rows,
+                     rows_fmap, token_rows)
+
+Transformer2DModelOutput = namedtuple("Transformer2DModelOutput", ["sample"])
 
 
 class Ctx:
-    """Per-forward state shared by every block."""
+    """Per-forward state shared by every block (fast path)."""
 
     def __init__(self, batch, frames, temb_all, ehs_rows, ctx_len, dist=None, kv_cache=None):
         self.batch = batch            # videos in this forward (2 with CFG)
@@ -37,45 +44,60 @@ class Ctx:
         self.kv_cache = kv_cache      # {id(attn): kv rows} or None
 
 
+def concat_channels(a, b):
+    """torch.cat([a, b], dim=1) of two channels-last feature maps (module path)."""
+    n, ca, h, w = a.shape
+    cb = b.shape[1]
+    out = torch.empty(n * h * w, ca + cb, device=a.device, dtype=torch.bfloat16)
+    ops.rows_add(None, fmap_rows(a), out=out[:, :ca])
+    ops.rows_add(None, fmap_rows(b), out=out[:, ca:])
+    return rows_fmap(out, (n, ca + cb, h, w))
+
+
 class ResnetBlock2D(nn.Module):
     def __init__(self, in_channels, out_channels, temb_channels, groups=32, eps=1e-5):
         super().__init__()
         self.in_channels, self.out_channels = in_channels, out_channels
         self.groups, self.eps = groups, eps
-        self.norm1 = nn.GroupNorm(groups, in_channels, eps=eps, affine=True)
-        self.conv1 = nn.Conv2d(in_channels, out_channels, 3, padding=1)
-        self.time_emb_proj = nn.Linear(temb_channels, out_channels)
-        self.norm2 = nn.GroupNorm(groups, out_channels, eps=eps, affine=True)
-        self.dropout = nn.Dropout(0.0)
-        self.conv2 = nn.Conv2d(out_channels, out_channels, 3, padding=1)
-        self.nonlinearity = nn.SiLU()
-        self.conv_shortcut = (nn.Conv2d(in_channels, out_channels, 1) if in_channels != out_channels
+        self.norm1 = GroupNorm(groups, in_channels, eps=eps, affine=True)
+        self.conv1 = Conv2d(in_channels, out_channels, 3, padding=1)
+        self.time_emb_proj = Linear(temb_channels, out_channels)
+        self.norm2 = GroupNorm(groups, out_channels, eps=eps, affine=True)
+        self.dropout = Dropout(0.0)
+        self.conv2 = Conv2d(out_channels, out_channels, 3, padding=1)
+        self.nonlinearity = SiLU()
+        self.conv_shortcut = (Conv2d(in_channels, out_channels, 1) if in_channels != out_channels
                               else None)
         self.temb_offset = 0  # column offset into Ctx.temb_all, set by UNetMotionModel.prepare
 
-    def prepare(self):
-        self._g1, self._b1 = f32(self.norm1.weight), f32(self.norm1.bias)
-        self._g2, self._b2 = f32(self.norm2.weight), f32(self.norm2.bias)
-        self._w1, self._c1 = pack_conv3x3(self.conv1.weight), f32(self.conv1.bias)
-        self._w2, self._c2 = pack_conv3x3(self.conv2.weight), f32(self.conv2.bias)
-        if self.conv_shortcut is not None:
-            self._ws = bf(self.conv_shortcut.weight.reshape(self.out_channels, self.in_channels))
-            self._bs = f32(self.conv_shortcut.bias)
-
-    def forward(self, x: Act, ctx: Ctx, skip: Optional[Act] = None) -> Act:
+    def run(self, x: Act, ctx: Ctx, skip: Optional[Act] = None) -> Act:
         hw = x.h * x.w
         x1 = skip.t if skip is not None else None
-        h = ops.group_norm(x.t, x.n, hw, self.groups, self.eps, self._g1, self._b1, silu=True, x1=x1)
+        n1, n2 = self.norm1, self.norm2
+        h = ops.group_norm(x.t, x.n, hw, self.groups, self.eps, n1._g, n1._b, silu=True, x1=x1)
         rb = ctx.temb_all[:, self.temb_offset:self.temb_offset + self.out_channels]
-        h, _, _ = ops.conv3x3(h, x.n, x.h, x.w, self._w1, bias=self._c1, rowbias=rb,
+        h, _, _ = ops.conv3x3(h, x.n, x.h, x.w, self.conv1._w, bias=self.conv1._b, rowbias=rb,
                               rb_div=ctx.frames * hw)
-        h = ops.group_norm(h, x.n, hw, self.groups, self.eps, self._g2, self._b2, silu=True)
+        h = ops.group_norm(h, x.n, hw, self.groups, self.eps, n2._g, n2._b, silu=True)
         if self.conv_shortcut is not None:
-            sc = ops.gemm(x.t, self._ws, a1=x1, bias=self._bs)
+            sc = ops.gemm(x.t, self.conv_shortcut._w, a1=x1, bias=self.conv_shortcut._b)
         else:
             sc = x.t
-        out, _, _ = ops.conv3x3(h, x.n, x.h, x.w, self._w2, bias=self._c2, res=sc)
+        out, _, _ = ops.conv3x3(h, x.n, x.h, x.w, self.conv2._w, bias=self.conv2._b, res=sc)
         return Act(out, x.n, x.h, x.w)
+
+    def forward(self, input_tensor, temb, *args, **kwargs):
+        """diffusers ResnetBlock2D.forward (output_scale_factor 1, pre-norm, time_embedding_norm
+        "default"): temb (B*F, temb_channels) is broadcast over each image's pixels."""
+        h = self.nonlinearity(self.norm1(input_tensor))
+        h = self.conv1(h)
+        t = self.time_emb_proj(self.nonlinearity(temb))               # (B*F, Cout)
+        n, c, hh, ww = h.shape
+        h = rows_fmap(ops.rows_add(fmap_rows(h), token_rows(t), y_div=hh * ww), tuple(h.shape))
+        h = self.dropout(self.nonlinearity(self.norm2(h)))
+        h = self.conv2(h)
+        sc = self.conv_shortcut(input_tensor) if self.conv_shortcut is not None else input_tensor
+        return add(sc, h)
 
 
 class BasicTransformerBlock(nn.Module):
@@ -85,32 +107,30 @@ class BasicTransformerBlock(nn.Module):
                  positional_embeddings=None, num_positional_embeddings=None):
         super().__init__()
         self.heads, self.dim_head = heads, dim_head
-        self.norm1 = nn.LayerNorm(dim, eps=1e-5)
+        self.norm1 = LayerNorm(dim, eps=1e-5)
         self.attn1 = Attention(dim, heads, dim_head)
-        self.norm2 = nn.LayerNorm(dim, eps=1e-5)
+        self.norm2 = LayerNorm(dim, eps=1e-5)
         self.attn2 = Attention(dim, heads, dim_head,
                                cross_attention_dim=None if double_self_attention else cross_attention_dim)
-        self.norm3 = nn.LayerNorm(dim, eps=1e-5)
+        self.norm3 = LayerNorm(dim, eps=1e-5)
         self.ff = FeedForward(dim)
         self.pos_embed = (SinusoidalPositionalEmbedding(dim, num_positional_embeddings)
                           if positional_embeddings == "sinusoidal" else None)
 
-    def prepare(self):
-        for n in ("norm1", "norm2", "norm3"):
-            m = getattr(self, n)
-            setattr(self, "_" + n, (f32(m.weight), f32(m.bias)))
-        self._pe = f32(self.pos_embed.pe[0]) if self.pos_embed is not None else None
+    def _nrm(self, i):
+        m = getattr(self, f"norm{i}")
+        return m._g, m._b
 
     # spatial: tokens are (image, pixel) rows
-    def forward_spatial(self, h, n_img, hw, ctx: Ctx):
+    def run_spatial(self, h, n_img, hw, ctx: Ctx):
         C = h.shape[1]
         d = self.dim_head
-        n = ops.layer_norm(h, *self._norm1)
+        n = ops.layer_norm(h, *self._nrm(1))
         qkv = ops.gemm(n, self.attn1._wqkv)
         a = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], n_img, self.heads, hw, hw, d,
                           scale=self.attn1.attn_scale)
         h = ops.gemm(a, self.attn1._wo, bias=self.attn1._bo, res=h)
-        n = ops.layer_norm(h, *self._norm2)
+        n = ops.layer_norm(h, *self._nrm(2))
         q = ops.gemm(n, self.attn2._wq)
         kv = None if ctx.kv_cache is None else ctx.kv_cache.get(id(self.attn2))
         if kv is None:
@@ -120,21 +140,37 @@ class BasicTransformerBlock(nn.Module):
         a = ops.attention(q, kv[:, :C], kv[:, C:], n_img, self.heads, hw, ctx.ctx_len, d,
                           kv_div=ctx.frames, scale=self.attn2.attn_scale)
         h = ops.gemm(a, self.attn2._wo, bias=self.attn2._bo, res=h)
-        n = ops.layer_norm(h, *self._norm3)
+        n = ops.layer_norm(h, *self._nrm(3))
         return self.ff.forward_rows(n, h)
 
     # temporal: tokens are (video, frame, position) rows; attention over frames
-    def forward_temporal(self, h, batch, frames, positions):
+    def run_temporal(self, h, batch, frames, positions):
         C = h.shape[1]
         d = self.dim_head
-        for attn, nrm in ((self.attn1, self._norm1), (self.attn2, self._norm2)):
-            n = ops.layer_norm(h, *nrm, pe=self._pe, pe_div=positions, pe_period=frames)
+        pe = self.pos_embed._pe
+        for attn, i in ((self.attn1, 1), (self.attn2, 2)):
+            n = ops.layer_norm(h, *self._nrm(i), pe=pe, pe_div=positions, pe_period=frames)
             qkv = ops.gemm(n, attn._wqkv)
             a = ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch, frames,
                                        positions, self.heads, d, scale=attn.attn_scale)
             h = ops.gemm(a, attn._wo, bias=attn._bo, res=h)
-        n = ops.layer_norm(h, *self._norm3)
+        n = ops.layer_norm(h, *self._nrm(3))
         return self.ff.forward_rows(n, h)
+
+    def forward(self, hidden_states, attention_mask=None, encoder_hidden_states=None,
+                encoder_attention_mask=None, timestep=None, cross_attention_kwargs=None,
+                class_labels=None, added_cond_kwargs=None):
+        """diffusers BasicTransformerBlock.forward over (N, S, C) tokens."""
+        n = self.norm1(hidden_states)
+        if self.pos_embed is not None:
+            n = self.pos_embed(n)
+        h = add(self.attn1(n, attention_mask=attention_mask), hidden_states)
+        n = self.norm2(h)
+        if self.pos_embed is not None:
+            n = self.pos_embed(n)
+        ctx = encoder_hidden_states if self.attn2.is_cross else None
+        h = add(self.attn2(n, encoder_hidden_states=ctx), h)
+        return add(self.ff(self.norm3(h)), h)
 
 
 class Transformer2DModel(nn.Module):
@@ -144,24 +180,32 @@ class Transformer2DModel(nn.Module):
         super().__init__()
         inner = heads * dim_head
         self.groups = groups
-        self.norm = nn.GroupNorm(groups, in_channels, eps=1e-6, affine=True)
-        self.proj_in = nn.Conv2d(in_channels, inner, 1)
+        self.norm = GroupNorm(groups, in_channels, eps=1e-6, affine=True)
+        self.proj_in = Conv2d(in_channels, inner, 1)
         self.transformer_blocks = nn.ModuleList(
             [BasicTransformerBlock(inner, heads, dim_head, cross_attention_dim=cross_attention_dim)])
-        self.proj_out = nn.Conv2d(inner, in_channels, 1)
+        self.proj_out = Conv2d(inner, in_channels, 1)
 
-    def prepare(self):
-        self._g, self._b = f32(self.norm.weight), f32(self.norm.bias)
-        self._wi, self._bi = bf(self.proj_in.weight.flatten(1)), f32(self.proj_in.bias)
-        self._wo, self._bo = bf(self.proj_out.weight.flatten(1)), f32(self.proj_out.bias)
-
-    def forward(self, x: Act, ctx: Ctx) -> Act:
+    def run(self, x: Act, ctx: Ctx) -> Act:
         hw = x.h * x.w
-        hn = ops.group_norm(x.t, x.n, hw, self.groups, 1e-6, self._g, self._b)
-        h = ops.gemm(hn, self._wi, bias=self._bi)
-        h = self.transformer_blocks[0].forward_spatial(h, x.n, hw, ctx)
-        out = ops.gemm(h, self._wo, bias=self._bo, res=x.t)
+        hn = ops.group_norm(x.t, x.n, hw, self.groups, 1e-6, self.norm._g, self.norm._b)
+        h = ops.gemm(hn, self.proj_in._w, bias=self.proj_in._b)
+        h = self.transformer_blocks[0].run_spatial(h, x.n, hw, ctx)
+        out = ops.gemm(h, self.proj_out._w, bias=self.proj_out._b, res=x.t)
         return Act(out, x.n, x.h, x.w)
+
+    def forward(self, hidden_states, encoder_hidden_states=None, timestep=None, added_cond_kwargs=None,
+                class_labels=None, cross_attention_kwargs=None, attention_mask=None,
+                encoder_attention_mask=None, return_dict: bool = True):
+        n, c, hh, ww = hidden_states.shape
+        h = self.proj_in(self.norm(hidden_states))
+        tok = fmap_rows(h).view(n, hh * ww, -1)          # permute(0,2,3,1).reshape(n, hw, c): a view
+        for blk in self.transformer_blocks:
+            tok = blk(tok, encoder_hidden_states=encoder_hidden_states, timestep=timestep,
+                      cross_attention_kwargs=cross_attention_kwargs, class_labels=class_labels)
+        h = self.proj_out(rows_fmap(token_rows(tok), (n, tok.shape[-1], hh, ww)))
+        out = add(h, hidden_states)
+        return Transformer2DModelOutput(out) if return_dict else (out,)
 
 
 class AnimateDiffTransformer3D(nn.Module):
@@ -172,34 +216,58 @@ class AnimateDiffTransformer3D(nn.Module):
         super().__init__()
         inner = heads * dim_head
         self.groups = groups
-        self.norm = nn.GroupNorm(groups, in_channels, eps=1e-6, affine=True)
-        self.proj_in = nn.Linear(in_channels, inner)
+        self.norm = GroupNorm(groups, in_channels, eps=1e-6, affine=True)
+        self.proj_in = Linear(in_channels, inner)
         self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(
             inner, heads, dim_head, double_self_attention=True, positional_embeddings="sinusoidal",
             num_positional_embeddings=max_seq_length)])
-        self.proj_out = nn.Linear(inner, in_channels)
+        self.proj_out = Linear(inner, in_channels)
 
-    def prepare(self):
-        self._g, self._b = f32(self.norm.weight), f32(self.norm.bias)
-        self._wi, self._bi = bf(self.proj_in.weight), f32(self.proj_in.bias)
-        self._wo, self._bo = bf(self.proj_out.weight), f32(self.proj_out.bias)
-
-    def forward(self, x: Act, ctx: Ctx) -> Act:
+    def run(self, x: Act, ctx: Ctx) -> Act:
         hw = x.h * x.w
         B, Fl = ctx.batch, ctx.frames
         dist = ctx.dist
         gather = dist.gather_gn_partials if dist is not None else None
-        hn = ops.group_norm(x.t, B, Fl * hw, self.groups, 1e-6, self._g, self._b, gather=gather, two_pass=False)
-        h = ops.gemm(hn, self._wi, bias=self._bi)
+        hn = ops.group_norm(x.t, B, Fl * hw, self.groups, 1e-6, self.norm._g, self.norm._b, gather=gather,
+                            two_pass=False)
+        h = ops.gemm(hn, self.proj_in._w, bias=self.proj_in._b)
         blk = self.transformer_blocks[0]
         if dist is None:
-            h = blk.forward_temporal(h, B, Fl, hw)
+            h = blk.run_temporal(h, B, Fl, hw)
         else:
             hp = dist.to_position_shards(h, B, Fl, hw, ops.block_transpose)
-            hp = blk.forward_temporal(hp, B, Fl * dist.world, hw // dist.world)
+            hp = blk.run_temporal(hp, B, Fl * dist.world, hw // dist.world)
             h = dist.to_frame_shards(hp, B, Fl, hw, ops.block_transpose)
-        out = ops.gemm(h, self._wo, bias=self._bo, res=x.t)
+        out = ops.gemm(h, self.proj_out._w, bias=self.proj_out._b, res=x.t)
         return Act(out, x.n, x.h, x.w)
+
+    def forward(self, hidden_states, encoder_hidden_states=None, timestep=None, class_labels=None,
+                num_frames: int = 1, cross_attention_kwargs=None):
+        """diffusers AnimateDiffTransformer3D.forward: hidden_states (B*F, C, H, W) with
+        num_frames = F (experiments/03_trace_forward_pass.py:182 calls it this way)."""
+        if hidden_states.dim() != 4:
+            raise ValueError(f"expected (batch*frames, C, H, W) with num_frames=F, got shape "
+                             f"{tuple(hidden_states.shape)} (the diffusers calling convention)")
+        bf_, c, hh, ww = hidden_states.shape
+        if bf_ % num_frames:
+            raise ValueError(f"batch*frames {bf_} is not a multiple of num_frames={num_frames}")
+        b = bf_ // num_frames
+        hw = hh * ww
+        x5 = hidden_states.reshape(b, num_frames, c, hh, ww).permute(0, 2, 1, 3, 4)   # (B, C, F, H, W)
+        hn = fmap_rows(self.norm(x5))                                                # rows (b, f, p)
+        tok = torch.empty_like(hn)
+        for i in range(b):  # permute(0,3,4,2,1): rows (b, f, p) -> tokens (b, p, f)
+            ops.block_transpose(hn[i * num_frames * hw:(i + 1) * num_frames * hw], num_frames, hw, 1,
+                                out=tok[i * num_frames * hw:(i + 1) * num_frames * hw])
+        h = self.proj_in(tok.view(b * hw, num_frames, c))
+        for blk in self.transformer_blocks:
+            h = blk(h, encoder_hidden_states=encoder_hidden_states, timestep=timestep)
+        h = token_rows(self.proj_out(h))
+        back = torch.empty_like(h)
+        for i in range(b):  # tokens (b, p, f) -> rows (b, f, p)
+            ops.block_transpose(h[i * num_frames * hw:(i + 1) * num_frames * hw], hw, num_frames, 1,
+                                out=back[i * num_frames * hw:(i + 1) * num_frames * hw])
+        return add(rows_fmap(back, (bf_, c, hh, ww)), hidden_states)
 
 
 class _MotionBlockBase(nn.Module):
@@ -208,12 +276,26 @@ class _MotionBlockBase(nn.Module):
         attns = getattr(self, "attentions", None)
         for i, res in enumerate(self.resnets):
             skip = skips_in.pop() if skips_in is not None else None
-            x = res(x, ctx, skip=skip)
+            x = res.run(x, ctx, skip=skip)
             if attns is not None:
-                x = attns[i](x, ctx)
-            x = self.motion_modules[i](x, ctx)
+                x = attns[i].run(x, ctx)
+            x = self.motion_modules[i].run(x, ctx)
             outs.append(x)
         return x, outs
+
+    def _forward_layers(self, h, temb, ehs, num_frames, res_tuple=None):
+        attns = getattr(self, "attentions", None)
+        outs = ()
+        for i, res in enumerate(self.resnets):
+            if res_tuple is not None:
+                h = concat_channels(h, res_tuple[-1])
+                res_tuple = res_tuple[:-1]
+            h = res(h, temb)
+            if attns is not None:
+                h = attns[i](h, encoder_hidden_states=ehs, return_dict=False)[0]
+            h = self.motion_modules[i](h, num_frames=num_frames)
+            outs = outs + (h,)
+        return h, outs
 
 
 class CrossAttnDownBlockMotion(_MotionBlockBase):
@@ -230,12 +312,22 @@ class CrossAttnDownBlockMotion(_MotionBlockBase):
         self.downsamplers = (nn.ModuleList([Downsample2D(out_channels, out_channels)])
                              if add_downsample else None)
 
-    def forward(self, x, ctx):
+    def run(self, x, ctx):
         x, outs = self._run_layers(x, ctx)
         if self.downsamplers is not None:
-            x = self.downsamplers[0](x)
+            x = self.downsamplers[0].run(x)
             outs.append(x)
         return x, outs
+
+    def forward(self, hidden_states, temb=None, encoder_hidden_states=None, attention_mask=None,
+                num_frames: int = 1, encoder_attention_mask=None, cross_attention_kwargs=None,
+                additional_residuals=None):
+        h, outs = self._forward_layers(hidden_states, temb, encoder_hidden_states, num_frames)
+        if self.downsamplers is not None:
+            for d in self.downsamplers:
+                h = d(h)
+            outs = outs + (h,)
+        return h, outs
 
 
 class DownBlockMotion(CrossAttnDownBlockMotion):
@@ -249,6 +341,9 @@ class DownBlockMotion(CrossAttnDownBlockMotion):
             for _ in range(num_layers)])
         self.downsamplers = (nn.ModuleList([Downsample2D(out_channels, out_channels)])
                              if add_downsample else None)
+
+    def forward(self, hidden_states, temb=None, num_frames: int = 1, *args, **kwargs):
+        return super().forward(hidden_states, temb, None, num_frames=num_frames)
 
 
 class CrossAttnUpBlockMotion(_MotionBlockBase):
@@ -267,11 +362,21 @@ class CrossAttnUpBlockMotion(_MotionBlockBase):
         self.upsamplers = (nn.ModuleList([Upsample2D(out_channels, out_channels)])
                            if add_upsample else None)
 
-    def forward(self, x, ctx, skips):
+    def run(self, x, ctx, skips):
         x, _ = self._run_layers(x, ctx, skips_in=skips)
         if self.upsamplers is not None:
-            x = self.upsamplers[0](x)
+            x = self.upsamplers[0].run(x)
         return x
+
+    def forward(self, hidden_states, res_hidden_states_tuple, temb=None, encoder_hidden_states=None,
+                cross_attention_kwargs=None, upsample_size=None, attention_mask=None,
+                encoder_attention_mask=None, num_frames: int = 1):
+        h, _ = self._forward_layers(hidden_states, temb, encoder_hidden_states, num_frames,
+                                    res_tuple=tuple(res_hidden_states_tuple))
+        if self.upsamplers is not None:
+            for u in self.upsamplers:
+                h = u(h)
+        return h
 
 
 class UpBlockMotion(CrossAttnUpBlockMotion):
@@ -279,6 +384,10 @@ class UpBlockMotion(CrossAttnUpBlockMotion):
                  eps, max_seq_length):
         super().__init__(resnet_in, out_channels, temb_channels, None, None, motion_heads, add_upsample,
                          groups, eps, max_seq_length, with_attn=False)
+
+    def forward(self, hidden_states, res_hidden_states_tuple, temb=None, upsample_size=None,
+                num_frames: int = 1, *args, **kwargs):
+        return super().forward(hidden_states, res_hidden_states_tuple, temb, None, num_frames=num_frames)
 
 
 class UNetMidBlockCrossAttnMotion(nn.Module):
@@ -293,9 +402,17 @@ class UNetMidBlockCrossAttnMotion(nn.Module):
             motion_heads, channels // motion_heads, channels, groups, max_seq_length)])
             if use_motion else None)
 
-    def forward(self, x, ctx):
-        x = self.resnets[0](x, ctx)
-        x = self.attentions[0](x, ctx)
+    def run(self, x, ctx):
+        x = self.resnets[0].run(x, ctx)
+        x = self.attentions[0].run(x, ctx)
         if self.motion_modules is not None:
-            x = self.motion_modules[0](x, ctx)
-        return self.resnets[1](x, ctx)
+            x = self.motion_modules[0].run(x, ctx)
+        return self.resnets[1].run(x, ctx)
+
+    def forward(self, hidden_states, temb=None, encoder_hidden_states=None, attention_mask=None,
+                cross_attention_kwargs=None, encoder_attention_mask=None, num_frames: int = 1):
+        h = self.resnets[0](hidden_states, temb)
+        h = self.attentions[0](h, encoder_hidden_states=encoder_hidden_states, return_dict=False)[0]
+        if self.motion_modules is not None:
+            h = self.motion_modules[0](h, num_frames=num_frames)
+        return self.resnets[1](h, temb)

@@ -3,11 +3,20 @@ diffusers' so the reference's inspection tooling (experiments/02_architecture_
 inspection.py:51-60, experiments/03_trace_forward_pass.py:134-139) and
 diffusers-keyed state dicts work unchanged.
 
-Parameters live in the standard torch containers (nn.Linear, nn.Conv2d, ...);
-`prepare()` derives the packed device operands the HIP kernels consume
-(conv weights [Cout][3][3][Cin], fused QKV, GEGLU row interleave, fp32
-biases/affines).  The forward passes run over NHWC row activations (see
-`Act`) and call vdiff.ops only.
+Two ways through every module, one set of kernels:
+
+* the fused fast path (`run` methods, NHWC row activations `Act`, epilogue fusions) —
+  what the denoising loop and `UNetMotionModel.forward` use;
+* the module path (`forward` / `__call__`, diffusers' signatures and tensor layouts:
+  (B*F, C, H, W) feature maps as channels-last views of the same rows, (N, S, C) token
+  tensors) — what runs when a caller drives modules one by one: a direct
+  `motion_modules[i](x, num_frames=F)` (03:182) or a forward-hook trace of the whole
+  UNet (utils/forward_tracer.py:177-206), whose hooks then see the diffusers shapes.
+
+The leaf classes below subclass torch's (same class names, same parameters) and only
+replace `forward` with the HIP kernels of vdiff.ops; `prepare()` derives the packed
+device operands (conv weights [Cout][3][3][Cin], fused QKV, GEGLU row interleave, fp32
+biases/affines) that both paths share.
 """
 from __future__ import annotations
 
@@ -72,6 +81,141 @@ def pack_geglu(w: torch.Tensor) -> torch.Tensor:
     return torch.stack([h.reshape(shp), g.reshape(shp)], 1).reshape(w.shape).contiguous()
 
 
+# ------------------------------------------------------------------ layout helpers
+def to_bf16_cuda(x: torch.Tensor) -> torch.Tensor:
+    if not x.is_cuda:
+        raise ValueError("vdiff modules run on the GPU only (got a CPU tensor); no CPU fallback")
+    return x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
+
+
+def fmap_rows(x: torch.Tensor):
+    """(N, C, H, W) or (B, C, F, H, W) feature map -> its NHWC rows [(..., y, x), C] (a view
+    when x is channels-last, e.g. every map the module path produces)."""
+    x = to_bf16_cuda(x)
+    perm = (0, 2, 3, 1) if x.dim() == 4 else (0, 2, 3, 4, 1)
+    xp = x.permute(*perm)
+    if not xp.is_contiguous():
+        xp = xp.contiguous()
+    return xp.reshape(-1, x.shape[1])
+
+
+def rows_fmap(rows: torch.Tensor, shape) -> torch.Tensor:
+    """NHWC rows -> a channels-last view of shape (N, C, H, W) or (B, C, F, H, W)."""
+    C = shape[1]
+    if len(shape) == 4:
+        n, _, h, w = shape
+        return rows.view(n, h, w, C).permute(0, 3, 1, 2)
+    b, _, f, h, w = shape
+    return rows.view(b, f, h, w, C).permute(0, 4, 1, 2, 3)
+
+
+def token_rows(x: torch.Tensor) -> torch.Tensor:
+    """(..., C) token tensor -> contiguous 2-D rows (a view when already contiguous)."""
+    x = to_bf16_cuda(x)
+    return (x if x.is_contiguous() else x.contiguous()).reshape(-1, x.shape[-1])
+
+
+def any_rows(x: torch.Tensor):
+    """Rows and an inverse for the layouts the module path passes around: token tensors
+    (..., C) and channels-last feature maps (N, C, H, W) / (B, C, F, H, W)."""
+    if x.dim() in (4, 5):
+        return fmap_rows(x), (lambda r, s=tuple(x.shape): rows_fmap(r, s))
+    return token_rows(x), (lambda r, s=tuple(x.shape): r.view(s))
+
+
+def add(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a + b of two equally shaped module-path tensors (the residual adds of diffusers' forwards)."""
+    ra, back = any_rows(a)
+    rb, _ = any_rows(b)
+    return back(ops.rows_add(ra, rb))
+
+
+# ------------------------------------------------------------------ torch leaves on HIP kernels
+class Linear(nn.Linear):
+    """torch.nn.Linear (same name and parameters); forward = the HIP GEMM, bias fused."""
+
+    def prepare(self):
+        self._w, self._b = bf(self.weight), f32(self.bias)
+
+    def forward(self, x):
+        out = ops.gemm(token_rows(x), self._w, bias=self._b)
+        return out.view(*x.shape[:-1], self.out_features)
+
+
+class Conv2d(nn.Conv2d):
+    """torch.nn.Conv2d (3x3 pad 1 stride 1/2, or 1x1) on the implicit-GEMM MFMA kernel."""
+
+    out_f32 = False  # conv_out: fp32 eps, as the fused path
+
+    def prepare(self):
+        k = self.kernel_size
+        if k == (3, 3):
+            self._cin_pad = (self.in_channels + 7) // 8 * 8
+            self._w = pack_conv3x3(self.weight, cin_pad=self._cin_pad)
+        elif k == (1, 1):
+            self._cin_pad = self.in_channels
+            self._w = bf(self.weight.reshape(self.out_channels, self.in_channels))
+        else:
+            raise NotImplementedError(f"kernel {k}")
+        self._b = f32(self.bias)
+
+    def forward(self, x):
+        if x.dim() != 4:
+            raise ValueError(f"Conv2d expects (N, C, H, W), got {tuple(x.shape)}")
+        n, c, h, w = x.shape
+        if c != self._cin_pad:  # conv_in: 4 channels -> 16-byte rows (zero channels 4..7)
+            rows = ops.pack_latents(x.float()[:, :, None], dup=1, cpad=self._cin_pad)
+        else:
+            rows = fmap_rows(x)
+        if self.kernel_size == (1, 1):
+            out = ops.gemm(rows, self._w, bias=self._b, out_f32=self.out_f32)
+            return rows_fmap(out, (n, self.out_channels, h, w))
+        out, ho, wo = ops.conv3x3(rows, n, h, w, self._w, stride=self.stride[0], bias=self._b,
+                                  out_f32=self.out_f32)
+        return rows_fmap(out, (n, self.out_channels, ho, wo))
+
+
+class GroupNorm(nn.GroupNorm):
+    """torch.nn.GroupNorm over (N, C, H, W) images or (B, C, F, H, W) videos (the motion
+    module's norm: statistics over C/G channels x F x H x W) on the HIP norm kernels."""
+
+    def prepare(self):
+        self._g, self._b = f32(self.weight), f32(self.bias)
+
+    def forward(self, x):
+        rows = fmap_rows(x)
+        pix = math.prod(x.shape[2:])
+        out = ops.group_norm(rows, x.shape[0], pix, self.num_groups, self.eps, self._g, self._b,
+                             two_pass=x.dim() == 4)
+        return rows_fmap(out, tuple(x.shape))
+
+
+class LayerNorm(nn.LayerNorm):
+    """torch.nn.LayerNorm over the last dim on the HIP row kernel."""
+
+    def prepare(self):
+        self._g, self._b = f32(self.weight), f32(self.bias)
+
+    def forward(self, x):
+        return ops.layer_norm(token_rows(x), self._g, self._b, eps=self.eps).view(x.shape)
+
+
+class SiLU(nn.SiLU):
+    def forward(self, x):
+        rows, back = any_rows(x)
+        return back(ops.silu_rows(rows))
+
+
+class Dropout(nn.Dropout):
+    """p = 0 everywhere in the reference's models (inference): the identity."""
+
+    def forward(self, x):
+        if self.p != 0.0 and self.training:
+            raise NotImplementedError("dropout with p > 0")
+        return x
+
+
+# ------------------------------------------------------------------ diffusers leaves
 class Timesteps(nn.Module):
     """diffusers:Timesteps(num_channels, flip_sin_to_cos=True, downscale_freq_shift=0)."""
 
@@ -79,13 +223,16 @@ class Timesteps(nn.Module):
         super().__init__()
         self.num_channels = num_channels
 
+    def forward(self, timesteps):
+        return ops.timestep_embed(timesteps.to(torch.float32).contiguous(), self.num_channels)
+
 
 class TimestepEmbedding(nn.Module):
     def __init__(self, in_channels: int, time_embed_dim: int):
         super().__init__()
-        self.linear_1 = nn.Linear(in_channels, time_embed_dim)
-        self.act = nn.SiLU()
-        self.linear_2 = nn.Linear(time_embed_dim, time_embed_dim)
+        self.linear_1 = Linear(in_channels, time_embed_dim)
+        self.act = SiLU()
+        self.linear_2 = Linear(time_embed_dim, time_embed_dim)
 
     def prepare(self):
         self._w1, self._b1 = bf(self.linear_1.weight), f32(self.linear_1.bias)
@@ -95,6 +242,11 @@ class TimestepEmbedding(nn.Module):
         """silu(linear_2(silu(linear_1(t_emb)))) — ResnetBlock2D consumes only silu(temb)."""
         h = ops.gemm(t_emb, self._w1, bias=self._b1, act=ops.ACT_SILU)
         return ops.gemm(h, self._w2, bias=self._b2, act=ops.ACT_SILU)
+
+    def forward(self, sample, condition=None):
+        if condition is not None:
+            raise NotImplementedError("timestep_cond is not used by the reference's pipeline")
+        return self.linear_2(self.act(self.linear_1(sample)))
 
 
 class SinusoidalPositionalEmbedding(nn.Module):
@@ -117,6 +269,13 @@ class SinusoidalPositionalEmbedding(nn.Module):
     def reset_buffers(self):
         self.pe = self.table(self.pe.shape[2], self.pe.shape[1]).to(self.pe.device)
 
+    def prepare(self):
+        self._pe = f32(self.pe[0])
+
+    def forward(self, x):
+        """x (N, S, C) + pe[:, :S]."""
+        return ops.rows_add(token_rows(x), self._pe, y_period=x.shape[1]).view(x.shape)
+
 
 class Attention(nn.Module):
     """diffusers:Attention (AttnProcessor2_0 semantics): to_q/k/v without bias,
@@ -129,10 +288,10 @@ class Attention(nn.Module):
         self.heads = heads
         self.dim_head = dim_head
         self.is_cross = cross_attention_dim is not None
-        self.to_q = nn.Linear(query_dim, inner, bias=False)
-        self.to_k = nn.Linear(kv_dim, inner, bias=False)
-        self.to_v = nn.Linear(kv_dim, inner, bias=False)
-        self.to_out = nn.ModuleList([nn.Linear(inner, query_dim), nn.Dropout(0.0)])
+        self.to_q = Linear(query_dim, inner, bias=False)
+        self.to_k = Linear(kv_dim, inner, bias=False)
+        self.to_v = Linear(kv_dim, inner, bias=False)
+        self.to_out = nn.ModuleList([Linear(inner, query_dim), Dropout(0.0)])
 
     # The softmax scale dim_head^-0.5 (and the log2(e) of the kernels' exp2) is
     # folded into the packed to_q rows: the projection GEMM rounds c*q to bf16 ONCE
@@ -153,11 +312,41 @@ class Attention(nn.Module):
     def project_kv(self, ctx_rows):
         return ops.gemm(ctx_rows, self._wkv)
 
+    def forward(self, hidden_states, encoder_hidden_states=None, attention_mask=None, **cross_attention_kwargs):
+        """AttnProcessor2_0 over (N, S, C) tokens: to_q/to_k/to_v modules, softmax(q k^T /
+        sqrt(d)) v per head on the flash kernel (the frame-attention kernel when the
+        sequence is a motion module's <= 32 frames), to_out modules."""
+        if attention_mask is not None:
+            raise NotImplementedError("attention_mask is not used by the reference's pipeline")
+        x = to_bf16_cuda(hidden_states)
+        ctx = x if encoder_hidden_states is None else to_bf16_cuda(encoder_hidden_states)
+        N, S, _ = x.shape
+        L = ctx.shape[1]
+        q, k, v = self.to_q(x), self.to_k(ctx), self.to_v(ctx)
+        h, d = self.heads, self.dim_head
+        qr, kr, vr = token_rows(q), token_rows(k), token_rows(v)
+        scale = d ** -0.5
+        if encoder_hidden_states is None and S <= 32:
+            o = ops.temporal_attention(qr, kr, vr, N, S, 1, h, d, scale=scale)
+        else:
+            o = ops.attention(qr, kr, vr, N, h, S, L, d, kv_div=N // ctx.shape[0], scale=scale)
+        out = self.to_out[0](o.view(N, S, h * d))
+        return self.to_out[1](out)
+
 
 class GEGLU(nn.Module):
     def __init__(self, dim_in: int, dim_out: int):
         super().__init__()
-        self.proj = nn.Linear(dim_in, dim_out * 2)
+        self.proj = Linear(dim_in, dim_out * 2)
+
+    def prepare(self):
+        self._w = pack_geglu(bf(self.proj.weight))
+        self._b = pack_geglu(f32(self.proj.bias))
+
+    def forward(self, hidden_states):
+        """h, g = proj(x).chunk(2); h * gelu(g) — one GEMM with the GEGLU epilogue."""
+        out = ops.gemm(token_rows(hidden_states), self._w, bias=self._b, act=ops.ACT_GEGLU)
+        return out.view(*hidden_states.shape[:-1], self._w.shape[0] // 2)
 
 
 class FeedForward(nn.Module):
@@ -166,40 +355,48 @@ class FeedForward(nn.Module):
     def __init__(self, dim: int, mult: int = 4):
         super().__init__()
         inner = dim * mult
-        self.net = nn.ModuleList([GEGLU(dim, inner), nn.Dropout(0.0), nn.Linear(inner, dim)])
+        self.net = nn.ModuleList([GEGLU(dim, inner), Dropout(0.0), Linear(inner, dim)])
 
     def prepare(self):
-        p = self.net[0].proj
-        self._w1 = pack_geglu(bf(p.weight))
-        self._b1 = pack_geglu(f32(p.bias))
         self._w2, self._b2 = bf(self.net[2].weight), f32(self.net[2].bias)
 
     def forward_rows(self, n, res):
-        g = ops.gemm(n, self._w1, bias=self._b1, act=ops.ACT_GEGLU)
+        g = ops.gemm(n, self.net[0]._w, bias=self.net[0]._b, act=ops.ACT_GEGLU)
         return ops.gemm(g, self._w2, bias=self._b2, res=res)
+
+    def forward(self, hidden_states):
+        for m in self.net:
+            hidden_states = m(hidden_states)
+        return hidden_states
 
 
 class Downsample2D(nn.Module):
     def __init__(self, channels: int, out_channels: int):
         super().__init__()
-        self.conv = nn.Conv2d(channels, out_channels, 3, stride=2, padding=1)
+        self.conv = Conv2d(channels, out_channels, 3, stride=2, padding=1)
 
-    def prepare(self):
-        self._w, self._b = pack_conv3x3(self.conv.weight), f32(self.conv.bias)
-
-    def forward(self, x: Act) -> Act:
-        t, h, w = ops.conv3x3(x.t, x.n, x.h, x.w, self._w, stride=2, bias=self._b)
+    def run(self, x: Act) -> Act:
+        t, h, w = ops.conv3x3(x.t, x.n, x.h, x.w, self.conv._w, stride=2, bias=self.conv._b)
         return Act(t, x.n, h, w)
+
+    def forward(self, hidden_states, *args, **kwargs):
+        return self.conv(hidden_states)
 
 
 class Upsample2D(nn.Module):
     def __init__(self, channels: int, out_channels: int):
         super().__init__()
-        self.conv = nn.Conv2d(channels, out_channels, 3, padding=1)
+        self.conv = Conv2d(channels, out_channels, 3, padding=1)
 
-    def prepare(self):
-        self._w, self._b = pack_conv3x3(self.conv.weight), f32(self.conv.bias)
-
-    def forward(self, x: Act) -> Act:
-        t, h, w = ops.conv3x3(x.t, x.n, x.h, x.w, self._w, upsample=True, bias=self._b)
+    def run(self, x: Act) -> Act:
+        t, h, w = ops.conv3x3(x.t, x.n, x.h, x.w, self.conv._w, upsample=True, bias=self.conv._b)
         return Act(t, x.n, h, w)
+
+    def forward(self, hidden_states, output_size=None, *args, **kwargs):
+        """F.interpolate(x, scale_factor=2.0, mode="nearest") then conv (the fast path folds
+        the upsample into the conv's loader instead)."""
+        if output_size is not None:
+            raise NotImplementedError("output_size")
+        n, c, h, w = hidden_states.shape
+        up = ops.upsample2x_rows(fmap_rows(hidden_states), n, h, w)
+        return self.conv(rows_fmap(up, (n, c, 2 * h, 2 * w)))

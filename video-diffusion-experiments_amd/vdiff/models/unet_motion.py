@@ -23,7 +23,7 @@ from .. import ops
 from ..config import down_block_plan, get_config, up_block_plan
 from .blocks import (CrossAttnDownBlockMotion, CrossAttnUpBlockMotion, Ctx, DownBlockMotion,
                      ResnetBlock2D, UNetMidBlockCrossAttnMotion, UpBlockMotion)
-from .layers import Act, TimestepEmbedding, Timesteps, bf, f32, pack_conv3x3
+from .layers import Act, Conv2d, GroupNorm, SiLU, TimestepEmbedding, Timesteps, bf, f32, fmap_rows, token_rows
 
 
 class FrozenDict(dict):
@@ -38,6 +38,11 @@ class FrozenDict(dict):
 
 UNetMotionOutput = namedtuple("UNetMotionOutput", ["sample"])
 
+
+def fmap_rows_f32(x):
+    """fp32 channels-last (N, C, H, W) -> its NHWC rows (conv_out's output)."""
+    return x.permute(0, 2, 3, 1).reshape(-1, x.shape[1])
+
 CIN_PAD = 8  # conv_in input channels padded 4 -> 8 (16-byte NHWC rows)
 
 
@@ -51,7 +56,7 @@ class UNetMotionModel(nn.Module):
         heads, mheads = cfg["num_attention_heads"], cfg["motion_num_attention_heads"]
         cross, mlen = cfg["cross_attention_dim"], cfg["motion_max_seq_length"]
         tdim = boc[0] * 4
-        self.conv_in = nn.Conv2d(cfg["in_channels"], boc[0], 3, padding=1)
+        self.conv_in = Conv2d(cfg["in_channels"], boc[0], 3, padding=1)
         self.time_proj = Timesteps(boc[0])
         self.time_embedding = TimestepEmbedding(boc[0], tdim)
         self.down_blocks = nn.ModuleList()
@@ -71,9 +76,10 @@ class UNetMotionModel(nn.Module):
             self.up_blocks.append(blk)
         self.mid_block = UNetMidBlockCrossAttnMotion(boc[-1], tdim, heads, cross, mheads, g, eps, mlen,
                                                      use_motion=cfg.get("use_motion_mid_block", True))
-        self.conv_norm_out = nn.GroupNorm(g, boc[0], eps=eps)
-        self.conv_act = nn.SiLU()
-        self.conv_out = nn.Conv2d(boc[0], cfg["out_channels"], 3, padding=1)
+        self.conv_norm_out = GroupNorm(g, boc[0], eps=eps)
+        self.conv_act = SiLU()
+        self.conv_out = Conv2d(boc[0], cfg["out_channels"], 3, padding=1)
+        self.conv_out.out_f32 = True  # eps leaves the UNet in fp32
         self._prepared = False
         self.dist = None  # vdiff.dist.FrameShard when frames are sharded across ranks
 
@@ -96,11 +102,8 @@ class UNetMotionModel(nn.Module):
             raise RuntimeError("UNetMotionModel.prepare(): move the model to the GPU first (no CPU path)")
         for m in self.modules():
             if m is not self and hasattr(m, "prepare"):
-                m.prepare()  # every block packs only its own operands
-        self._w_in = pack_conv3x3(self.conv_in.weight, cin_pad=CIN_PAD)
-        self._b_in = f32(self.conv_in.bias)
-        self._w_out, self._b_out = pack_conv3x3(self.conv_out.weight), f32(self.conv_out.bias)
-        self._g_out, self._be_out = f32(self.conv_norm_out.weight), f32(self.conv_norm_out.bias)
+                m.prepare()  # every module packs only its own operands
+        assert self.conv_in._cin_pad == CIN_PAD
         res = self.resnets_in_order()
         off = 0
         for r in res:
@@ -121,19 +124,60 @@ class UNetMotionModel(nn.Module):
         """Packed NHWC input rows [batch*frames*h*w, 8] -> eps rows fp32 [..., out_channels]."""
         g = self.config["norm_num_groups"]
         n_img = ctx.batch * ctx.frames
-        t, _, _ = ops.conv3x3(x_rows, n_img, h, w, self._w_in, bias=self._b_in)
+        t, _, _ = ops.conv3x3(x_rows, n_img, h, w, self.conv_in._w, bias=self.conv_in._b)
         x = Act(t, n_img, h, w)
         skips = [x]
         for blk in self.down_blocks:
-            x, outs = blk(x, ctx)
+            x, outs = blk.run(x, ctx)
             skips.extend(outs)
-        x = self.mid_block(x, ctx)
+        x = self.mid_block.run(x, ctx)
         for blk in self.up_blocks:
-            x = blk(x, ctx, skips)
-        hn = ops.group_norm(x.t, x.n, x.h * x.w, g, self.config["norm_eps"], self._g_out, self._be_out,
-                            silu=True)
-        eps, _, _ = ops.conv3x3(hn, x.n, x.h, x.w, self._w_out, bias=self._b_out, out_f32=True)
+            x = blk.run(x, ctx, skips)
+        no = self.conv_norm_out
+        hn = ops.group_norm(x.t, x.n, x.h * x.w, g, self.config["norm_eps"], no._g, no._b, silu=True)
+        eps, _, _ = ops.conv3x3(hn, x.n, x.h, x.w, self.conv_out._w, bias=self.conv_out._b, out_f32=True)
         return eps
+
+    def has_hooks(self) -> bool:
+        """Forward (pre-)hooks registered on any module of the tree, or globally."""
+        from torch.nn.modules import module as _m
+        if _m._global_forward_hooks or _m._global_forward_pre_hooks:
+            return True
+        return any(m._forward_hooks or m._forward_pre_hooks for m in self.modules() if m is not self)
+
+    def forward_modules(self, sample, t, ehs):
+        """diffusers UNetMotionModel.forward module by module: every block
+        and leaf through __call__ with diffusers-layout tensors, all on the HIP kernels — the
+        path a forward-hook trace (experiments/03_trace_forward_pass.py:105-113) observes."""
+        B, Cc, Fr, H, W = sample.shape
+        L = ehs.shape[1]
+        emb = self.time_embedding(self.time_proj(t))                       # (B, 1280)
+        emb = ops.rows_add(None, emb, y_div=Fr, out=torch.empty(B * Fr, emb.shape[1], device=emb.device,
+                                                                dtype=torch.bfloat16))  # repeat_interleave(F)
+        ehs_rows = token_rows(ehs)
+        ehs_rep = torch.empty(B * Fr * L, ehs.shape[2], device=ehs.device, dtype=torch.bfloat16)
+        for b in range(B):  # ehs.repeat_interleave(F, 0)
+            ops.rows_add(None, ehs_rows[b * L:(b + 1) * L], out=ehs_rep[b * Fr * L:(b + 1) * Fr * L])
+        ehs_rep = ehs_rep.view(B * Fr, L, -1)
+        x = sample.permute(0, 2, 1, 3, 4).reshape(B * Fr, Cc, H, W)
+        h = self.conv_in(x)
+        skips = (h,)
+        for blk in self.down_blocks:
+            if isinstance(blk, DownBlockMotion):
+                h, res = blk(h, emb, num_frames=Fr)
+            else:
+                h, res = blk(h, emb, encoder_hidden_states=ehs_rep, num_frames=Fr)
+            skips = skips + res
+        h = self.mid_block(h, emb, encoder_hidden_states=ehs_rep, num_frames=Fr)
+        for blk in self.up_blocks:
+            n = len(blk.resnets)
+            res, skips = skips[-n:], skips[:-n]
+            if isinstance(blk, UpBlockMotion):
+                h = blk(h, res, emb, num_frames=Fr)
+            else:
+                h = blk(h, res, emb, encoder_hidden_states=ehs_rep, num_frames=Fr)
+        h = self.conv_out(self.conv_act(self.conv_norm_out(h)))            # fp32 (B*F, C, H, W)
+        return ops.unpack_nhwc(fmap_rows_f32(h), B, h.shape[1], Fr, H, W)
 
     def forward(self, sample, timestep, encoder_hidden_states, timestep_cond=None, attention_mask=None,
                 cross_attention_kwargs=None, added_cond_kwargs=None,
@@ -154,10 +198,13 @@ class UNetMotionModel(nn.Module):
         t = t.to(torch.float32).expand(B).contiguous()
         ehs = encoder_hidden_states.to(device=dev, dtype=torch.bfloat16).contiguous()
         L = ehs.shape[1]
-        te = ops.timestep_embed(t, self.time_proj.num_channels)
-        ctx = self.make_ctx(te, ehs.reshape(B * L, -1), B, Fr, L)
-        x_rows = ops.pack_latents(sample.to(dev), dup=1, cpad=CIN_PAD)
-        eps_rows = self.forward_rows(x_rows, H, W, ctx)
-        out = ops.unpack_nhwc(eps_rows, B, self.config["out_channels"], Fr, H, W)
+        if self.has_hooks():
+            out = self.forward_modules(sample.to(dev, torch.float32), t, ehs)
+        else:
+            te = ops.timestep_embed(t, self.time_proj.num_channels)
+            ctx = self.make_ctx(te, ehs.reshape(B * L, -1), B, Fr, L)
+            x_rows = ops.pack_latents(sample.to(dev), dup=1, cpad=CIN_PAD)
+            eps_rows = self.forward_rows(x_rows, H, W, ctx)
+            out = ops.unpack_nhwc(eps_rows, B, self.config["out_channels"], Fr, H, W)
         out = out.to(sample.dtype) if sample.dtype.is_floating_point else out
         return UNetMotionOutput(out) if return_dict else (out,)

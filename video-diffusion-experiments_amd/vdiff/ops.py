@@ -317,6 +317,40 @@ def block_transpose(src, nb, na, nc, out=None):
     return out
 
 
+# ---------------------------------------------------------------- module-level path (rows.hip)
+def rows_add(x, y, y_div=1, y_period=None, out=None):
+    """out[r] = (x[r] if x is not None else 0) + y[(r // y_div) % y_period]: bf16 rows x, y bf16 or
+    fp32 rows.  `out` may be a column slice of a wider buffer (channel concat)."""
+    _dev(x, y, out)
+    rows = out.shape[0] if out is not None else x.shape[0]
+    C = y.shape[1] if x is None else x.shape[1]
+    if out is None:
+        out = torch.empty(rows, C, device=y.device, dtype=BF16)
+    y_f32 = y.dtype == torch.float32
+    period = y.shape[0] if y_period is None else y_period
+    check(lib().vd_rows_eltwise(0, _p(x), _rows(x) if x is not None else 0, _p(y), _rows(y, y.dtype), int(y_f32),
+                                y_div, period, rows, C, _p(out), _rows(out), _stream()), "vd_rows_eltwise(add)")
+    return out
+
+
+def silu_rows(x, out=None):
+    _dev(x, out)
+    if out is None:
+        out = torch.empty_like(x)
+    check(lib().vd_rows_eltwise(1, _p(x), _rows(x), None, 0, 0, 1, 1, x.shape[0], x.shape[1], _p(out),
+                                _rows(out), _stream()), "vd_rows_eltwise(silu)")
+    return out
+
+
+def upsample2x_rows(x, n_img, h, w, out=None):
+    _dev(x, out)
+    if out is None:
+        out = torch.empty(n_img * 4 * h * w, x.shape[1], device=x.device, dtype=BF16)
+    check(lib().vd_upsample_nearest2x(_p(x), _rows(x), n_img, h, w, x.shape[1], _p(out), _rows(out), _stream()),
+          "vd_upsample_nearest2x")
+    return out
+
+
 # ---------------------------------------------------------------- DiT (§8f rank 3)
 def patchify(lat, p, kpad, dup=1, in_div=1.0, out=None):
     """latents fp32 (B,C,F,H,W) -> bf16 token rows [(b,f,hp,wp)][kpad] (x dup for CFG)."""

@@ -21,9 +21,16 @@ the graph.
 
 Out of scope: CLIP text encoding (a deterministic stub encoder
 stands in; real embeddings can be passed as prompt_embeds).  VAE decoding (§8f
-rank 1) runs when the pipeline holds a `vdiff.AutoencoderKL`: output_type "pt" /
-"np" return diffusers' postprocessed video ((B, F, 3, H, W) tensor / (B, F, H, W, 3)
-array in [0, 1]), "latent" the final latents.
+rank 1) runs when the pipeline holds a `vdiff.AutoencoderKL` (from_config builds one
+by default): output_type "pil" (diffusers' default: `.frames[0]` is the first video's
+list of PIL images, which 05_grid_search_ablation.py:169-182 saves as PNG / GIF),
+"pt" / "np" (diffusers' postprocessed video, (B, F, 3, H, W) tensor / (B, F, H, W, 3)
+array in [0, 1]) or "latent" (the final latents).
+
+prepare_latents follows diffusers' randn_tensor for the reference's CPU generator
+(05:156 `torch.manual_seed(seed)`): x_T = torch.randn(shape, generator, dtype) drawn on
+the CPU in the pipeline's torch_dtype — float16 in the reference (05:35, 05:130-134) —
+then moved to the GPU (kept in fp32 from there on).
 """
 from __future__ import annotations
 
@@ -163,7 +170,26 @@ class DenoiseLoop:
         return self.lat
 
 
+def numpy_to_pil(images):
+    """diffusers' numpy_to_pil: (F, H, W, 3) floats in [0, 1] -> list of RGB PIL images."""
+    from PIL import Image
+    arr = (images * 255).round().astype("uint8")
+    return [Image.fromarray(a) for a in arr]
+
+
+def export_to_gif(frames, output_gif_path, fps: int = 10):
+    """diffusers.utils.export_to_gif (05:28, :181): PIL frames -> an animated GIF."""
+    frames[0].save(str(output_gif_path), save_all=True, append_images=list(frames[1:]), optimize=False,
+                   duration=1000 // fps, loop=0)
+    return str(output_gif_path)
+
+
 class AnimateDiffPipeline:
+    # dtype the initial noise is drawn in on the CPU generator: the reference loads the
+    # pipeline with torch_dtype=torch.float16 (05:35, 05:130-134) and diffusers' randn_tensor
+    # draws in that dtype
+    latent_draw_dtype = torch.float16
+
     def __init__(self, unet: UNetMotionModel, scheduler=None, text_encoder=None, vae=None, dist=None):
         self.unet = unet
         self.scheduler = scheduler or DDIMScheduler()
@@ -173,9 +199,12 @@ class AnimateDiffPipeline:
         self.unet.dist = dist
 
     @classmethod
-    def from_config(cls, config="full", device="cuda", seed=0, scheduler=None, dist=None, vae=None):
-        """Synthetic-weight pipeline; vae=None (latents only), "tiny"/"full" (a synthetic
-        AutoencoderKL of that config) or an AutoencoderKL instance."""
+    def from_config(cls, config="full", device="cuda", seed=0, scheduler=None, dist=None, vae="auto"):
+        """Synthetic-weight pipeline; vae "auto" (a synthetic AutoencoderKL of the UNet's config,
+        so the default output_type "pil" works), "tiny"/"full", an AutoencoderKL instance, or
+        None (latents only)."""
+        if vae == "auto":
+            vae = config if config in ("tiny", "full") else None
         unet = UNetMotionModel(config)
         init_synthetic_(unet, seed)
         unet = unet.to(device=device, dtype=torch.bfloat16)
@@ -219,23 +248,33 @@ class AnimateDiffPipeline:
 
     @staticmethod
     def postprocess_video(video, output_type):
-        """diffusers VideoProcessor.postprocess_video for "pt" / "np": per video, frames first,
-        denormalised (x / 2 + 0.5).clamp(0, 1)."""
+        """diffusers VideoProcessor.postprocess_video for "pt" / "np" / "pil": per video, frames
+        first, denormalised (x / 2 + 0.5).clamp(0, 1); "pil" -> a list (per video) of lists of
+        PIL images."""
         v = (video / 2 + 0.5).clamp(0, 1).permute(0, 2, 1, 3, 4)      # (B, F, 3, H, W)
         if output_type == "pt":
             return v
-        return v.permute(0, 1, 3, 4, 2).cpu().numpy()                  # (B, F, H, W, 3)
+        arr = v.permute(0, 1, 3, 4, 2).float().cpu().numpy()           # (B, F, H, W, 3)
+        if output_type == "np":
+            return arr
+        return [numpy_to_pil(a) for a in arr]
+
+    def prepare_latents(self, batch, num_frames, h, w, generator=None, latents=None):
+        """diffusers AnimateDiffPipeline.prepare_latents -> fp32 on the GPU, x init_noise_sigma."""
+        if latents is None:
+            shape = (batch, self.unet.config["in_channels"], num_frames, h, w)
+            latents = torch.randn(shape, generator=generator, dtype=self.latent_draw_dtype)
+        return latents.to(self.unet.device, torch.float32) * self.scheduler.init_noise_sigma
 
     @torch.no_grad()
     def __call__(self, prompt=None, num_frames=16, height=None, width=None, num_inference_steps=50,
                  guidance_scale=7.5, negative_prompt=None, num_videos_per_prompt=1, eta=0.0,
                  generator=None, latents=None, prompt_embeds=None, negative_prompt_embeds=None,
-                 output_type="latent", return_dict=True, use_graph=True, **unused):
+                 output_type="pil", return_dict=True, use_graph=True, **unused):
         if eta != 0.0:
             raise NotImplementedError("eta > 0")
-        if output_type not in ("latent", "pt", "np"):
-            raise NotImplementedError(f"output_type {output_type!r}: PIL is not part of this build; "
-                                      "use 'pt', 'np' or 'latent'")
+        if output_type not in ("latent", "pt", "np", "pil"):
+            raise NotImplementedError(f"output_type {output_type!r}: use 'pil', 'pt', 'np' or 'latent'")
         if output_type != "latent" and self.vae is None:
             raise ValueError(f"output_type {output_type!r} needs a VAE: AnimateDiffPipeline(..., vae=...)")
         dev = self.unet.device
@@ -257,10 +296,7 @@ class AnimateDiffPipeline:
         else:
             ehs = prompt_embeds
         self.scheduler.set_timesteps(num_inference_steps)
-        if latents is None:
-            latents = torch.randn((B, self.unet.config["in_channels"], num_frames, h, w),
-                                  generator=generator, dtype=torch.float32)
-        latents = latents.to(dev, torch.float32) * self.scheduler.init_noise_sigma
+        latents = self.prepare_latents(B, num_frames, h, w, generator=generator, latents=latents)
         local = latents
         if self.dist is not None:
             fl = self.dist.frames_local(num_frames)

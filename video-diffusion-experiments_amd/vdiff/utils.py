@@ -1,0 +1,3 @@
+"""diffusers.utils stand-ins the reference's sampling scripts import
+(experiments/05_grid_search_ablation.py:28 `from diffusers.utils import export_to_gif`)."""
+from .pipeline import export_to_gif, numpy_to_pil  # noqa: F401
