@@ -51,7 +51,8 @@ const char* vd_build_hash(void);
  *
  * a_mode VD_A_DENSE : A[m, k] = a0[m*lda0 + k]              for k <  k0
  *                              a1[m*lda1 + (k - k0)]       for k >= k0  (channel concat)
- * a_mode VD_A_CONV3X3: implicit-GEMM 3x3 conv, pad 1, over NHWC images; the
+ * a_mode VD_A_CONV3X3: implicit-GEMM 3x3 conv, pad 1, over NHWC images (or a kt x 3 x 3
+ *   conv over the frames of each video, see kt below); the
  *   K index is tap*(Cin) + ci with Cin = k0 + (channels of a1); channels
  *   [0,k0) come from a0 (pixel stride lda0), the rest from a1 (pixel stride
  *   lda1) — this is the up-block torch.cat([x, skip], 1) without materialising
@@ -84,6 +85,14 @@ typedef struct vd_gemm_desc {
   /* split-K workspace (fp32 partial slabs); size from vd_gemm_ws_bytes(), may be
    * NULL when that returns 0. */
   void* ws; int64_t ws_bytes;
+  /* 3-D / (2+1)D conv (VD_A_CONV3X3 only): a kt x ks x ks kernel over the frames of each
+   * video — kt temporal taps (1 or 3; 0 means 1), ks spatial (3, or 1 for the temporal half
+   * of a (2+1)D conv; 0 means 3; pad ks/2).  K index = (dt*ks*ks + tap)*Cin + ci.  Output
+   * image n = b*frames_out + f reads, at temporal tap dt, input image
+   * b*frames_in + f + t_off + dt - kt/2, zero outside [0, frames_in) (the conv's temporal
+   * zero padding; a frame-sharded rank passes its halo'd frames with frames_in =
+   * frames_out + 2, t_off = 1).  n_img counts OUTPUT images. */
+  int32_t kt, ks, frames_in, frames_out, t_off;
 } vd_gemm_desc;
 
 int vd_gemm(const vd_gemm_desc* d, vd_stream_t stream);

@@ -113,7 +113,19 @@ def _worker(rank, world, port, errq):
         want = ref.reshape(B, F, C, HW).permute(0, 1, 3, 2)[:, rank * Fl:(rank + 1) * Fl].reshape(-1, C)
         err = (got - want).abs().max().item()
         assert err < 1e-4, f"sharded motion module max err {err}"
-        # ---- 3. latent all-gather over frames
+        # ---- 3. kt = 3 temporal conv under frame sharding: one-frame halo (P2P) + a conv
+        # over the halo'd frames with no temporal padding == the unsharded 3-D conv's frames
+        Cc, Co = 8, 16
+        vid = torch.randn(B, Cc, F, H, W)
+        wt = torch.randn(Co, Cc, 3, 3, 3) * 0.2
+        full = torch.nn.functional.conv3d(vid, wt, padding=1)                  # (B, Co, F, H, W)
+        rows = vid.permute(0, 2, 3, 4, 1)[:, rank * Fl:(rank + 1) * Fl].reshape(-1, Cc).contiguous()
+        halo = fs.halo_frames(rows, B, Fl, HW)                                # (b, Fl + 2, p) rows
+        hv = halo.reshape(B, Fl + 2, H, W, Cc).permute(0, 4, 1, 2, 3)
+        got = torch.nn.functional.conv3d(hv, wt, padding=(0, 1, 1))
+        err = (got - full[:, :, rank * Fl:(rank + 1) * Fl]).abs().max().item()
+        assert err < 1e-4, f"halo'd temporal conv max err {err}"
+        # ---- 4. latent all-gather over frames
         lat = torch.full((1, 4, Fl, 2, 2), float(rank))
         g = fs.all_gather_frames(lat)
         assert g.shape == (1, 4, F, 2, 2) and torch.equal(g[0, 0, :, 0, 0], torch.tensor([0., 0., 1., 1.]))

@@ -350,6 +350,70 @@ def test_conv3x3(cuda, case):
     close_f32(out, want, rtol=1e-3, atol=1e-4 * max(1.0, want.abs().max().item()))
 
 
+@pytest.mark.parametrize("kt,ks,stride,path", [(3, 3, 1, 0), (3, 3, 2, 0), (3, 1, 1, 0), (1, 3, 1, 0),
+                                                (3, 3, 1, 1), (3, 1, 1, 1), (3, 3, 1, 2)])
+def test_conv3d_temporal_taps(cuda, kt, ks, stride, path):
+    """The north star's 3-D / (2+1)D conv over (B, C, T, H, W): kernel (3,3,3), the temporal
+    half (3,1,1) and the reference's per-frame (1,3,3), spatial stride 1 / 2, temporal zero
+    padding at the video's ends, fp32 output vs fp64 F.conv3d at rtol 1e-3 / atol 1e-4
+    (scaled by the output's magnitude); path 0 = automatic (v2 LDS-DMA), 1 = v1, 2 = v2 split."""
+    from vdiff._lib import lib
+    from vdiff.models.layers import pack_conv3d
+    torch.manual_seed(3)
+    B, T, h, w, ci, co = 2, 5, 16, 12, 64, 160
+    x = rnd(B * T * h * w, ci)
+    wt = bf(torch.randn(co, ci, kt, ks, ks, device=cuda) * 0.05)
+    b = torch.randn(co, device=cuda)
+    lib().vd_gemm_select_path({0: 0, 1: 1, 2: 2}[path])
+    try:
+        out, ho, wo = ops.conv3d(x, B, T, h, w, pack_conv3d(wt), kt=kt, ks=ks, stride=stride, bias=b, out_f32=True)
+    finally:
+        lib().vd_gemm_select_path(0)
+    vid = x.double().reshape(B, T, h, w, ci).permute(0, 4, 1, 2, 3).cpu()
+    want = F.conv3d(vid, wt.double().cpu(), b.double().cpu(), stride=(1, stride, stride),
+                    padding=(kt // 2, ks // 2, ks // 2))
+    want = want.permute(0, 2, 3, 4, 1).reshape(-1, co)
+    assert out.shape == want.shape
+    close_f32(out, want, rtol=1e-3, atol=1e-4 * max(1.0, want.abs().max().item()))
+
+
+def test_conv3d_halo_form_matches_full_video(cuda):
+    """A frame-sharded rank's call: its frames plus one halo frame each side (frames_in =
+    frames_out + 2, t_off = 1, no temporal padding needed inside) gives exactly the full
+    video's conv on those frames."""
+    from vdiff.models.layers import pack_conv3d
+    torch.manual_seed(4)
+    B, T, h, w, ci, co = 2, 8, 8, 8, 64, 128
+    x = rnd(B * T * h * w, ci)
+    wp = pack_conv3d(bf(torch.randn(co, ci, 3, 3, 3, device=cuda) * 0.05))
+    full, _, _ = ops.conv3d(x, B, T, h, w, wp, out_f32=True)
+    v = x.view(B, T, h * w, ci)
+    f0, fl = 3, 2                                           # this "rank" holds frames 3, 4
+    halo = v[:, f0 - 1:f0 + fl + 1].reshape(-1, ci).contiguous()
+    part, _, _ = ops.conv3d(halo, B, fl + 2, h, w, wp, frames_out=fl, t_off=1, out_f32=True)
+    want = full.view(B, T, h * w, co)[:, f0:f0 + fl].reshape(-1, co)
+    assert torch.equal(part, want)
+
+
+def test_conv3d_module_on_videos(cuda):
+    """vdiff Conv3d (torch.nn.Conv3d subclass) on a (B, C, T, H, W) video, (2+1)D factorised:
+    (1,3,3) then (3,1,1), against torch's conv3d in fp64 on the same bf16 values."""
+    from vdiff.models.layers import Conv3d
+    torch.manual_seed(5)
+    sp, tp = Conv3d(64, 64, (1, 3, 3), padding=(0, 1, 1)), Conv3d(64, 64, (3, 1, 1), padding=(1, 0, 0))
+    for m in (sp, tp):
+        with torch.no_grad():
+            m.weight.mul_(0.5)
+        m.to("cuda", BF).prepare()
+    x = rnd(2, 64, 6, 10, 10)
+    y = tp(sp(x))
+    assert y.shape == (2, 64, 6, 10, 10)
+    with torch.no_grad():
+        ref = F.conv3d(x.double(), sp.weight.double(), sp.bias.double(), padding=(0, 1, 1))
+        ref = F.conv3d(ref.to(BF).double(), tp.weight.double(), tp.bias.double(), padding=(1, 0, 0))
+    close_bf16(y, ref)
+
+
 # ---------------------------------------------------------------- norms
 @pytest.mark.parametrize("kind", ["image", "video", "concat"])
 def test_group_norm(cuda, kind):

@@ -59,44 +59,77 @@ def trace(model, depth, *args, **kwargs):
 
 @pytest.fixture(scope="module")
 def full_unet(cuda):
-    from vdiff.weights import materialize_synthetic
-    return materialize_synthetic("full", device="cuda", seed=0).prepare()
+    """CPU-seeded synthetic weights: the ones tests/golden/full_f16_t500.npz was made with."""
+    return init_synthetic_(UNetMotionModel("full"), seed=0).to("cuda", torch.bfloat16).prepare()
 
 
-def test_depth5_hook_trace_sees_diffusers_shapes(full_unet):
-    """03's synthetic inputs (03:86-98: sample (1, 4, 16, 64, 64), t = 500, ehs (1, 77, 768)):
-    32 spatial and 42 temporal Attention records (03:134-139's name rules), spatial input
-    (B*F, H*W, C) = (16, 4096, 320), temporal input (B*H*W, F, C) = (4096, 16, 320) at level 1;
-    the traced (module-by-module) output equals the fused path's within bf16 noise."""
+def _attention_records(rec):
+    """03:134-139's classification of the traced class-"Attention" modules."""
+    spatial = [(n, r) for n, r in rec.items() if r[0] == "Attention" and "motion_modules" not in n and "attentions" in n]
+    temporal = [(n, r) for n, r in rec.items() if r[0] == "Attention" and "motion_modules" in n]
+    return spatial, temporal
+
+
+def test_depth5_trace_matches_the_reference_rule(full_unet):
+    """03's own call, ForwardTracer(unet, trace_depth=5) on 03:86-98's inputs (sample
+    (1, 4, 16, 64, 64), t = 500, ehs (1, 77, 768)): depth = name.count(".") (forward_tracer.py:
+    87-89), so only the mid block's attention modules (5 dots) are within depth 5 — the
+    down/up blocks' are 6 deep — 2 spatial + 2 temporal records, as diffusers' tree gives;
+    the temporal input is the [B*H*W, F, C] = (64, 16, 1280) layout 03:160-169 interprets."""
     g = torch.Generator().manual_seed(0)
     sample = torch.randn(1, 4, 16, 64, 64, generator=g).cuda()
     ehs = torch.randn(1, 77, 768, generator=g).cuda()
-    fast = full_unet(sample, torch.tensor([500]), encoder_hidden_states=ehs).sample
-    out, rec, order = trace(full_unet, 5, sample, torch.tensor([500]), encoder_hidden_states=ehs)
-    assert not full_unet.has_hooks()
-    spatial = [(n, r) for n, r in rec.items() if r[0] == "Attention" and "attentions" in n]
-    temporal = [(n, r) for n, r in rec.items() if r[0] == "Attention" and "motion_modules" in n]
-    assert len(spatial) == 32 and len(temporal) == 42
-    s0 = rec["down_blocks.0.attentions.0.transformer_blocks.0.attn1"]
-    t0 = rec["down_blocks.0.motion_modules.0.transformer_blocks.0.attn1"]
-    assert s0[1][0] == (16, 4096, 320) and s0[2][0] == (16, 4096, 320)
-    assert t0[1][0] == (4096, 16, 320) and t0[2][0] == (4096, 16, 320)
-    assert rec["down_blocks.0.attentions.0.transformer_blocks.0.attn2"][1][0] == (16, 4096, 320)
-    assert rec["mid_block.motion_modules.0.transformer_blocks.0.attn1"][1][0] == (64, 16, 1280)
-    # leaves and blocks fire with tensors, never an internal row container
+    _, rec, order = trace(full_unet, 5, sample, torch.tensor([500]), encoder_hidden_states=ehs)
+    spatial, temporal = _attention_records(rec)
+    assert [n for n, _ in spatial] == ["mid_block.attentions.0.transformer_blocks.0.attn1",
+                                       "mid_block.attentions.0.transformer_blocks.0.attn2"]
+    assert len(temporal) == 2 and temporal[0][1][1][0] == (64, 16, 1280)
+    assert spatial[0][1][1][0] == (16, 64, 1280)
     assert rec["conv_in"][1][0] == (16, 4, 64, 64) and rec["conv_in"][2][0] == (16, 320, 64, 64)
     assert rec["down_blocks.0.resnets.0.norm1"][0] == "GroupNorm"
     assert rec["down_blocks.0.motion_modules.0"][1][0] == (16, 320, 64, 64)
     assert rec["up_blocks.3.resnets.0"][1][0] == (16, 960, 64, 64)   # the concat input
-    assert rec["mid_block.attentions.0.transformer_blocks.0.attn1.to_q"][0] == "Linear"
     assert rec["up_blocks.0.upsamplers.0.conv"][1][0] == (16, 1280, 16, 16)
     for name, (_, ins, outs) in rec.items():
         assert all("Act" not in str(s) for s in ins + outs), name
     assert order[0] == "time_proj" and order[-1] == "conv_out"
-    err = rel_l2(out.sample, fast)
-    print(f"module path vs fused path: rel-L2 {err:.5f}; {len(rec)} modules traced")
-    assert out.sample.shape == (1, 4, 16, 64, 64)
-    assert err < 0.01, err
+    assert all(n.count(".") <= 5 for n in rec)
+
+
+def test_full_trace_sees_diffusers_shapes(full_unet):
+    """Every module hooked (trace_depth=None) on the full-config fixture's CFG batch (B = 2,
+    F = 16, t = 500): 32 spatial and 42 temporal Attention records (03:134-139's name rules;
+    docs/02:90-91's 32 spatial modules), spatial input (B*F, H*W, C) = (32, 4096, 320),
+    temporal input (B*H*W, F, C) = (8192, 16, 320) at level 1.  The module-by-module output
+    (separate residual adds: other bf16 rounding points than the fused path) is held to the
+    fp32 oracle at the same 3 % rel-L2 as the fused path (the bf16 realisation floor is
+    ~1.3-1.5 %, tests/test_oracle.py::test_bf16_realisation_floor)."""
+    from pathlib import Path
+    import sys
+    gdir = Path(__file__).resolve().parent / "golden"
+    sys.path.insert(0, str(gdir))
+    from make_full_golden import T, full_inputs
+    gold = np.load(gdir / "full_f16_t500.npz")
+    lat, ehs = full_inputs()
+    x = torch.cat([lat, lat]).cuda()
+    out, rec, order = trace(full_unet, 99, x, T, encoder_hidden_states=ehs.cuda())
+    assert not full_unet.has_hooks()
+    spatial, temporal = _attention_records(rec)
+    assert len(spatial) == 32 and len(temporal) == 42
+    s0 = rec["down_blocks.0.attentions.0.transformer_blocks.0.attn1"]
+    t0 = rec["down_blocks.0.motion_modules.0.transformer_blocks.0.attn1"]
+    assert s0[1][0] == (32, 4096, 320) and s0[2][0] == (32, 4096, 320)
+    assert t0[1][0] == (8192, 16, 320) and t0[2][0] == (8192, 16, 320)
+    assert rec["down_blocks.0.attentions.0.transformer_blocks.0.attn2"][1][0] == (32, 4096, 320)
+    assert rec["mid_block.motion_modules.0.transformer_blocks.0.attn1"][1][0] == (128, 16, 1280)
+    assert rec["down_blocks.0.attentions.0.transformer_blocks.0.attn1.to_q"][0] == "Linear"
+    assert rec["down_blocks.0.motion_modules.0.transformer_blocks.0.pos_embed"][2][0] == (8192, 16, 320)
+    for name, (_, ins, outs) in rec.items():
+        assert all("Act" not in str(s) for s in ins + outs), name
+    err = rel_l2(out.sample, torch.from_numpy(gold["eps"]))
+    print(f"module path (full, F=16) vs fp32 oracle: rel-L2 {err:.5f}; {len(rec)} modules traced")
+    assert out.sample.shape == (2, 4, 16, 64, 64)
+    assert err < 0.03, err
 
 
 def test_direct_motion_module_call_matches_oracle(full_unet):

@@ -135,8 +135,26 @@ def test_tiny_unet_matches_oracle(tiny_unet, gold, t):
     r_dev, m_dev = _errs(out, torch.from_numpy(gold[f"eps_t{t}_dev"]))
     print(f"tiny UNet t={t}: vs fp32 oracle rel-L2 {err:.5f}; vs device-emulating oracle rel-L2 "
           f"{r_dev:.5f} max|err|/max|want| {m_dev:.5f}")
+    # end to end both oracles sit at the bf16 realisation floor (~1.3 %, test_oracle.py::
+    # test_bf16_realisation_floor); the tight bound is per block, test_tiny_blocks_match_...
     assert err < 0.03, err
-    assert r_dev < 0.005, r_dev
+    assert r_dev < 0.03, r_dev
+
+
+def test_tiny_blocks_match_device_emulation(tiny_unet, gold):
+    """Per block, from the device's own input (tests/parity_blocks.py): every block of the
+    tiny UNet against the device-emulating oracle within 0.25 % rel-L2 (a fraction of one bf16
+    rounding: the residual is fp32 summation order flipping a few stores) and against the fp32
+    oracle within 0.6 %; the table is printed."""
+    sys.path.insert(0, str(Path(__file__).resolve().parent))
+    from parity_blocks import block_errors
+    rows = block_errors(tiny_unet, torch.from_numpy(gold["latents"]), torch.from_numpy(gold["ehs"]), log=print)
+    assert len(rows) >= 20
+    worst_dev = max(r[2] for r in rows)
+    worst_32 = max(r[1] for r in rows)
+    print(f"worst block: vs dev {worst_dev:.5f}, vs fp32 {worst_32:.5f}")
+    assert worst_dev < 0.0025, rows
+    assert worst_32 < 0.006, rows
 
 
 def test_scheduler_step_api_matches_oracle(tiny_unet, gold):
@@ -252,8 +270,10 @@ def test_full_unet_sixteen_frames_matches_oracle(cuda):
     weights, as the committed fixture tests/golden/full_f16_t500.npz) on all 16 frames — every
     motion module attends over F = 16 — at t = 500, against the fp32 oracle and the oracle that
     emulates the device's bf16 storage and attention arithmetic (act="dev").  Printed: rel-L2
-    and max|err|/max|want| against both.  Bounds: 3 % rel-L2 vs fp32 (the bf16-activation
-    budget, as the tiny model); 0.5 % vs the device emulation."""
+    and max|err|/max|want| against both.  Bounds: 3 % rel-L2 against either — end to end any
+    two bf16 realisations of the network sit ~1.3-1.5 % apart (the fixture's own dev-vs-fp32
+    is 1.48 %; test_oracle.py::test_bf16_realisation_floor), so the tight check is per block
+    (test_tiny_blocks_match_device_emulation)."""
     sys.path.insert(0, str(GOLD))
     from make_full_golden import T, full_inputs
     gold = np.load(GOLD / "full_f16_t500.npz")
@@ -268,4 +288,4 @@ def test_full_unet_sixteen_frames_matches_oracle(cuda):
     print(f"full UNet F=16 t={T}: vs fp32 oracle rel-L2 {r32:.5f} max {m32:.5f}; "
           f"vs device-emulating oracle rel-L2 {rdv:.5f} max {mdv:.5f}")
     assert r32 < 0.03, r32
-    assert rdv < 0.005, rdv
+    assert rdv < 0.03, rdv

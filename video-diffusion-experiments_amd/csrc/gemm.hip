@@ -238,12 +238,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
   const bf16_t* a1 = (const bf16_t*)d.a1;
   const bf16_t* w = (const bf16_t*)d.w;
 
-  // Per staged A row: pixel coordinates for the conv gather.
-  int pimg[RA], poh[RA], pow_[RA];
+  // Per staged A row: pixel coordinates for the conv gather.  pimg = the input image of
+  // temporal tap 0, pfr = its frame index inside the video (valid range [0, frames_in)).
+  int pimg[RA], pfr[RA], poh[RA], pow_[RA];
   bool prow[RA];
   int cin = 0, hgrid = 0, wgrid = 0;
   if constexpr (MODE == VD_A_CONV3X3) {
-    cin = (int)d.K / 9;
+    cin = (int)d.K / (d.ks * d.ks * d.kt);
     hgrid = d.upsample ? 2 * d.h_in : d.h_in;
     wgrid = d.upsample ? 2 * d.w_in : d.w_in;
     const int hw = d.h_out * d.w_out;
@@ -252,8 +253,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
       const int64_t m = m0 + sr + 32 * i;
       prow[i] = m < M;
       const int mm = prow[i] ? (int)m : 0;
-      pimg[i] = mm / hw;
-      const int p = mm - pimg[i] * hw;
+      const int img = mm / hw;
+      const int vid = img / d.frames_out;
+      pfr[i] = img - vid * d.frames_out + d.t_off - d.kt / 2;
+      pimg[i] = vid * d.frames_in + pfr[i];
+      const int p = mm - img * hw;
       poh[i] = p / d.w_out;
       pow_[i] = p - poh[i] * d.w_out;
     }
@@ -277,9 +281,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
       }
     } else {
       const bool kin = k < K;
-      const int tap = kin ? (int)(k / cin) : 0;
-      const int ci = (int)k - tap * cin;
-      const int dy = tap / 3, dx = tap - 3 * (tap / 3);
+      const int tap27 = kin ? (int)(k / cin) : 0;
+      const int ci = (int)k - tap27 * cin;
+      const int ks2 = d.ks * d.ks;
+      const int dt = tap27 / ks2, tap = tap27 - ks2 * dt;
+      const int dy = d.ks == 3 ? tap / 3 : 1, dx = d.ks == 3 ? tap - 3 * (tap / 3) : 1;
       const bool in0 = ci < d.k0;
       const bf16_t* base = in0 ? a0 + ci : a1 + (ci - d.k0);
       const int64_t ld = in0 ? d.lda0 : d.lda1;
@@ -287,11 +293,12 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
       for (int i = 0; i < RA; ++i) {
         int ih = poh[i] * d.stride + dy - 1;
         int iw = pow_[i] * d.stride + dx - 1;
+        const int fin = pfr[i] + dt;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (kin && prow[i] && ih >= 0 && ih < hgrid && iw >= 0 && iw < wgrid) {
+        if (kin && prow[i] && ih >= 0 && ih < hgrid && iw >= 0 && iw < wgrid && fin >= 0 && fin < d.frames_in) {
           ih >>= d.upsample;
           iw >>= d.upsample;
-          const int64_t pix = ((int64_t)pimg[i] * d.h_in + ih) * d.w_in + iw;
+          const int64_t pix = ((int64_t)(pimg[i] + dt) * d.h_in + ih) * d.w_in + iw;
           v = *(const uint4*)(base + pix * ld);
         }
         ra[i] = v;
@@ -428,14 +435,14 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.a1 ? d.a1 : d.a0), 0, d.a1 ? a1_bytes : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, w_bytes, 0x00020000);
   const int nbw = (C::NBI - wid + 7) / 8;  // this wave's B DMA instructions per K-tile
-  const int cin = MODE == VD_A_CONV3X3 ? (int)(K / 9) : 0;
+  const int cin = MODE == VD_A_CONV3X3 ? (int)(K / (d.ks * d.ks * d.kt)) : 0;
   const int hgrid = d.upsample ? 2 * d.h_in : d.h_in;
   const int wgrid = d.upsample ? 2 * d.w_in : d.w_in;
 
   // ---- issue cursor: the (unit, k-tile) whose DMA goes out next
   int iu = u_begin, ikt = 0, ikt1 = 0;
   uint32_t boff[C::NBMAX], aoff0[C::NA], aoff1[C::NA];
-  int poh[C::NA], pow_[C::NA], pimg[C::NA];
+  int poh[C::NA], pow_[C::NA], pimg[C::NA], pfr[C::NA];
   int c_tap = 0, c_ci = 0;
   bool c_new = true;
   auto unit_kr = [&](int u, int& kt0, int& kt1) {
@@ -469,8 +476,11 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
       for (int j = 0; j < C::NA; ++j) {
         int64_t m = m0 + (wid * 4 + j) * 8 + rb;
         m = m < M ? m : M - 1;
-        pimg[j] = (int)(m / hw);
-        const int p = (int)(m - (int64_t)pimg[j] * hw);
+        const int img = (int)(m / hw);
+        const int vid = img / d.frames_out;
+        pfr[j] = img - vid * d.frames_out + d.t_off - d.kt / 2;  // frame of temporal tap 0
+        pimg[j] = vid * d.frames_in + pfr[j];
+        const int p = (int)(m - (int64_t)img * hw);
         poh[j] = p / d.w_out;
         pow_[j] = p - poh[j] * d.w_out;
       }
@@ -492,14 +502,17 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     } else {
       if (c_new) {  // new tap: recompute the rows' pixel offsets
         c_new = false;
-        const int dy = c_tap / 3, dx = c_tap - 3 * dy;
+        const int ks2 = d.ks * d.ks;
+        const int dt = c_tap / ks2, t9 = c_tap - ks2 * dt;
+        const int dy = d.ks == 3 ? t9 / 3 : 1, dx = d.ks == 3 ? t9 - 3 * (t9 / 3) : 1;
 #pragma unroll
         for (int j = 0; j < C::NA; ++j) {
           int ih = poh[j] * d.stride + dy - 1, iw = pow_[j] * d.stride + dx - 1;
-          const bool ok = ih >= 0 && ih < hgrid && iw >= 0 && iw < wgrid;
+          const int fin = pfr[j] + dt;
+          const bool ok = ih >= 0 && ih < hgrid && iw >= 0 && iw < wgrid && fin >= 0 && fin < d.frames_in;
           ih >>= d.upsample;
           iw >>= d.upsample;
-          const uint32_t pix = (uint32_t)((pimg[j] * d.h_in + ih) * d.w_in + iw);
+          const uint32_t pix = (uint32_t)(((pimg[j] + dt) * d.h_in + ih) * d.w_in + iw);
           aoff0[j] = ok ? pix * (uint32_t)(d.lda0 * 2) + lc16 : G2_OOB;
           aoff1[j] = ok ? pix * (uint32_t)(d.lda1 * 2) + lc16 : G2_OOB;
         }
@@ -1651,12 +1664,23 @@ Plan plan(const vd_gemm_desc& d) {
   read_num_cus();
   Plan p;
   if (g_path == 1 || d.K % G4_BK || d.k0 % G4_BK || d.M < G2_BM || d.N < 64) return p;
-  const int64_t a_rows = d.a_mode == VD_A_CONV3X3 ? (int64_t)d.n_img * d.h_in * d.w_in : d.M;
+  const int64_t a_rows = d.a_mode == VD_A_CONV3X3
+                             ? (int64_t)d.n_img / d.frames_out * d.frames_in * d.h_in * d.w_in : d.M;
   const int64_t a0b = a_rows * d.lda0 * 2, a1b = d.a1 ? a_rows * d.lda1 * 2 : 0, wb = d.N * d.ldw * 2;
   if (a0b >= (int64_t)G2_OOB || a1b >= (int64_t)G2_OOB || wb >= (int64_t)G2_OOB) return p;
   p.a0b = (uint32_t)a0b; p.a1b = (uint32_t)a1b; p.wb = (uint32_t)wb;
   const bool cin32 = d.a_mode != VD_A_CONV3X3 || (d.K / 9) % G4_BK == 0;
-  const bool k64 = d.K % BK == 0 && d.k0 % BK == 0 && (d.a_mode != VD_A_CONV3X3 || (d.K / 9) % BK == 0);
+  const bool k64 = d.K % BK == 0 && d.k0 % BK == 0 &&
+                   (d.a_mode != VD_A_CONV3X3 || (d.K / (d.ks * d.ks * d.kt)) % BK == 0);
+  if (d.kt > 1 || d.ks == 1) {  // temporal taps: the v2 loader (or v1 when the channels do not tile by 64)
+    if (!k64) return p;
+    p.ver = 2;
+    const int64_t p128 = (d.N + 127) / 128 * 128, p160 = (d.N + 159) / 160 * 160;
+    p.bn = (p160 < p128 || (p160 == p128 && d.N % 160 == 0)) ? 160 : 128;
+    p.split = split_for(((d.M + G2_BM - 1) / G2_BM) * ((d.N + p.bn - 1) / p.bn), d.K / BK);
+    p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 : 0;
+    return p;
+  }
   // v5 (256 x 320, BK 32): forced, where K or k0 is not a multiple of 64, and on the shape
   // it wins (tools/kbench.py: the L1 attention QKV projection M 131072 x N 960 x K 320)
   const bool v5auto = d.a_mode == VD_A_DENSE && d.M >= 65536 && d.K <= 320 && d.N % 320 == 0 && d.N >= 640 &&
@@ -1723,7 +1747,20 @@ Plan plan(const vd_gemm_desc& d) {
 
 }  // namespace
 
-extern "C" int64_t vd_gemm_ws_bytes(const vd_gemm_desc* d) { return d ? plan(*d).ws_bytes : 0; }
+// kt <= 1 (a plain 2-D conv or any dense GEMM): one "frame" per video, no temporal offset,
+// so the conv loaders' temporal arithmetic reduces to the 2-D one.
+vd_gemm_desc normalized(const vd_gemm_desc& in) {
+  vd_gemm_desc d = in;
+  if (d.a_mode != VD_A_CONV3X3 || d.ks <= 0) d.ks = 3;
+  if (d.a_mode != VD_A_CONV3X3 || d.kt <= 1) {
+    d.kt = 1;
+    d.frames_in = d.frames_out = 1;
+    d.t_off = 0;
+  }
+  return d;
+}
+
+extern "C" int64_t vd_gemm_ws_bytes(const vd_gemm_desc* d) { return d ? plan(normalized(*d)).ws_bytes : 0; }
 
 // Test/benchmark hooks: force the v1 (register-staged) GEMM path / pick a path.
 extern "C" int vd_gemm_force_v1(int32_t on) {
@@ -1739,7 +1776,15 @@ extern "C" int vd_gemm_select_path(int32_t path) {
 
 extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   if (!dp) return VD_EINVAL;
-  const vd_gemm_desc& d = *dp;
+  if (dp->a_mode == VD_A_CONV3X3 && (dp->kt > 1 || dp->ks == 1)) {
+    VD_CHECK_ARG((dp->kt <= 1 || dp->kt == 3) && (dp->ks == 1 || dp->ks == 3 || dp->ks == 0));
+    VD_CHECK_ARG(dp->upsample == 0);
+  }
+  if (dp->a_mode == VD_A_CONV3X3 && dp->kt > 1) {
+    VD_CHECK_ARG(dp->frames_in > 0 && dp->frames_out > 0);
+    VD_CHECK_ARG(dp->n_img % dp->frames_out == 0 && dp->t_off >= 0 && dp->t_off + dp->frames_out <= dp->frames_in);
+  }
+  const vd_gemm_desc d = normalized(*dp);
   hipStream_t s = (hipStream_t)stream;
   VD_CHECK_ARG(d.M >= 0 && d.N > 0 && d.K > 0);
   if (d.M == 0) return VD_OK;
@@ -1755,8 +1800,8 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   if (d.res) VD_CHECK_ARG(al8(d.res) && d.ld_res % 4 == 0);
   VD_CHECK_ARG(d.act == VD_ACT_NONE || d.act == VD_ACT_SILU || d.act == VD_ACT_GEGLU || d.act == VD_ACT_GELU);
   if (d.a_mode == VD_A_CONV3X3) {
-    VD_CHECK_ARG(d.K % 9 == 0);
-    const int64_t cin = d.K / 9;
+    VD_CHECK_ARG(d.K % (d.ks * d.ks * d.kt) == 0);
+    const int64_t cin = d.K / (d.ks * d.ks * d.kt);
     VD_CHECK_ARG(cin % 8 == 0 && d.k0 <= cin);
     if (d.k0 < cin) VD_CHECK_ARG(d.a1 != nullptr);
     VD_CHECK_ARG(d.stride == 1 || d.stride == 2);
@@ -1765,7 +1810,7 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
     VD_CHECK_ARG(d.M == (int64_t)d.n_img * d.h_out * d.w_out);
     if (d.upsample) VD_CHECK_ARG(d.h_out == 2 * d.h_in && d.w_out == 2 * d.w_in);
     else VD_CHECK_ARG(d.h_out == (d.h_in - 1) / d.stride + 1 && d.w_out == (d.w_in - 1) / d.stride + 1);
-    VD_CHECK_ARG((int64_t)d.n_img * d.h_in * d.w_in < 0x7fffffff);
+    VD_CHECK_ARG((int64_t)d.n_img / d.frames_out * d.frames_in * d.h_in * d.w_in < 0x7fffffff);
   } else {
     VD_CHECK_ARG(d.a_mode == VD_A_DENSE);
     if (d.k0 < d.K) VD_CHECK_ARG(d.a1 != nullptr);

@@ -78,6 +78,7 @@ class GemmDesc(C.Structure):
         ("act", c_i32),
         ("out", c_vp), ("ldc", c_i64), ("out_f32", c_i32),
         ("ws", c_vp), ("ws_bytes", c_i64),
+        ("kt", c_i32), ("ks", c_i32), ("frames_in", c_i32), ("frames_out", c_i32), ("t_off", c_i32),
     ]
 
 

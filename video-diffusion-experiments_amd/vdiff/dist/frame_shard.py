@@ -69,6 +69,32 @@ class FrameShard:
         recv = self._a2a(send)                                      # (r,  b, f_loc, pl)  r = position chunk
         return transpose(recv, W, batch * frames_local, pl)         # (b, f_loc, r, pl) = (b, f_loc, p)
 
+    # -- temporal conv halo ------------------------------------------------------
+    def halo_frames(self, x: torch.Tensor, batch: int, frames_local: int, hw: int) -> torch.Tensor:
+        """rows (b, f_loc, p) -> rows (b, f_loc + 2, p): every video's local frames between the
+        last frame of the previous rank and the first frame of the next (zeros at the video's
+        ends = the conv's temporal zero padding) — the one-frame halo a kt = 3 temporal conv
+        (ops.conv3d with frames_in = f_loc + 2, t_off = 1) needs under frame sharding.  Point to
+        point: each rank sends 2 frames per video to each neighbour."""
+        C = x.shape[1]
+        W, r = self.world, self.rank
+        v = x.view(batch, frames_local, hw, C)
+        first, last = v[:, 0].contiguous(), v[:, -1].contiguous()
+        left = torch.zeros_like(first)
+        right = torch.zeros_like(last)
+        g = (lambda k: dist.get_global_rank(self.group, k)) if self.group is not None else (lambda k: k)
+        ops = []
+        if r > 0:
+            ops += [dist.P2POp(dist.isend, first, g(r - 1), self.group),
+                    dist.P2POp(dist.irecv, left, g(r - 1), self.group)]
+        if r < W - 1:
+            ops += [dist.P2POp(dist.isend, last, g(r + 1), self.group),
+                    dist.P2POp(dist.irecv, right, g(r + 1), self.group)]
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return torch.cat([left[:, None], v, right[:, None]], 1).reshape(-1, C)
+
     def all_gather_frames(self, x: torch.Tensor) -> torch.Tensor:
         """(B, C, F_loc, H, W) latents of every rank -> (B, C, F, H, W)."""
         parts = torch.empty(self.world * x.numel(), device=x.device, dtype=x.dtype)

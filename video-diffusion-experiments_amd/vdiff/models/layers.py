@@ -71,6 +71,12 @@ def pack_conv3x3(wt: torch.Tensor, cin_pad: Optional[int] = None) -> torch.Tenso
     return w.reshape(co, -1).to(torch.bfloat16).contiguous()
 
 
+def pack_conv3d(wt: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, kt, ks, ks] -> [Cout, kt*ks*ks*Cin] with K = (dt*ks*ks + tap)*Cin + ci."""
+    co = wt.shape[0]
+    return wt.detach().permute(0, 2, 3, 4, 1).reshape(co, -1).to(torch.bfloat16).contiguous()
+
+
 def pack_geglu(w: torch.Tensor) -> torch.Tensor:
     """Interleave the hidden/gate halves of GEGLU.proj in 16-row blocks
     (hidden block i, gate block i, ...) so both halves of an output column land
@@ -173,6 +179,29 @@ class Conv2d(nn.Conv2d):
         out, ho, wo = ops.conv3x3(rows, n, h, w, self._w, stride=self.stride[0], bias=self._b,
                                   out_f32=self.out_f32)
         return rows_fmap(out, (n, self.out_channels, ho, wo))
+
+
+class Conv3d(nn.Conv3d):
+    """torch.nn.Conv3d over (B, C, T, H, W) videos, kernel (kt, ks, ks) with kt in {1, 3},
+    ks in {1, 3}, padding (kt//2, ks//2, ks//2), stride (1, s, s) — the north star's 3-D /
+    (2+1)D conv (kernel (3,3,3), or (1,3,3) then (3,1,1)) on the implicit-GEMM MFMA kernel
+    with temporal taps; (1,3,3) is the reference's per-frame conv."""
+
+    def prepare(self):
+        kt, ks, ks2 = self.kernel_size
+        if kt not in (1, 3) or ks != ks2 or ks not in (1, 3) or self.padding != (kt // 2, ks // 2, ks // 2) \
+                or self.stride[0] != 1 or self.stride[1] != self.stride[2] or self.in_channels % 8:
+            raise NotImplementedError(f"Conv3d kernel {self.kernel_size} pad {self.padding} stride {self.stride}")
+        self._w, self._b = pack_conv3d(self.weight), f32(self.bias)
+
+    def forward(self, x):
+        if x.dim() != 5:
+            raise ValueError(f"Conv3d expects (B, C, T, H, W), got {tuple(x.shape)}")
+        b, c, t, h, w = x.shape
+        kt, ks, _ = self.kernel_size
+        out, ho, wo = ops.conv3d(fmap_rows(x), b, t, h, w, self._w, kt=kt, ks=ks, stride=self.stride[1],
+                                 bias=self._b)
+        return rows_fmap(out, (b, self.out_channels, t, ho, wo))
 
 
 class GroupNorm(nn.GroupNorm):

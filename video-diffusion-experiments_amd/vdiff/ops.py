@@ -111,6 +111,38 @@ def conv3x3(x, n_img, h_in, w_in, w, *, x1=None, stride=1, upsample=False, bias=
     return out, h_out, w_out
 
 
+def conv3d(x, batch, frames_in, h_in, w_in, w, *, kt=3, ks=3, frames_out=None, t_off=0, stride=1, bias=None,
+           rowbias=None, rb_div=1, res=None, act=ACT_NONE, out=None, out_f32=False):
+    """kt x ks x ks conv (pad kt/2, ks/2; spatial stride 1/2, temporal stride 1) over the frames
+    of each video: x = NHWC rows of batch*frames_in images, w packed [Cout][kt][ks][ks][Cin]
+    (K = (dt*ks*ks + tap)*Cin + ci, pack_conv3d).  Output frame f of a video reads input frames
+    f + t_off + dt - kt/2 (zero outside [0, frames_in)): frames_out = frames_in, t_off = 0 is
+    the plain 3-D conv; a frame-sharded rank passes halo'd frames (frames_in = frames_out + 2,
+    t_off = 1).  ks = 1, kt = 3 is the temporal half of a (2+1)D conv."""
+    _dev(x, w, bias, rowbias, res, out)
+    frames_out = frames_in if frames_out is None else frames_out
+    N, K = w.shape
+    cin = x.shape[1]
+    if K != kt * ks * ks * cin:
+        raise ValueError(f"conv3d weight K={K} != kt*ks*ks*Cin = {kt * ks * ks * cin}")
+    if x.shape[0] != batch * frames_in * h_in * w_in:
+        raise ValueError("conv3d input rows != batch*frames_in*h*w")
+    h_out, w_out = (h_in - 1) // stride + 1, (w_in - 1) // stride + 1
+    n_img = batch * frames_out
+    M = n_img * h_out * w_out
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=torch.float32 if out_f32 else BF16)
+    d = GemmDesc(a0=_p(x), lda0=_rows(x), k0=cin, a1=None, lda1=0, a_mode=A_CONV3X3,
+                 n_img=n_img, h_in=h_in, w_in=w_in, h_out=h_out, w_out=w_out, stride=stride, upsample=0,
+                 w=_p(w), ldw=_rows(w), M=M, N=N, K=K, bias=_p(bias), rowbias=_p(rowbias),
+                 ld_rb=rowbias.stride(0) if rowbias is not None else 0, rb_div=rb_div,
+                 res=_p(res), ld_res=_rows(res) if res is not None else 0, act=act,
+                 out=_p(out), ldc=_rows(out, torch.float32 if out_f32 else BF16), out_f32=int(out_f32),
+                 kt=kt, ks=ks, frames_in=frames_in, frames_out=frames_out, t_off=t_off)
+    _run_gemm(d, x.device, "vd_gemm(conv3d)")
+    return out, h_out, w_out
+
+
 # ---------------------------------------------------------------- norms
 def gn_splits(n_inst: int, pix: int) -> int:
     """Pixel splits per instance for vd_gn_partial: ~2048 partial blocks in total, at
