@@ -173,6 +173,11 @@ int vd_attention(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
 /* Test/benchmark hook: on != 0 routes d = 40 to the 16x16x32 flash kernel instead of
  * the 32x32x16 one (default). */
 int vd_attention_force_v1(int32_t on);
+/* Test/benchmark hook: the d = 40 kernel — 0 = automatic (flash32), 1 = the 16x16x32 flash
+ * kernel, 2 = flash32 (4 waves, 32x32x16), 3 = flash32pp (8 waves: two staggered groups
+ * software-pipelined PV(t-1)+QK(t) | softmax(t); bitwise equal to flash32, measured slower —
+ * tools/attn_ab.py). */
+int vd_attention_select(int32_t kernel);
 
 /* Temporal (motion-module) self-attention over frames (a9): token (b, f, p) is
  * row (b*frames + f)*positions + p of q/k/v/o (the NHWC layout, no permute);
@@ -208,6 +213,30 @@ int vd_softmax_rows(const float* s, int64_t ld_s, int64_t rows, int64_t cols, vo
  * (f < frames-2; sad may be NULL when frames == 2).  2 <= frames <= 32. */
 int vd_frame_metrics(const void* frames_u8, int64_t videos, int32_t frames, int64_t bytes_per_frame,
                      uint64_t* sse, uint64_t* sad, vd_stream_t stream);
+
+/* Dense optical flow of every consecutive frame pair (replaces
+ * OpticalFlowEstimator.compute_flow, experiments/06_measure_grid_search.py:163-188 =
+ * cv2.calcOpticalFlowFarneback(grey_f, grey_f+1, None, pyr_scale, levels, winsize,
+ * iterations, poly_n, poly_sigma, flags=0) with grey = uint8(mean_c(x/255)*255), :173).
+ * frames_u8: [videos][frames][H][W][3] uint8; flow out: fp32 [videos][frames-1][H][W][2]
+ * (dx, dy); poly_n 5 or 7; workspace: at least the byte count vd_farneback_workspace
+ * returns for the same sizes (-1 on bad sizes), device memory. */
+int64_t vd_farneback_workspace(int64_t videos, int32_t frames, int32_t H, int32_t W);
+int vd_farneback_flow(const void* frames_u8, int64_t videos, int32_t frames, int32_t H, int32_t W,
+                      double pyr_scale, int32_t levels, int32_t winsize, int32_t iterations,
+                      int32_t poly_n, double poly_sigma, float* flow, void* workspace,
+                      int64_t workspace_bytes, vd_stream_t stream);
+
+/* Flow magnitude moments and warp error per pair (06:190-199 compute_flow_stats,
+ * :259-284 warp_frame, :336-337): stats [videos*(frames-1)][3] fp64 =
+ * { sum |flow|, sum |flow|^2 over H*W, sum over 3*H*W of (warp(frame_f, flow) - frame_f+1)^2 }
+ * with frames as u8/255, warp = grid_sample(bilinear, border, align_corners=True) at
+ * (x + dx, y + dy).  Deterministic (fixed-order partials in the workspace: at least the
+ * byte count vd_flow_warp_workspace returns). */
+int64_t vd_flow_warp_workspace(int64_t videos, int32_t frames);
+int vd_flow_warp_stats(const void* frames_u8, const float* flow, int64_t videos, int32_t frames,
+                       int32_t H, int32_t W, double* stats, void* workspace, int64_t workspace_bytes,
+                       vd_stream_t stream);
 
 /* ---------------------------------------------------------------- step glue
  * vd_timestep_embed: diffusers Timesteps(dim, flip_sin_to_cos=True, shift 0)

@@ -18,8 +18,10 @@ resize(INTER_LINEAR)), restated below step by step in numpy with OpenCV's border
 coefficient tables and float32/float64 split.  PARITY is pinned by the reference's own
 records — `outputs/06_grid_search_metrics/*_metrics.json` hold per-pair
 flow_magnitude_mean / flow_magnitude_std / warp_error computed by the reference from the
-frames in `outputs/05_grid_search/*/frames` (tests/test_flow_oracle.py states the deviation
-achieved; OpenCV's SIMD summation order is not reproducible bit for bit).
+frames in `outputs/05_grid_search/*/frames`; tests/golden/make_metrics_golden.py runs this
+restatement over all 78 measured videos and records the largest relative deviation per field
+in tests/golden/metrics/oracle_vs_reference.json (~1e-6: OpenCV's SIMD summation order is not
+reproduced bit for bit), and tests/test_flow_oracle.py re-checks the committed video.
 """
 from __future__ import annotations
 
@@ -314,3 +316,16 @@ def pair_metrics(f1: torch.Tensor, f2: torch.Tensor) -> dict:
     warped = warp_frame(f1, flow)
     return {"flow_magnitude_mean": st["magnitude_mean"], "flow_magnitude_std": st["magnitude_std"],
             "warp_error": F.mse_loss(warped, f2).item(), "flow": flow}
+
+
+def video_flow_metrics(frames_u8: np.ndarray) -> dict:
+    """Flow / warp part of 06's measure_video_metrics (06:320-383) over [F, H, W, 3] uint8
+    frames (05's PNGs as 06:97-113 loads them: float / 255, [C, H, W])."""
+    fr = torch.from_numpy(frames_u8).permute(0, 3, 1, 2).float() / 255
+    pairs = [pair_metrics(fr[i], fr[i + 1]) for i in range(len(fr) - 1)]
+    mags = [p["flow_magnitude_mean"] for p in pairs]
+    warps = [p["warp_error"] for p in pairs]
+    return {"frame_metrics": [{k: p[k] for k in ("flow_magnitude_mean", "flow_magnitude_std", "warp_error")}
+                              for p in pairs],
+            "mean_flow_magnitude": float(np.mean(mags)), "flow_magnitude_variance": float(np.var(mags)),
+            "mean_warp_error": float(np.mean(warps)), "warp_error_variance": float(np.var(warps))}

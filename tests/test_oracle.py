@@ -177,7 +177,8 @@ def test_metrics_oracle_pinned_to_reference_records():
         assert got[k] == pytest.approx(ref[k], rel=1e-6), k
     sweep = json.loads((GOLD / "metrics" / "oracle_vs_reference.json").read_text())
     assert sweep["experiments"] == 78
-    assert max(sweep["max_relative_deviation"].values()) < 1e-6
+    exact = {k: v for k, v in sweep["max_relative_deviation"].items() if "flow" not in k and "warp" not in k}
+    assert max(exact.values()) < 1e-6  # the flow / warp fields: tests/test_flow_oracle.py
 
 
 def test_bf16_realisation_floor():

@@ -32,7 +32,7 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int KT = 64;   // keys per tile
-int g_flash32 = 1;       // d = 40 on the 32x32x16 kernel (vd_attention_force_v1 turns it off)
+int g_flash32 = 1;       // d = 40: 1 = flash32 (4-wave, default), 2 = flash32pp (8-wave pipeline), 0 = flash_attn 16x16x32
 
 template <int D>
 struct AttnCfg {
@@ -714,12 +714,370 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
   }
 }
 
+// ============================================================ flash32pp
+// flash32 as a software pipeline over two staggered wave groups (FA3-style ping-pong;
+// MI355X_MICROARCH.md "Two waves per SIMD" items 1-3 and 9).  Each wave's tile work is
+// split into
+//     M(t) = PV(t-1) + QK^T(t)        — MFMA only (16 + 12 x 32x32x16)
+//     V(t) = the softmax of tile t    — VALU only (tile max / rescale, exp2, bf16 pack)
+// with tile t's P fragments kept in registers from V(t) to M(t+1), and group 1 (waves
+// 4-7) runs one barrier behind group 0: on every SIMD one wave issues MFMAs while its
+// partner does its VALU.  (In the 4-wave flash32 both waves of a SIMD reached the same
+// phase together: a 64x64 tile cost ~1800 cycles per wave against 896 of MFMA.)
+// Barriers: every interval ends with one; the group leaving M waits for its LDS traffic
+// first (__syncthreads), the group leaving V passes a raw s_barrier (the next tile's
+// global loads stay in flight).  LDS: three K/V buffers, tile t in buffer t % 3; group 0
+// issues the global loads of tile t+2 at the start of V(t) and writes them in M(t+1)
+// (interval 2t+2), when buffer (t+2) % 3 = (t-1) % 3 was last read by group 1's M(t)
+// (V of tile t-1) in interval 2t+1.  512 queries per workgroup share each K/V tile.
+__device__ __forceinline__ void bar_raw() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int D>
+__device__ __forceinline__ void f32_qk(const bf16_t* kl, int r32, int hh, const bf16x8 (&kfr)[2][F32Cfg<D>::KSTEPS],
+                                       const bf16x8 (&qf)[2][F32Cfg<D>::KSTEPS], f32x16 (&s)[2][2]) {
+  using C = F32Cfg<D>;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+    for (int ks = 0; ks < C::KSTEPS; ++ks) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        if (ks == 0) {
+          f32x16 z;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) z[i] = 0.f;
+          s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], z, 0, 0, 0);
+        } else {
+          s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], s[kb][qb], 0, 0, 0);
+        }
+      }
+    }
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void f32_read_k(const bf16_t* kl, int r32, int hh, bf16x8 (&kfr)[2][F32Cfg<D>::KSTEPS]) {
+  using C = F32Cfg<D>;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int ks = 0; ks < C::KSTEPS; ++ks)
+      kfr[kb][ks] = *(const bf16x8*)(kl + (kb * 32 + r32) * C::KS + ks * 16 + 8 * hh);
+}
+
+template <int D, bool UNITC, bool EXACT>
+__device__ __forceinline__ bool f32pp_loop(bf16_t* lds, const bf16_t* kb_ptr, const bf16_t* vb_ptr, int ldk32,
+                                           int ldv32, int64_t skv, const int (&krow)[F32Cfg<D>::LREG],
+                                           const uint32_t (&kcol)[F32Cfg<D>::LREG],
+                                           const uint32_t (&ldsk)[F32Cfg<D>::LREG],
+                                           const uint32_t (&ldsv)[F32Cfg<D>::LREG],
+                                           bf16x8 (&qf)[2][F32Cfg<D>::KSTEPS], f32x16 (&oacc)[F32Cfg<D>::NDB][2],
+                                           int r32, int hh, int vtr, float c, bool g0) {
+  using C = F32Cfg<D>;
+  constexpr int QB = 2;
+  constexpr float RESCALE = 4294967296.0f;        // 2^32
+  constexpr float BAD = 1.2676506002282294e30f;   // 2^100
+#pragma unroll
+  for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[db][qb][i] = 0.f;
+  float mu[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) mu[qb] = 0.f;
+  bool bad = false;
+
+  const int ntiles = (int)((skv + KT - 1) / KT);
+  const bool ragged = (skv % KT) != 0;
+  stage_t<C::LREG> kvst;
+  if (g0) {  // tiles 0 and 1 before the loop
+    kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, 0, skv, krow, kcol);
+    kv_store<C::LREG>(kvst, lds, lds, ldsk, ldsv);
+    if (ntiles > 1) {
+      kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, 1, skv, krow, kcol);
+      kv_store<C::LREG>(kvst, lds + C::STAGE, lds + C::STAGE, ldsk, ldsv);
+    }
+  }
+  __syncthreads();
+  if (!g0) bar_raw();  // the stagger: group 1 runs one barrier behind
+
+  // ---- M(0): QK^T of tile 0
+  f32x16 s[2][QB];
+  {
+    bf16x8 kfr[2][C::KSTEPS];
+    f32_read_k<D>(lds, r32, hh, kfr);
+    f32_qk<D>(lds, r32, hh, kfr, qf, s);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    // ================= V(t): softmax of tile t -> pf (group 0 also issues tile t+2's loads)
+    if (g0 && t + 2 < ntiles) kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, t + 2, skv, krow, kcol);
+    if (ragged && t == ntiles - 1) {
+      const int kvalid = (int)(skv - (int64_t)t * KT);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (key >= kvalid) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) s[kb][qb][i] = -INFINITY;
+          }
+        }
+    }
+    if (EXACT || t == 0) {
+      float tm[QB];
+      bool need = t == 0;
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const float m = tile_max(s[0][qb], s[1][qb]);
+        tm[qb] = vmax2(m, partner32(m));
+        need |= (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
+      }
+      if (__any(need)) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          const bool up = t == 0 || (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
+          const float nmu = up ? (float)(__bf16)(mu[qb] + tm[qb]) : mu[qb];
+          const float delta = nmu - mu[qb];
+          const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
+          mu[qb] = nmu;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[kb][qb][i] -= delta;
+#pragma unroll
+          for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
+          if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
+        }
+      }
+    }
+    if (!EXACT && t > 1) {  // fast pass: rescale from the row sum of tiles 0..t-1 past 2^32
+      float lq[QB];
+      bool resc = false, over = false;
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const float lown = oacc[C::L_DB][qb][C::L_I];
+        const float lp = partner32(lown);
+        lq[qb] = hh == C::L_H ? lown : lp;
+        resc |= lq[qb] > RESCALE;
+        over |= !(lq[qb] < BAD);
+      }
+      if (__any(over)) {
+        bad = true;
+      } else if (__any(resc)) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          const float step = lq[qb] > RESCALE ? __builtin_amdgcn_logf(lq[qb]) : 0.f;
+          const float nmu = (float)(__bf16)(mu[qb] + (UNITC ? step : step / c));
+          const float delta = nmu - mu[qb];
+          const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
+          mu[qb] = nmu;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[kb][qb][i] -= delta;
+#pragma unroll
+          for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
+          if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
+        }
+      }
+    }
+    bf16x8 pf[2][2][QB];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            f[j] = (__bf16)__builtin_amdgcn_exp2f(UNITC ? s[kb][qb][8 * s2 + j] : s[kb][qb][8 * s2 + j] * c);
+          pf[kb][s2][qb] = f;
+        }
+    bar_raw();  // end of V(t)
+
+    // ================= M(t+1): PV(t) + QK^T(t+1); group 0 writes tile t+2
+    {
+      const bf16_t* vl = lds + (t % 3) * C::STAGE + C::K_ELEMS;
+      bf16x8 vfr[C::NDB][2][2];
+#pragma unroll
+      for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16_t* p0 = vl + (db * KT + kb * 32 + 16 * s2) * 32 + vtr;
+            const bf16x4 lo =
+                __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(p0));
+            const bf16x4 hi =
+                __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(p0 + 8 * 32));
+            vfr[db][kb][s2] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          }
+#pragma unroll
+      for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+              oacc[db][qb] =
+                  __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[db][kb][s2], pf[kb][s2][qb], oacc[db][qb], 0, 0, 0);
+      // P and the V fragments die here; keep QK^T's accumulators from overlapping them
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 1 < ntiles) {
+        bf16x8 kfr[2][C::KSTEPS];
+        f32_read_k<D>(lds + ((t + 1) % 3) * C::STAGE, r32, hh, kfr);
+        f32_qk<D>(lds, r32, hh, kfr, qf, s);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (g0 && t + 2 < ntiles) {
+        bf16_t* nb = lds + ((t + 2) % 3) * C::STAGE;
+        kv_store<C::LREG>(kvst, nb, nb, ldsk, ldsv);
+      }
+    }
+    __syncthreads();  // end of M(t+1): tile t+2's LDS writes (group 0) complete
+  }
+  if (g0) bar_raw();  // balance the stagger
+  if (!EXACT) {
+    bool over = false;
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      const float lown = oacc[C::L_DB][qb][C::L_I];
+      const float lp = partner32(lown);
+      over |= !((hh == C::L_H ? lown : lp) < BAD);
+    }
+    bad |= __any(over);
+  }
+  return bad;
+}
+
+template <int D, bool UNITC>
+__global__ __launch_bounds__(2 * NT, 1) void flash32pp_kernel(
+    const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
+    const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
+    int64_t sq, int64_t skv, int64_t kv_div, float c) {
+  using C = F32Cfg<D>;
+  constexpr int QB = 2;
+  constexpr int QWG = 8 * 32 * QB;  // queries per workgroup
+  __shared__ __attribute__((aligned(16))) bf16_t lds[3 * C::STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool g0 = wave < 4;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int nqb = (int)((sq + QWG - 1) / QWG);
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qblk = lid % nqb;
+  const int h = (lid / nqb) % heads;
+  const int64_t b = (lid / nqb) / heads;
+  const int64_t q0 = (int64_t)qblk * QWG + wave * (32 * QB);
+  const int64_t bkv = b / kv_div;
+  const bf16_t* qb_ptr = q + b * sq * ldq + (int64_t)h * D;
+  const bf16_t* kb_ptr = k + bkv * skv * ldk + (int64_t)h * D;
+  const bf16_t* vb_ptr = v + bkv * skv * ldv + (int64_t)h * D;
+
+  bf16x8 qf[QB][C::KSTEPS];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    const int64_t qi = q0 + qb * 32 + r32;
+#pragma unroll
+    for (int ks = 0; ks < C::KSTEPS; ++ks) {
+      const int dd = ks * 16 + 8 * hh;
+      uint4 u = make_uint4(0, 0, 0, 0);
+      if (qi < sq && dd < D) u = *(const uint4*)(qb_ptr + qi * ldq + dd);
+      qf[qb][ks] = __builtin_bit_cast(bf16x8, u);
+    }
+  }
+  for (int idx = tid; idx < 3 * KT; idx += 2 * NT) {
+    const int buf = idx / KT, r = idx % KT;
+    bf16_t* kl = lds + buf * C::STAGE;
+    bf16_t* vl = kl + C::K_ELEMS;
+    for (int cc = C::DCH; cc < C::DK / 8; ++cc)
+      *(uint4*)(kl + r * C::KS + cc * 8) = make_uint4(cc == C::DCH ? 0x3F80u : 0u, 0, 0, 0);
+    for (int cc = C::DCH; cc < C::DVP / 8; ++cc)
+      *(uint4*)(vl + ((cc >> 2) * KT + r) * 32 + (cc & 3) * 8) = make_uint4(cc == C::DCH ? 0x3F80u : 0u, 0, 0, 0);
+  }
+  // staging slots of group 0's 256 threads (group 1 never stages)
+  const int st = tid & (NT - 1);
+  int krow[C::LREG];
+  uint32_t kcol[C::LREG], ldsk[C::LREG], ldsv[C::LREG];
+#pragma unroll
+  for (int i = 0; i < C::LREG; ++i) {
+    const int idx = (st + i * NT) % (KT * C::DCH);
+    const int r = idx / C::DCH, cc = idx % C::DCH;
+    krow[i] = r;
+    kcol[i] = (uint32_t)(cc * 8);
+    ldsk[i] = (uint32_t)(r * C::KS + cc * 8);
+    ldsv[i] = (uint32_t)(C::K_ELEMS + ((cc >> 2) * KT + r) * 32 + (cc & 3) * 8);
+  }
+  const int ldk32 = (int)ldk, ldv32 = (int)ldv;
+  const int g16 = lane >> 4, i16 = lane & 15;
+  const int vtr = ((4 * hh + (i16 >> 2)) * 32) + 16 * (g16 & 1) + 4 * (i16 & 3);
+  f32x16 oacc[C::NDB][QB];
+  const bool bad = f32pp_loop<D, UNITC, false>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv,
+                                               qf, oacc, r32, hh, vtr, c, g0);
+  if (__syncthreads_or(bad)) {
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb)
+      if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)0.0f;
+    f32pp_loop<D, UNITC, true>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv, qf, oacc, r32, hh,
+                               vtr, c, g0);
+  }
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    const float lown = oacc[C::L_DB][qb][C::L_I];
+    const float lp = partner32(lown);
+    const float l = hh == C::L_H ? lown : lp;
+    const float inv = __builtin_amdgcn_rcpf(l);
+    const int64_t qi = q0 + qb * 32 + r32;
+    bf16_t* orow = o + (b * sq + (qi < sq ? qi : 0)) * ldo + (int64_t)h * D;
+#pragma unroll
+    for (int db = 0; db < C::NDB; ++db) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const f32x16& a = oacc[db][qb];
+        uint32_t x0 = pack2(a[8 * m + 0] * inv, a[8 * m + 1] * inv), x1 = pack2(a[8 * m + 2] * inv, a[8 * m + 3] * inv);
+        uint32_t y0 = pack2(a[8 * m + 4] * inv, a[8 * m + 5] * inv), y1 = pack2(a[8 * m + 6] * inv, a[8 * m + 7] * inv);
+        auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+        auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+        const int dd = 32 * db + 16 * m + 8 * hh;
+        if (qi < sq && dd + 8 <= D) *(uint4*)(orow + dd) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+    }
+  }
+}
+
 template <int D>
 int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                  void* o, int64_t ldo, int64_t batch, int heads, int64_t sq, int64_t skv,
                  int64_t kv_div, float scale, hipStream_t s) {
   const float c = scale * 1.4426950408889634f;
   if constexpr (D == 40) {
+    if (g_flash32 == 2 && ((uintptr_t)o & 15) == 0 && ldo % 8 == 0) {  // ping-pong 8-wave kernel
+      const int64_t nblk = (sq + 511) / 512 * heads * batch;
+      if (nblk > 0x7fffffff) return VD_EINVAL;
+      const dim3 grid((unsigned)nblk);
+      if (c == 1.0f)
+        hipLaunchKernelGGL((flash32pp_kernel<D, true>), grid, dim3(2 * NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
+      else
+        hipLaunchKernelGGL((flash32pp_kernel<D, false>), grid, dim3(2 * NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
+      return vd_launch_status();
+    }
     if (g_flash32 && ((uintptr_t)o & 15) == 0 && ldo % 8 == 0) {
       const int64_t nblk = (sq + 255) / 256 * heads * batch;
       if (nblk > 0x7fffffff) return VD_EINVAL;
@@ -1159,7 +1517,15 @@ int g_temporal_valu = 0;  // vd_temporal_force_valu
 
 // Test/benchmark hook: route d = 40 to the 16x16x32 kernel instead of flash32.
 extern "C" int vd_attention_force_v1(int32_t on) {
-  g_flash32 = !on;
+  g_flash32 = on ? 0 : 1;
+  return VD_OK;
+}
+
+// Test/benchmark hook: the d = 40 kernel — 0 = automatic (flash32pp), 1 = flash_attn (16x16x32),
+// 2 = flash32 (4-wave 32x32x16), 3 = flash32pp (8-wave ping-pong).
+extern "C" int vd_attention_select(int32_t kernel) {
+  if (kernel < 0 || kernel > 3) return VD_EINVAL;
+  g_flash32 = kernel == 1 ? 0 : (kernel == 3 ? 2 : 1);
   return VD_OK;
 }
 

@@ -28,6 +28,7 @@ SIGNATURES = {
     "vd_gemm_force_v1": ([c_i32], c_i32),
     "vd_gemm_select_path": ([c_i32], c_i32),
     "vd_attention_force_v1": ([c_i32], c_i32),
+    "vd_attention_select": ([c_i32], c_i32),
     "vd_temporal_force_valu": ([c_i32], c_i32),
     "vd_gemm_ws_bytes": ([c_vp], c_i64),
     "vd_gn_partial": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp], c_i32),
@@ -42,6 +43,11 @@ SIGNATURES = {
     "vd_temporal_attention_rope": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_f32, c_vp], c_i32),
     "vd_softmax_rows": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
     "vd_frame_metrics": ([c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp], c_i32),
+    "vd_farneback_workspace": ([c_i64, c_i32, c_i32, c_i32], c_i64),
+    "vd_farneback_flow": ([c_vp, c_i64, c_i32, c_i32, c_i32, C.c_double, c_i32, c_i32, c_i32, c_i32, C.c_double,
+                           c_vp, c_vp, c_i64, c_vp], c_i32),
+    "vd_flow_warp_workspace": ([c_i64, c_i32], c_i64),
+    "vd_flow_warp_stats": ([c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp], c_i32),
     "vd_timestep_embed": ([c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp], c_i32),
     "vd_pack_latents": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i64, c_f32, c_vp], c_i32),
     "vd_unpack_nhwc": ([c_vp, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp], c_i32),

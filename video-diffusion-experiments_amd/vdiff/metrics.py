@@ -5,10 +5,11 @@ read like its load_frames (:97-113: sorted frame_*.png, PIL RGB), and per video 
 consecutive-pair MSE / PSNR (:209-218), their mean / population std, and the flicker
 index (:221-235) are reported under the reference's JSON keys.  The pixel work — every
 byte of every frame, for a whole batch of videos — is one pass of the HIP kernel
-vd_frame_metrics (exact integer sums); the host only forms the scalars.  LPIPS (AlexNet
-weights) and the Farneback flow / warp error (OpenCV) have no offline counterpart here:
-their fields are None, and temporal_consistency_score is formed only when per-pair LPIPS
-values are supplied.
+vd_frame_metrics (exact integer sums); the host only forms the scalars.  The optical-flow
+fields (06:163-199 Farneback flow magnitude, :259-284 warp error) come from the HIP
+Farneback pipeline vd_farneback_flow + vd_flow_warp_stats over every pair of the batch.
+LPIPS (AlexNet weights) has no offline counterpart here: its fields are None, and
+temporal_consistency_score is formed only when per-pair LPIPS values are supplied.
 """
 from __future__ import annotations
 
@@ -46,6 +47,62 @@ def frame_sums(videos_u8: torch.Tensor):
     return sse, sad
 
 
+# OpticalFlowEstimator.compute_flow's cv2 arguments (06:176-186)
+FARNEBACK = dict(pyr_scale=0.5, levels=3, winsize=15, iterations=3, poly_n=5, poly_sigma=1.2)
+
+
+def _u8_videos(videos_u8: torch.Tensor) -> torch.Tensor:
+    if not videos_u8.is_cuda or videos_u8.dtype != torch.uint8 or videos_u8.dim() != 5 or videos_u8.shape[-1] != 3:
+        raise ValueError("takes a uint8 CUDA tensor [videos, frames, H, W, 3] (no CPU fallback)")
+    return videos_u8.contiguous()
+
+
+def farneback_flow(videos_u8: torch.Tensor, **params) -> torch.Tensor:
+    """uint8 [V, F, H, W, 3] on the GPU -> flow fp32 [V, F-1, H, W, 2]: cv2.calcOpticalFlowFarneback
+    of every consecutive grey pair (06:163-188), parameters as 06 passes them unless overridden."""
+    x = _u8_videos(videos_u8)
+    V, Fr, H, W = x.shape[:4]
+    p = {**FARNEBACK, **params}
+    ws_bytes = lib().vd_farneback_workspace(V, Fr, H, W)
+    if ws_bytes < 0:
+        raise ValueError(f"bad video shape {tuple(x.shape)}")
+    ws = torch.empty(ws_bytes, device=x.device, dtype=torch.uint8)
+    flow = torch.empty(V, Fr - 1, H, W, 2, device=x.device, dtype=torch.float32)
+    stream = torch.cuda.current_stream().cuda_stream
+    check(lib().vd_farneback_flow(x.data_ptr(), V, Fr, H, W, p["pyr_scale"], p["levels"], p["winsize"],
+                                  p["iterations"], p["poly_n"], p["poly_sigma"], flow.data_ptr(), ws.data_ptr(),
+                                  ws_bytes, stream), "vd_farneback_flow")
+    return flow
+
+
+def flow_sums(videos_u8: torch.Tensor, flow: torch.Tensor) -> torch.Tensor:
+    """-> fp64 [V, F-1, 3] = {sum |flow|, sum |flow|^2, sum (warp_frame(f, flow) - f')^2}."""
+    x = _u8_videos(videos_u8)
+    V, Fr, H, W = x.shape[:4]
+    if tuple(flow.shape) != (V, Fr - 1, H, W, 2) or flow.dtype != torch.float32 or not flow.is_cuda:
+        raise ValueError("flow must be fp32 CUDA [V, F-1, H, W, 2]")
+    flow = flow.contiguous()
+    ws_bytes = lib().vd_flow_warp_workspace(V, Fr)
+    ws = torch.empty(ws_bytes, device=x.device, dtype=torch.uint8)
+    stats = torch.empty(V, Fr - 1, 3, device=x.device, dtype=torch.float64)
+    stream = torch.cuda.current_stream().cuda_stream
+    check(lib().vd_flow_warp_stats(x.data_ptr(), flow.data_ptr(), V, Fr, H, W, stats.data_ptr(), ws.data_ptr(),
+                                   ws_bytes, stream), "vd_flow_warp_stats")
+    return stats
+
+
+def flow_fields(stats, hw: int) -> dict:
+    """One video's [F-1, 3] flow sums -> the per-pair and aggregate flow / warp fields of the
+    reference's record (06:190-199 magnitude mean / population std, :336-338, :379-383)."""
+    mag_mean = [s[0] / hw for s in stats]
+    mag_std = [float(np.sqrt(max(s[1] / hw - (s[0] / hw) ** 2, 0.0))) for s in stats]
+    warp = [s[2] / (3 * hw) for s in stats]
+    return {"mean_flow_magnitude": float(np.mean(mag_mean)), "flow_magnitude_variance": float(np.var(mag_mean)),
+            "mean_warp_error": float(np.mean(warp)), "warp_error_variance": float(np.var(warp)),
+            "pairs": [{"flow_magnitude_mean": m, "flow_magnitude_std": sd, "warp_error": w}
+                      for m, sd, w in zip(mag_mean, mag_std, warp)]}
+
+
 def _psnr(mse: float) -> float:
     return 100.0 if mse < 1e-10 else float(10 * np.log10(1.0 / mse))
 
@@ -74,12 +131,22 @@ def video_metrics(sse, sad, n_values: int, lpips: Optional[Sequence[float]] = No
     return rec
 
 
-def measure_videos(videos_u8: torch.Tensor, lpips=None) -> list:
-    """uint8 [V, F, H, W, 3] (GPU) -> one record per video."""
+def measure_videos(videos_u8: torch.Tensor, lpips=None, flow: bool = True) -> list:
+    """uint8 [V, F, H, W, 3] (GPU) -> one record per video (flow fields from the HIP Farneback
+    pipeline unless flow=False)."""
     sse, sad = frame_sums(videos_u8)
     sse, sad = sse.cpu().tolist(), sad.cpu().tolist()
     n = int(np.prod(videos_u8.shape[2:]))
-    return [video_metrics(sse[v], sad[v], n, None if lpips is None else lpips[v]) for v in range(len(sse))]
+    recs = [video_metrics(sse[v], sad[v], n, None if lpips is None else lpips[v]) for v in range(len(sse))]
+    if flow:
+        hw = int(videos_u8.shape[2] * videos_u8.shape[3])
+        st = flow_sums(videos_u8, farneback_flow(videos_u8)).cpu().tolist()
+        for rec, s in zip(recs, st):
+            ff = flow_fields(s, hw)
+            for fm, pm in zip(rec["frame_metrics"], ff.pop("pairs")):
+                fm.update(pm)
+            rec.update(ff)
+    return recs
 
 
 def frames_from_video(video: torch.Tensor) -> torch.Tensor:
