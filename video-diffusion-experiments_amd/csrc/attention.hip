@@ -394,7 +394,7 @@ __device__ __forceinline__ float partner32(float x) {
 // >= the running max (l >= 2^(max - mu)), so nothing underflows that matters;
 // a row sum >= 2^100 (or non-finite) means a score jumped past the fp32/bf16
 // range and the pass reports `bad` so the block reruns EXACT.
-template <int D, bool UNITC, bool EXACT>
+template <int D, bool UNITC, bool EXACT, bool IL = false>
 __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, const bf16_t* vb_ptr, int ldk32,
                                          int ldv32, int64_t skv, const int (&krow)[F32Cfg<D>::LREG],
                                          const uint32_t (&kcol)[F32Cfg<D>::LREG],
@@ -428,12 +428,13 @@ __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, cons
   }
   __syncthreads();
 
-  for (int t = 0; t < ntiles; ++t) {
+  // one K/V tile: the general form (tile max on tile 0 / every tile of the exact pass,
+  // ragged-key masking, rescale one tile late)
+  auto tile_generic = [&](int t) {
     const int buf = t & 1;
     if (t + 1 < ntiles) kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, t + 1, skv, krow, kcol);
     const bf16_t* kl = lds + buf * C::STAGE;
     const bf16_t* vl = kl + C::K_ELEMS;
-
     // ---- x^T = K'.Q'^T  (= s - mu)
     f32x16 s[2][QB];
     bf16x8 kfr[2][C::KSTEPS];  // all K fragments of the tile first: one LDS latency, not six
@@ -591,6 +592,146 @@ __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, cons
       }
     }
     __syncthreads();
+  };
+  // a steady-state tile of the fast pass (not the first, not a ragged last one),
+  // software-pipelined inside the wave: the exps of key block 0 issue in the shadow of
+  // key block 1's QK^T MFMAs, and key block 1's exps in the shadow of block 0's PV MFMAs
+  // (MI355X_MICROARCH.md: an MFMA leaves 24 of its 32 issue cycles to VALU work).  The
+  // rescale check runs before the tile's QK^T instead of after it: the new -mu is in Q'
+  // before the MFMAs, so the scores come out already shifted.  Kept out of the general
+  // tile's loop: the two bodies in one loop spill (the register allocator merges them).
+  auto tile_il = [&](int t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, t + 1, skv, krow, kcol);
+    const bf16_t* kl = lds + buf * C::STAGE;
+    const bf16_t* vl = kl + C::K_ELEMS;
+    if (t > 1) {
+      float lq[QB];
+      bool resc = false, over = false;
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const float lown = oacc[C::L_DB][qb][C::L_I];
+        const float lp = partner32(lown);
+        lq[qb] = hh == C::L_H ? lown : lp;
+        resc |= lq[qb] > RESCALE;
+        over |= !(lq[qb] < BAD);
+      }
+      if (__any(over)) {
+        bad = true;
+      } else if (__any(resc)) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          const float step = lq[qb] > RESCALE ? __builtin_amdgcn_logf(lq[qb]) : 0.f;
+          const float nmu = (float)(__bf16)(mu[qb] + (UNITC ? step : step / c));
+          const float alpha = __builtin_amdgcn_exp2f(UNITC ? mu[qb] - nmu : (mu[qb] - nmu) * c);
+          mu[qb] = nmu;
+#pragma unroll
+          for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
+          if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
+        }
+      }
+    }
+    bf16x8 kfr[2][C::KSTEPS];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < C::KSTEPS; ++ks)
+        kfr[kb][ks] = *(const bf16x8*)(kl + (kb * 32 + r32) * C::KS + ks * 16 + 8 * hh);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 s[2][QB];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < C::KSTEPS; ++ks)
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          if (ks == 0) {
+            f32x16 z;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) z[i] = 0.f;
+            s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], z, 0, 0, 0);
+          } else {
+            s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], s[kb][qb], 0, 0, 0);
+          }
+        }
+    bf16x8 vfr[C::NDB][2][2];
+#pragma unroll
+    for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16_t* p0 = vl + (db * KT + kb * 32 + 16 * s2) * 32 + vtr;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (bf16x4 __attribute__((address_space(3)))*)(p0));
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (bf16x4 __attribute__((address_space(3)))*)(p0 + 8 * 32));
+          vfr[db][kb][s2] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      bf16x8 pf[2][QB];
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            f[j] = (__bf16)__builtin_amdgcn_exp2f(UNITC ? s[kb][qb][8 * s2 + j] : s[kb][qb][8 * s2 + j] * c);
+          pf[s2][qb] = f;
+        }
+#pragma unroll
+      for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb)
+            oacc[db][qb] =
+                __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[db][kb][s2], pf[s2][qb], oacc[db][qb], 0, 0, 0);
+    }
+    // issue order: QK^T(kb 0); QK^T(kb 1) | exp(kb 0); rest of exp(kb 0); PV(kb 0) | exp(kb 1); PV(kb 1)
+    constexpr int NQK = 2 * C::KSTEPS * QB / 2;       // MFMAs per key block
+    constexpr int NPV = C::NDB * 2 * QB;              // MFMAs per key block
+    constexpr int NV = 16 * QB + 8 * QB;              // exps + packs per key block
+    constexpr int V1 = NV / 2 / NQK;                  // per QK^T(kb 1) MFMA
+    constexpr int V2 = NV / NPV;                      // per PV(kb 0) MFMA
+#pragma unroll
+    for (int i = 0; i < NQK; ++i) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+    for (int i = 0; i < NQK; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, V1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x002, NV - V1 * NQK, 0);
+#pragma unroll
+    for (int i = 0; i < NPV; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, V2, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NPV; ++i) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < ntiles) {
+      bf16_t* nb = lds + (buf ^ 1) * C::STAGE;
+#pragma unroll
+      for (int i = 0; i < C::LREG; ++i) {
+        *(uint4*)(nb + ldsk[i]) = make_uint4(kvst[4 * i], kvst[4 * i + 1], kvst[4 * i + 2], kvst[4 * i + 3]);
+        *(uint4*)(nb + ldsv[i]) = make_uint4(kvst[4 * C::LREG + 4 * i], kvst[4 * C::LREG + 4 * i + 1],
+                                             kvst[4 * C::LREG + 4 * i + 2], kvst[4 * C::LREG + 4 * i + 3]);
+      }
+    }
+    __syncthreads();
+  };
+  if constexpr (IL && !EXACT) {
+    tile_generic(0);
+    const int tend = ragged ? ntiles - 1 : ntiles;
+    for (int t = 1; t < tend; ++t) tile_il(t);
+    if (ragged && ntiles > 1) tile_generic(ntiles - 1);
+  } else {
+    for (int t = 0; t < ntiles; ++t) tile_generic(t);
   }
   if (!EXACT) {  // the last tiles' row sums were not checked in the loop
     bool over = false;
@@ -605,7 +746,7 @@ __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, cons
   return bad;
 }
 
-template <int D, bool UNITC>
+template <int D, bool UNITC, bool IL = false>
 __global__ __launch_bounds__(NT, 2) void flash32_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
@@ -676,8 +817,8 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
   // V^T tr-read lane offset inside a [32 d] image row block (elements)
   const int vtr = ((4 * hh + (i16 >> 2)) * 32) + 16 * (g16 & 1) + 4 * (i16 & 3);
   f32x16 oacc[C::NDB][QB];
-  const bool bad = f32_loop<D, UNITC, false>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv,
-                                             qf, oacc, r32, hh, vtr, c);
+  const bool bad = f32_loop<D, UNITC, false, IL>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv,
+                                                 qf, oacc, r32, hh, vtr, c);
   if (__syncthreads_or(bad)) {  // a score jumped > ~100 (log2) past mu somewhere: exact pass
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb)
@@ -1082,7 +1223,10 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
       const int64_t nblk = (sq + 255) / 256 * heads * batch;
       if (nblk > 0x7fffffff) return VD_EINVAL;
       const dim3 grid((unsigned)nblk);
-      if (c == 1.0f)
+      if (c == 1.0f && g_flash32 == 3)
+        hipLaunchKernelGGL((flash32_kernel<D, true, true>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
+      else if (c == 1.0f)
         hipLaunchKernelGGL((flash32_kernel<D, true>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                            (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
       else
@@ -1521,11 +1665,12 @@ extern "C" int vd_attention_force_v1(int32_t on) {
   return VD_OK;
 }
 
-// Test/benchmark hook: the d = 40 kernel — 0 = automatic (flash32pp), 1 = flash_attn (16x16x32),
-// 2 = flash32 (4-wave 32x32x16), 3 = flash32pp (8-wave ping-pong).
+// Test/benchmark hook: the d = 40 kernel — 0 = automatic, 1 = flash_attn (16x16x32),
+// 2 = flash32 (4-wave 32x32x16), 3 = flash32pp (8-wave pipeline), 4 = flash32 with the
+// intra-wave interleaved steady state (unit c only).
 extern "C" int vd_attention_select(int32_t kernel) {
-  if (kernel < 0 || kernel > 3) return VD_EINVAL;
-  g_flash32 = kernel == 1 ? 0 : (kernel == 3 ? 2 : 1);
+  if (kernel < 0 || kernel > 4) return VD_EINVAL;
+  g_flash32 = kernel == 1 ? 0 : (kernel == 3 ? 2 : (kernel == 4 ? 3 : 1));
   return VD_OK;
 }
 
