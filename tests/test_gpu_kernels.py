@@ -318,11 +318,14 @@ def test_conv3x3_splitk(cuda):
 
 
 # ---------------------------------------------------------------- conv
-@pytest.mark.parametrize("case", ["s1", "s2", "up", "concat", "cin8", "cout4"])
+@pytest.mark.parametrize("case", ["s1", "s2", "up", "concat", "cin8", "cout4", "m128"])
 def test_conv3x3(cuda, case):
+    """m128: fewer output rows than one 256-row tile (a 1-2 image rank's level 4) -> 64x64 tiles."""
     torch.manual_seed(1)
     n, h, w = 3, 12, 10
     c0, c1, co = 64, 0, 128
+    if case == "m128":
+        n, h, w, c0, co = 2, 8, 8, 256, 320
     stride, up = 1, False
     if case == "s2":
         stride = 2

@@ -56,8 +56,11 @@ def run_b():
     return e0, e1
 
 
+only = sys.argv[2] if len(sys.argv) > 2 else "abc"
 res = {}
 for name, fn in (("a batch-2 forward", run_a), ("b two streams", run_b), ("c two forwards, one stream", run_c)):
+    if name[0] not in only:
+        continue
     fn()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()

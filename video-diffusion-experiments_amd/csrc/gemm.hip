@@ -1663,7 +1663,7 @@ void read_num_cus() {  // once per process: the plan (and the workspace size) de
 Plan plan(const vd_gemm_desc& d) {
   read_num_cus();
   Plan p;
-  if (g_path == 1 || d.K % G4_BK || d.k0 % G4_BK || d.M < G2_BM || d.N < 64) return p;
+  if (g_path == 1 || d.K % G4_BK || d.k0 % G4_BK || d.M < G6_BM || d.N < 64) return p;
   const int64_t a_rows = d.a_mode == VD_A_CONV3X3
                              ? (int64_t)d.n_img / d.frames_out * d.frames_in * d.h_in * d.w_in : d.M;
   const int64_t a0b = a_rows * d.lda0 * 2, a1b = d.a1 ? a_rows * d.lda1 * 2 : 0, wb = d.N * d.ldw * 2;
@@ -1672,6 +1672,14 @@ Plan plan(const vd_gemm_desc& d) {
   const bool cin32 = d.a_mode != VD_A_CONV3X3 || (d.K / 9) % G4_BK == 0;
   const bool k64 = d.K % BK == 0 && d.k0 % BK == 0 &&
                    (d.a_mode != VD_A_CONV3X3 || (d.K / (d.ks * d.ks * d.kt)) % BK == 0);
+  // fewer rows than one 256-row tile (the deep levels of a 1-2 image rank): 64 x 64 tiles
+  // (v1's 128-row tiles left L4's K = 11520 convs on 8 workgroups: 453 us vs ~30)
+  if (d.M < G2_BM) {
+    if (!k64 || d.kt > 1 || d.ks == 1 || (g_path != 0 && g_path != 6 && g_path != 8)) return p;  // v6: 2-D 3x3 taps
+    p.ver = 6;
+    p.bn = 64;
+    return p;
+  }
   if (d.kt > 1 || d.ks == 1) {  // temporal taps: the v2 loader (or v1 when the channels do not tile by 64)
     if (!k64) return p;
     p.ver = 2;
