@@ -170,6 +170,12 @@ int vd_layernorm_select(int32_t multi_row);
 int vd_attention(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                  int64_t ldv, void* o, int64_t ldo, int64_t batch, int32_t heads, int64_t sq,
                  int64_t skv, int32_t d, int64_t kv_div, float scale, vd_stream_t stream);
+/* vd_attention with the output O in fp32 (o: float rows, ldo in floats, 16-byte aligned):
+ * the same kernels and arithmetic, minus the final bf16 rounding of O — the parity tests
+ * hold it to rtol 1e-3 / atol 1e-4 against an fp64 reference. */
+int vd_attention_f32(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                     int64_t ldv, float* o, int64_t ldo, int64_t batch, int32_t heads,
+                     int64_t sq, int64_t skv, int32_t d, int64_t kv_div, float scale, vd_stream_t stream);
 /* Test/benchmark hook: on != 0 routes d = 40 to the 16x16x32 flash kernel instead of
  * the 32x32x16 one (default). */
 int vd_attention_force_v1(int32_t on);

@@ -627,6 +627,35 @@ def test_flash_attention_unit_scale(cuda):
     close_bf16(got, want)
 
 
+@pytest.mark.parametrize("d,sq,skv,batch,kv_div", [(40, 4096, 4096, 2, 1), (40, 1000, 333, 2, 1), (40, 777, 77, 4, 4),
+                                                  (80, 1024, 1024, 2, 1), (160, 256, 256, 3, 1), (64, 300, 300, 2, 1),
+                                                  (32, 200, 77, 2, 2), (128, 130, 130, 1, 1)])
+def test_attention_fp32_out_north_star_tolerance(attn_path, d, sq, skv, batch, kv_div):
+    """vd_attention_f32 against fp64 softmax(q k^T / log2 e) v at the north star's rtol 1e-3 /
+    atol 1e-4.  Scores are integers (q, k in {-1, 0, 1}) and the scale is the model path's
+    unit c, so every P = 2^(s - max) is exactly representable in bf16: what is checked is the
+    kernels' tiling, online softmax, ragged tails, row sums and fp32 accumulation — the one
+    rounding the product path adds on purpose (P to bf16 before PV, and O to bf16) is the
+    subject of the bf16-output tests above."""
+    torch.manual_seed(d + sq)
+    heads = 2
+    C = heads * d
+    q = bf(torch.randint(-1, 2, (batch * sq, C), device="cuda").float())
+    k = bf(torch.randint(-1, 2, (batch // kv_div * skv, C), device="cuda").float())
+    v = rnd(batch // kv_div * skv, C)
+    got = ops.attention(q, k, v, batch, heads, sq, skv, d, kv_div=kv_div, scale=1.0 / math.log2(math.e), out_f32=True)
+    assert got.dtype == torch.float32
+    qd = q.double().reshape(batch, sq, heads, d).transpose(1, 2)
+    kd = k.double().reshape(batch // kv_div, skv, heads, d).transpose(1, 2).repeat_interleave(kv_div, 0)
+    vd = v.double().reshape(batch // kv_div, skv, heads, d).transpose(1, 2).repeat_interleave(kv_div, 0)
+    s = qd @ kd.transpose(-1, -2)
+    p = torch.exp2(s - s.amax(-1, keepdim=True))
+    want = ((p @ vd) / p.sum(-1, keepdim=True)).transpose(1, 2).reshape(batch * sq, C)
+    err = (got.double() - want).abs()
+    print(f"d={d} sq={sq} skv={skv}: max |O - O_fp64| {err.max().item():.2e}")
+    assert torch.all(err <= 1e-4 + 1e-3 * want.abs()), err.max().item()
+
+
 @pytest.fixture(params=["mfma", "valu"])
 def temporal_path(request, cuda):
     """frames <= 16 with d in {40, 80, 160} run on the MFMA kernel unless forced to VALU."""

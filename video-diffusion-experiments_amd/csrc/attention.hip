@@ -97,7 +97,7 @@ template <int D, int QBLK>
 __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
-    int64_t sq, int64_t skv, int64_t kv_div, float c) {
+    int64_t sq, int64_t skv, int64_t kv_div, float c, int out_f32 = 0) {
   using C = AttnCfg<D>;
   // When PV is padded (DV > D) column D of V is set to 1.0, so the PV MFMA also
   // produces the softmax row sum (no per-score adds).
@@ -290,12 +290,17 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
     const int64_t qi = q0 + qb * 16 + fr;
     if (qi >= sq) continue;
     bf16_t* orow = o + (b * sq + qi) * ldo + (int64_t)h * D;
+    float* frow = (float*)o + (b * sq + qi) * ldo + (int64_t)h * D;  // out_f32: O in fp32 (tests)
 #pragma unroll
     for (int a = 0; a < C::DV / 16; ++a) {
       const int dd = a * 16 + 4 * fg;
       if (dd < D) {
-        *(uint2*)(orow + dd) = make_uint2(pack2(oacc[a][qb][0] * inv, oacc[a][qb][1] * inv),
-                                          pack2(oacc[a][qb][2] * inv, oacc[a][qb][3] * inv));
+        if (out_f32)
+          *(float4*)(frow + dd) = make_float4(oacc[a][qb][0] * inv, oacc[a][qb][1] * inv, oacc[a][qb][2] * inv,
+                                              oacc[a][qb][3] * inv);
+        else
+          *(uint2*)(orow + dd) = make_uint2(pack2(oacc[a][qb][0] * inv, oacc[a][qb][1] * inv),
+                                            pack2(oacc[a][qb][2] * inv, oacc[a][qb][3] * inv));
       }
     }
   }
@@ -750,7 +755,7 @@ template <int D, bool UNITC, bool IL = false>
 __global__ __launch_bounds__(NT, 2) void flash32_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
-    int64_t sq, int64_t skv, int64_t kv_div, float c) {
+    int64_t sq, int64_t skv, int64_t kv_div, float c, int out_f32 = 0) {
   using C = F32Cfg<D>;
   constexpr int QB = 2;  // 32-query blocks per wave
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * C::STAGE];
@@ -837,6 +842,19 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
     const float l = hh == C::L_H ? lown : lp;
     const float inv = __builtin_amdgcn_rcpf(l);
     const int64_t qi = q0 + qb * 32 + r32;
+    if (out_f32) {  // tests: O in fp32; register i of d-block db holds d = 32 db + 8 (i >> 2) + 4 hh + (i & 3)
+      float* frow = (float*)o + (b * sq + qi) * ldo + (int64_t)h * D;
+#pragma unroll
+      for (int db = 0; db < C::NDB; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d0 = 32 * db + 8 * g + 4 * hh;
+          const f32x16& a = oacc[db][qb];
+          if (qi < sq && d0 + 4 <= D)
+            *(float4*)(frow + d0) = make_float4(a[4 * g] * inv, a[4 * g + 1] * inv, a[4 * g + 2] * inv, a[4 * g + 3] * inv);
+        }
+      continue;
+    }
     bf16_t* orow = o + (b * sq + (qi < sq ? qi : 0)) * ldo + (int64_t)h * D;
 #pragma unroll
     for (int db = 0; db < C::NDB; ++db) {
@@ -1204,10 +1222,10 @@ __global__ __launch_bounds__(2 * NT, 1) void flash32pp_kernel(
 template <int D>
 int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                  void* o, int64_t ldo, int64_t batch, int heads, int64_t sq, int64_t skv,
-                 int64_t kv_div, float scale, hipStream_t s) {
+                 int64_t kv_div, float scale, hipStream_t s, int out_f32 = 0) {
   const float c = scale * 1.4426950408889634f;
   if constexpr (D == 40) {
-    if (g_flash32 == 2 && ((uintptr_t)o & 15) == 0 && ldo % 8 == 0) {  // ping-pong 8-wave kernel
+    if (g_flash32 == 2 && !out_f32 && ((uintptr_t)o & 15) == 0 && ldo % 8 == 0) {  // ping-pong 8-wave kernel
       const int64_t nblk = (sq + 511) / 512 * heads * batch;
       if (nblk > 0x7fffffff) return VD_EINVAL;
       const dim3 grid((unsigned)nblk);
@@ -1219,19 +1237,19 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
                            (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
       return vd_launch_status();
     }
-    if (g_flash32 && ((uintptr_t)o & 15) == 0 && ldo % 8 == 0) {
+    if (g_flash32 && ((uintptr_t)o & 15) == 0 && ldo % (out_f32 ? 4 : 8) == 0) {
       const int64_t nblk = (sq + 255) / 256 * heads * batch;
       if (nblk > 0x7fffffff) return VD_EINVAL;
       const dim3 grid((unsigned)nblk);
       if (c == 1.0f && g_flash32 == 3)
         hipLaunchKernelGGL((flash32_kernel<D, true, true>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
       else if (c == 1.0f)
         hipLaunchKernelGGL((flash32_kernel<D, true>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
       else
         hipLaunchKernelGGL((flash32_kernel<D, false>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
       return vd_launch_status();
     }
   }
@@ -1239,12 +1257,12 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
     const dim3 grid((unsigned)((sq + 255) / 256), (unsigned)heads, (unsigned)batch);
     hipLaunchKernelGGL((flash_attn_kernel<D, 4>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                        (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv,
-                       kv_div, c);
+                       kv_div, c, out_f32);
   } else {
     const dim3 grid((unsigned)((sq + 127) / 128), (unsigned)heads, (unsigned)batch);
     hipLaunchKernelGGL((flash_attn_kernel<D, 2>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                        (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv,
-                       kv_div, c);
+                       kv_div, c, out_f32);
   }
   return vd_launch_status();
 }
@@ -1674,25 +1692,40 @@ extern "C" int vd_attention_select(int32_t kernel) {
   return VD_OK;
 }
 
-extern "C" int vd_attention(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+static int attention_entry(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                             int64_t ldv, void* o, int64_t ldo, int64_t batch, int32_t heads,
                             int64_t sq, int64_t skv, int32_t d, int64_t kv_div, float scale,
-                            vd_stream_t stream) {
+                            vd_stream_t stream, int out_f32) {
   VD_CHECK_ARG(q && k && v && o && al16(q) && al16(k) && al16(v) && ((uintptr_t)o & 7) == 0);
   VD_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0);
+  if (out_f32) VD_CHECK_ARG(((uintptr_t)o & 15) == 0);
   VD_CHECK_ARG(batch > 0 && heads > 0 && sq > 0 && skv > 0 && kv_div > 0 && batch % kv_div == 0);
   VD_CHECK_ARG(batch <= 65535 && heads <= 65535);
   VD_CHECK_ARG(skv * ldk < 0x7fffffff && skv * ldv < 0x7fffffff);
   hipStream_t s = (hipStream_t)stream;
   switch (d) {
-    case 32: return launch_flash<32>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s);
-    case 40: return launch_flash<40>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s);
-    case 64: return launch_flash<64>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s);
-    case 80: return launch_flash<80>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s);
-    case 128: return launch_flash<128>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s);
-    case 160: return launch_flash<160>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s);
+    case 32: return launch_flash<32>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
+    case 40: return launch_flash<40>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
+    case 64: return launch_flash<64>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
+    case 80: return launch_flash<80>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
+    case 128: return launch_flash<128>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
+    case 160: return launch_flash<160>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
     default: return VD_EUNSUPPORTED;
   }
+}
+
+extern "C" int vd_attention(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                            int64_t ldv, void* o, int64_t ldo, int64_t batch, int32_t heads,
+                            int64_t sq, int64_t skv, int32_t d, int64_t kv_div, float scale,
+                            vd_stream_t stream) {
+  return attention_entry(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, d, kv_div, scale, stream, 0);
+}
+
+extern "C" int vd_attention_f32(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                                int64_t ldv, float* o, int64_t ldo, int64_t batch, int32_t heads,
+                                int64_t sq, int64_t skv, int32_t d, int64_t kv_div, float scale,
+                                vd_stream_t stream) {
+  return attention_entry(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, d, kv_div, scale, stream, 1);
 }
 
 // Test/benchmark hook: on != 0 runs every temporal attention on the VALU kernel.

@@ -39,6 +39,7 @@ SIGNATURES = {
     "vd_layernorm": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
     "vd_layernorm_select": ([c_i32], c_i32),
     "vd_attention": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_i64, c_f32, c_vp], c_i32),
+    "vd_attention_f32": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_i64, c_f32, c_vp], c_i32),
     "vd_temporal_attention": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
     "vd_temporal_attention_rope": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_f32, c_vp], c_i32),
     "vd_softmax_rows": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),

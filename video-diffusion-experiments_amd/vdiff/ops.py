@@ -229,15 +229,16 @@ def layer_norm(x, gamma, beta, eps=1e-5, pe=None, pe_div=1, pe_period=1, out=Non
 
 
 # ---------------------------------------------------------------- attention
-def attention(q, k, v, batch, heads, sq, skv, d, kv_div=1, scale=None, out=None):
-    """q/k/v: 2-D row views (may be column slices of a fused QKV buffer)."""
+def attention(q, k, v, batch, heads, sq, skv, d, kv_div=1, scale=None, out=None, out_f32=False):
+    """q/k/v: 2-D row views (may be column slices of a fused QKV buffer).  out_f32: O in fp32
+    (vd_attention_f32; the tests' north-star-tolerance mode)."""
     _dev(q, k, v, out)
     if out is None:
-        out = torch.empty(batch * sq, heads * d, device=q.device, dtype=BF16)
+        out = torch.empty(batch * sq, heads * d, device=q.device, dtype=torch.float32 if out_f32 else BF16)
     scale = d ** -0.5 if scale is None else scale
-    check(lib().vd_attention(_p(q), q.stride(0), _p(k), k.stride(0), _p(v), v.stride(0), _p(out),
-                             out.stride(0), batch, heads, sq, skv, d, kv_div, scale, _stream()),
-          "vd_attention")
+    fn = lib().vd_attention_f32 if out_f32 else lib().vd_attention
+    check(fn(_p(q), q.stride(0), _p(k), k.stride(0), _p(v), v.stride(0), _p(out), out.stride(0), batch, heads, sq,
+             skv, d, kv_div, scale, _stream()), "vd_attention_f32" if out_f32 else "vd_attention")
     return out
 
 
