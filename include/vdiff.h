@@ -182,7 +182,8 @@ int vd_attention_force_v1(int32_t on);
 /* Test/benchmark hook: the d = 40 kernel — 0 = automatic (flash32), 1 = the 16x16x32 flash
  * kernel, 2 = flash32 (4 waves, 32x32x16), 3 = flash32pp (8 waves: two staggered groups
  * software-pipelined PV(t-1)+QK(t) | softmax(t); bitwise equal to flash32, measured slower —
- * tools/attn_ab.py), 4 = flash32 with the intra-wave interleaved steady state. */
+ * tools/attn_ab.py), 4 = flash32 with the intra-wave interleaved steady state, 5 = flash32 at
+ * one workgroup per CU (occupancy probe). */
 int vd_attention_select(int32_t kernel);
 
 /* Temporal (motion-module) self-attention over frames (a9): token (b, f, p) is

@@ -23,15 +23,15 @@ qkv = (torch.randn(n_img * S, 3 * C, device="cuda", generator=g) * 1.5).to(torch
 q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
 scale = 1.0 / math.log2(math.e)
 flop = 4.0 * S * S * d * heads * n_img
-outs, res = {}, {1: [], 2: [], 3: [], 4: []}
+outs, res = {}, {1: [], 2: [], 3: [], 4: [], 5: []}
 names = {1: "flash_attn 16x16x32", 2: "flash32 (4 waves)", 3: "flash32pp (pipelined stagger)",
-         4: "flash32 interleaved"}
-for sel in (1, 2, 3, 4):
+         4: "flash32 interleaved", 5: "flash32, 1 WG per CU"}
+for sel in (1, 2, 3, 4, 5):
     lib().vd_attention_select(sel)
     outs[sel] = ops.attention(q, k, v, n_img, heads, S, S, d, scale=scale)
 torch.cuda.synchronize()
 for _ in range(rounds):
-    for sel in (1, 2, 3, 4):
+    for sel in (1, 2, 3, 4, 5):
         lib().vd_attention_select(sel)
         out = torch.empty_like(outs[sel])
         for _ in range(2):
@@ -44,7 +44,7 @@ for _ in range(rounds):
         e1.synchronize()
         res[sel].append(e0.elapsed_time(e1) / 10)
 lib().vd_attention_select(0)
-for sel in (1, 2, 3, 4):
+for sel in (1, 2, 3, 4, 5):
     ms = sorted(res[sel])
     print(f"{names[sel]:30s} median {ms[len(ms) // 2] * 1e3:7.1f} us  min {ms[0] * 1e3:7.1f} us  "
           f"{flop / ms[len(ms) // 2] / 1e9:7.1f} TF/s  ({flop / ms[len(ms) // 2] / 1e9 / 2500:.3f} of peak)")

@@ -1245,7 +1245,7 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
         hipLaunchKernelGGL((flash32_kernel<D, true, true>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                            (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
       else if (c == 1.0f)
-        hipLaunchKernelGGL((flash32_kernel<D, true>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+        hipLaunchKernelGGL((flash32_kernel<D, true>), grid, dim3(NT), g_flash32 == 4 ? 96 * 1024 : 0, s, (const bf16_t*)q, ldq,
                            (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
       else
         hipLaunchKernelGGL((flash32_kernel<D, false>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
@@ -1685,10 +1685,11 @@ extern "C" int vd_attention_force_v1(int32_t on) {
 
 // Test/benchmark hook: the d = 40 kernel — 0 = automatic, 1 = flash_attn (16x16x32),
 // 2 = flash32 (4-wave 32x32x16), 3 = flash32pp (8-wave pipeline), 4 = flash32 with the
-// intra-wave interleaved steady state (unit c only).
+// intra-wave interleaved steady state (unit c only), 5 = flash32 held to one workgroup per
+// CU (96 KiB of dynamic LDS: one wave per SIMD — the occupancy probe of DESIGN.md §5).
 extern "C" int vd_attention_select(int32_t kernel) {
-  if (kernel < 0 || kernel > 4) return VD_EINVAL;
-  g_flash32 = kernel == 1 ? 0 : (kernel == 3 ? 2 : (kernel == 4 ? 3 : 1));
+  if (kernel < 0 || kernel > 5) return VD_EINVAL;
+  g_flash32 = kernel == 1 ? 0 : (kernel == 3 ? 2 : (kernel == 4 ? 3 : (kernel == 5 ? 4 : 1)));
   return VD_OK;
 }
 
