@@ -48,6 +48,11 @@ for sel in (1, 2, 3, 4, 5):
     ms = sorted(res[sel])
     print(f"{names[sel]:30s} median {ms[len(ms) // 2] * 1e3:7.1f} us  min {ms[0] * 1e3:7.1f} us  "
           f"{flop / ms[len(ms) // 2] / 1e9:7.1f} TF/s  ({flop / ms[len(ms) // 2] / 1e9 / 2500:.3f} of peak)")
+ref = torch.softmax((q.float().reshape(n_img, S, heads, d).transpose(1, 2)[:2] @ k.float().reshape(n_img, S, heads, d).transpose(1, 2)[:2].transpose(-1, -2)) * scale * math.log2(math.e) * math.log(2), -1) @ v.float().reshape(n_img, S, heads, d).transpose(1, 2)[:2]
+ref = ref.transpose(1, 2).reshape(2 * S, C)
+for sel in (2, 4):
+    e = (outs[sel][:2 * S].float() - ref).norm() / ref.norm()
+    print(f"select {sel}: rel-L2 vs fp32 softmax attention (2 images) {e.item():.3e}")
 print("interleaved vs flash32: max|diff| =", (outs[4].float() - outs[2].float()).abs().max().item(),
       " mean|diff| =", (outs[4].float() - outs[2].float()).abs().mean().item())
 print("flash32pp == flash32 bitwise:", torch.equal(outs[2], outs[3]),
