@@ -142,6 +142,9 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--attn-reps", type=int, default=20)
     ap.add_argument("--no-nocfg", action="store_true", help="skip the B=1 (no-CFG) variant")
+    ap.add_argument("--overlap", type=int, default=1,
+                    help="N>1: chunk each motion module's all-to-alls over positions and overlap them with "
+                         "the transformer block on a second stream (vdiff.dist.FrameShard overlap_chunks)")
     ap.add_argument("--layout", default="auto", choices=["auto", "frame", "cfg-frame"],
                     help="N>1 placement (vdiff.dist.layout): auto = cfg-frame at 2 GPUs, frame otherwise")
     args = ap.parse_args()
@@ -161,7 +164,7 @@ def main():
     frames = args.frames or (16 if cfg_name == "full" else 4)
     t0 = time.time()
     from vdiff.dist import NodeLayout
-    lay = NodeLayout(args.layout, frames, cfg=True, world=world, rank=rank)
+    lay = NodeLayout(args.layout, frames, cfg=True, world=world, rank=rank, overlap_chunks=args.overlap)
     unet = materialize_synthetic(cfg_name, device="cuda", seed=0)
     unet.dist = lay.frame_shard
     unet.prepare()

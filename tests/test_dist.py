@@ -84,6 +84,20 @@ def _worker(rank, world, port, errq):
         want = full.reshape(B, F, HW, 8)[:, :, rank * Pl:(rank + 1) * Pl].reshape(-1, 8)
         assert torch.equal(hp, want), "to_position_shards content"
         assert torch.equal(fs.to_frame_shards(hp, B, Fl, HW, bt), loc), "round trip"
+        # ---- 1b. the chunked, overlapped temporal window (FrameShard(overlap_chunks=2)) ==
+        # the plain one, with a block that mixes every frame of each position
+        def mix(rows, b_, f_, p_):
+            r4 = rows.reshape(b_, f_, p_, -1)
+            w = torch.arange(1, f_ + 1, dtype=rows.dtype).reshape(1, f_, 1, 1)
+            return (r4 * w + r4.sum(1, keepdim=True)).reshape(-1, rows.shape[1])
+        HW2 = 16
+        base = torch.randn(B * F * HW2, 8)
+        loc2 = base.reshape(B, F, HW2, 8)[:, rank * Fl:(rank + 1) * Fl].reshape(-1, 8).contiguous()
+        plain = fs.temporal_window(loc2, B, Fl, HW2, bt, mix)
+        over = FrameShard(overlap_chunks=2).temporal_window(loc2, B, Fl, HW2, bt, mix)
+        assert torch.equal(plain, over), "overlapped temporal window"
+        full_mix = mix(base, B, F, HW2).reshape(B, F, HW2, 8)[:, rank * Fl:(rank + 1) * Fl].reshape(-1, 8)
+        assert torch.allclose(plain, full_mix, atol=1e-5), "temporal window content"
         # ---- 2. sharded motion module == unsharded oracle
         sd = {}
         p = "m"

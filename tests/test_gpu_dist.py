@@ -56,6 +56,29 @@ def test_sharded_loop_world1_matches_unsharded(pg):
     assert torch.equal(out, ref)
 
 
+def test_overlapped_window_world1_rccl_graph(pg):
+    """FrameShard(overlap_chunks=2) on the real RCCL backend: the chunked all-to-alls run on a
+    side stream joined by events, all captured into the step's hipGraph; at world size 1 every
+    all-to-all is an identity, so the loop must equal the unsharded one bit for bit."""
+    torch.manual_seed(0)
+    unet = init_synthetic_(UNetMotionModel("tiny"), seed=3).to("cuda", torch.bfloat16).prepare()
+    lat = torch.randn(1, 4, 4, 64, 64, device="cuda")
+    ehs = torch.randn(2, 77, 64, device="cuda")
+    s = DDIMScheduler(beta_schedule="linear", steps_offset=1, clip_sample=False)
+    s.set_timesteps(50)
+    ref = DenoiseLoop(unet, s, lat, ehs, 7.5, use_graph=True).prime().run(2).clone()
+    fs = FrameShard(overlap_chunks=2)
+    unet.dist = fs
+    try:
+        loop = DenoiseLoop(unet, s, lat, ehs, 7.5, use_graph=True).prime()
+        assert loop.graph is not None, f"graph capture of the overlapped all-to-alls failed: {loop.graph_error}"
+        got = loop.run(2)
+        out = fs.all_gather_frames(got)
+    finally:
+        unet.dist = None
+    assert torch.equal(out, ref)
+
+
 def test_dit_sharded_loop_world1_matches_unsharded(pg):
     """The DiT's frame-sharded path (an all-to-all re-shard around every temporal block,
     tools/dit_bench.py's multi-GPU mode) on RCCL, captured into the step's hipGraph."""

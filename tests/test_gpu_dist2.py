@@ -57,7 +57,7 @@ def _sched():
     return s
 
 
-def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2):
+def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2, overlap=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -70,8 +70,9 @@ def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2):
         def gather_gn_partials(self, ws):
             return super().gather_gn_partials(ws.cpu()).to(ws.device)
 
-        def _a2a(self, x):
-            return super()._a2a(x.cpu()).to(x.device)
+        def _a2a(self, x, out=None):
+            got = super()._a2a(x.cpu()).to(x.device)
+            return got if out is None else out.copy_(got)
 
         def all_gather_frames(self, x):
             return super().all_gather_frames(x.cpu())
@@ -83,7 +84,8 @@ def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2):
     try:
         unet = _model(cfg)
         lay = NodeLayout(layout, FRAMES if cfg == "tiny" else FULL_FRAMES, world=world, rank=rank)
-        fs = HostStagedShard(lay.frame_shard.group) if lay.frame_shard is not None else None
+        fs = (HostStagedShard(lay.frame_shard.group, overlap_chunks=overlap)
+              if lay.frame_shard is not None else None)
         cs = HostStagedCfg(lay.cfg_shard.group) if lay.cfg_shard is not None else None
         unet.dist = fs
         lat, ehs = _inputs(cfg)
@@ -108,16 +110,18 @@ def unsharded_ref(cuda):
     return DenoiseLoop(_model(), _sched(), lat.cuda(), ehs.cuda(), 7.5, use_graph=False).prime().run(2).cpu()
 
 
-@pytest.mark.parametrize("world,layout", [(2, "frame"), (4, "frame"), (8, "frame"),
-                                          (2, "cfg-frame"), (4, "cfg-frame"), (8, "cfg-frame")])
-def test_ranks_on_one_gpu_match_unsharded(unsharded_ref, world, layout):
+@pytest.mark.parametrize("world,layout,overlap", [(2, "frame", 1), (4, "frame", 1), (8, "frame", 1),
+                                                  (2, "cfg-frame", 1), (4, "cfg-frame", 1), (8, "cfg-frame", 1),
+                                                  (2, "frame", 2), (4, "cfg-frame", 4)])
+def test_ranks_on_one_gpu_match_unsharded(unsharded_ref, world, layout, overlap):
     """layout "cfg-frame" (SURVEY §8e (ii)): the two CFG halves on two rank groups, eps
-    swapped between CFG pairs before the update; at world 2 no motion-module collective."""
+    swapped between CFG pairs before the update; at world 2 no motion-module collective.
+    overlap > 1: the motion modules' all-to-alls chunked over positions on a side stream."""
     ref = unsharded_ref
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "out.pt")
-        mp.start_processes(_worker, args=(world, _port(), path, layout), nprocs=world, join=True,
-                           start_method="spawn")
+        mp.start_processes(_worker, args=(world, _port(), path, layout, "tiny", 2, overlap), nprocs=world,
+                           join=True, start_method="spawn")
         got = torch.load(path, weights_only=True)
     assert got.shape == ref.shape
     err = ((got.double() - ref.double()).norm() / ref.double().norm()).item()

@@ -1,0 +1,84 @@
+"""Per-rank step time of an N-way frame-sharded run, emulated on ONE GPU.
+
+    python tools/rank_emulate.py --world 8 --chunks 1 2 4 [--comm copy|none]
+
+Rank 0 of the "frame" layout: 16/N frames of both CFG halves, the motion modules'
+re-shards exactly as FrameShard issues them (same transposes, same chunking, same
+side stream), but every collective replaced by a device copy of the same size
+(`--comm copy`: the local share of the traffic) or by nothing (`--comm none`).
+The numerics are not a video's (the copies do not exchange frames); the launches,
+shapes and stream structure are rank 0's.  This isolates what chunking costs in
+compute (smaller GEMMs, more launches) from what it can hide (the all-to-all time,
+DESIGN.md §6's communication budget)."""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "video-diffusion-experiments_amd")]
+
+import torch  # noqa: E402
+
+from vdiff import DDIMScheduler, DenoiseLoop  # noqa: E402
+from vdiff.dist import FrameShard  # noqa: E402
+from vdiff.weights import materialize_synthetic  # noqa: E402
+
+
+class EmulatedShard(FrameShard):
+    def __init__(self, world, chunks, comm):
+        self.group, self.world, self.rank, self.chunks = None, world, 0, chunks
+        self._side = {}
+        self.comm = comm
+
+    def _a2a(self, x, out=None):
+        out = torch.empty_like(x) if out is None else out
+        if self.comm == "copy":
+            out.copy_(x)
+        return out
+
+    def gather_gn_partials(self, ws):
+        return ws.repeat_interleave(self.world, dim=1) if self.world > 1 else ws
+
+    def all_gather_frames(self, x):
+        return x
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--chunks", type=int, nargs="+", default=[1, 2, 4])
+    ap.add_argument("--comm", default="copy", choices=["copy", "none"])
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--frames", type=int, default=16)
+    args = ap.parse_args()
+    unet = materialize_synthetic("full", device="cuda", seed=0)
+    fl = args.frames // args.world
+    lat = torch.randn(1, 4, fl, 64, 64, device="cuda")
+    ehs = torch.randn(2, 77, unet.config["cross_attention_dim"], device="cuda")
+    s = DDIMScheduler(beta_schedule="linear", steps_offset=1, clip_sample=False)
+    s.set_timesteps(50)
+    ts = s.timesteps.repeat(2)
+    res = {}
+    for c in args.chunks:
+        unet.dist = EmulatedShard(args.world, c, args.comm) if args.world > 1 else None
+        unet.prepare()
+        loop = DenoiseLoop(unet, s, lat, ehs, 7.5, timesteps=ts, use_graph=True).prime()
+        assert loop.graph is not None, loop.graph_error
+        loop.run(3)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        loop.run(args.steps)
+        torch.cuda.synchronize()
+        ms = 1e3 * (time.perf_counter() - t0) / args.steps
+        res[c] = round(ms, 3)
+        print(f"world {args.world} frames/rank {fl} chunks {c} comm {args.comm}: {ms:.3f} ms/step", flush=True)
+        del loop
+    print(json.dumps({"world": args.world, "frames_local": fl, "comm": args.comm, "ms_per_step": res}))
+
+
+if __name__ == "__main__":
+    main()

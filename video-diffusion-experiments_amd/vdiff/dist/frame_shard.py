@@ -19,18 +19,29 @@ MI355X, "gloo" in the CPU tests) on the current stream, so they are captured
 into the step's hipGraph.  The row permutations around the all-to-alls are
 `transpose(src, nb, na, nc)` — the HIP kernel vd_block_transpose in the product
 path, injected so the decomposition itself is testable on CPU.
+
+`FrameShard(overlap_chunks=c)` (c > 1) splits each rank's positions into c chunks and
+pipelines the temporal window: each chunk's transformer block runs on a second stream
+(captured into the same graph through event edges) while the capturing stream carries the
+neighbouring chunks' all-to-alls.  Same arithmetic, same result.
 """
 from __future__ import annotations
+
+import contextlib
 
 import torch
 import torch.distributed as dist
 
 
 class FrameShard:
-    def __init__(self, group=None):
+    def __init__(self, group=None, overlap_chunks: int = 1):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        if overlap_chunks < 1:
+            raise ValueError("overlap_chunks must be >= 1")
+        self.chunks = overlap_chunks
+        self._side = {}  # device -> compute stream of the overlapped temporal window
 
     def frames_local(self, frames: int) -> int:
         if frames % self.world:
@@ -45,8 +56,8 @@ class FrameShard:
         return out.reshape((self.world,) + tuple(ws.shape)).transpose(0, 1).reshape(ws.shape[0], self.world * ws.shape[1], *ws.shape[2:]).contiguous()
 
     # -- temporal window re-shard ---------------------------------------------
-    def _a2a(self, x: torch.Tensor) -> torch.Tensor:
-        out = torch.empty_like(x)
+    def _a2a(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        out = torch.empty_like(x) if out is None else out
         dist.all_to_all_single(out, x, group=self.group)
         return out
 
@@ -68,6 +79,63 @@ class FrameShard:
         send = transpose(hp, batch, W, frames_local * pl)           # (r', b, f_loc, pl)
         recv = self._a2a(send)                                      # (r,  b, f_loc, pl)  r = position chunk
         return transpose(recv, W, batch * frames_local, pl)         # (b, f_loc, r, pl) = (b, f_loc, p)
+
+    def _side_stream(self, device):
+        if device not in self._side:
+            self._side[device] = torch.cuda.Stream(device=device)
+        return self._side[device]
+
+    def temporal_window(self, h, batch, frames_local, hw, transpose, block):
+        """rows (b, f_loc, p) of this rank's frames -> block over ALL frames of this rank's
+        positions -> rows (b, f_loc, p) again.  `block(rows, batch, frames, positions)` is the
+        motion module's transformer block on rows (b, f, p).  With overlap_chunks == 1 this is
+        to_position_shards / block / to_frame_shards.  With c > 1 the positions are cut into c
+        chunks; chunk k's block runs on a side stream while the capturing stream carries chunk
+        k+1's incoming and chunk k-1's outgoing all-to-all.  (RCCL collectives must stay on the
+        capturing stream: issued from a forked stream, hipGraph capture of them segfaults —
+        tools/capture_probe.py; a forked COMPUTE stream captures and replays correctly.)
+        The block is per position, so which positions a rank takes per chunk is free: chunk c
+        sends positions (c*W + r)*pc + j to rank r, making every chunk's buffers contiguous."""
+        W, C = self.world, self.chunks
+        if hw % W:
+            raise ValueError(f"{hw} positions do not shard over {W} ranks")
+        pl = hw // W
+        if C == 1 or pl % C:
+            hp = self.to_position_shards(h, batch, frames_local, hw, transpose)
+            hp = block(hp, batch, frames_local * W, pl)
+            return self.to_frame_shards(hp, batch, frames_local, hw, transpose)
+        pc, BF, cols = pl // C, batch * frames_local, h.shape[1]
+        send = transpose(h, BF, C * W, pc).view(C, W * BF * pc, cols)  # (c, r, bf, j)
+        cuda = h.is_cuda
+        if cuda:
+            main = torch.cuda.current_stream(h.device)
+            side = self._side_stream(h.device)
+        recv = [self._a2a(send[0])]                                     # (s, b, f_loc, j)
+        back_recv = torch.empty_like(send)                              # (c, s', bf, j)
+        for c in range(C):
+            if cuda:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+                ctx = torch.cuda.stream(side)
+            else:
+                ctx = contextlib.nullcontext()
+            with ctx:
+                hp = transpose(recv[c], W, batch, frames_local * pc)      # (b, s, f_loc, j) = (b, f, j)
+                hp = block(hp, batch, frames_local * W, pc)
+                back = transpose(hp, batch, W, frames_local * pc)        # (s, b, f_loc, j)
+                if cuda:
+                    done = torch.cuda.Event()
+                    done.record(side)
+            if cuda:
+                back.record_stream(main)  # made on the side stream, read by main's all-to-all
+            if c + 1 < C:
+                recv.append(self._a2a(send[c + 1]))                     # overlaps chunk c's block
+            if cuda:
+                main.wait_event(done)
+            self._a2a(back.view(W * BF * pc, cols), back_recv[c])       # (s', b, f_loc, j)
+        # rows (c, s', bf, j) -> (bf, c, s', j) = (b, f_loc, p)
+        return transpose(back_recv.view(C * W * BF * pc, cols), C * W, BF, pc)
 
     # -- temporal conv halo ------------------------------------------------------
     def halo_frames(self, x: torch.Tensor, batch: int, frames_local: int, hw: int) -> torch.Tensor:

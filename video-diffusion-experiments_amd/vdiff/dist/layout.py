@@ -49,7 +49,9 @@ class NodeLayout:
     """Group construction for a layout; every rank must build it (new_group is collective)."""
 
     def __init__(self, layout: str = "auto", frames: int = 16, cfg: bool = True, world=None, rank=None,
-                 backend=None):
+                 backend=None, overlap_chunks: int = 1):
+        """overlap_chunks > 1: the motion modules' all-to-alls are chunked over positions and
+        overlapped with the transformer blocks on a second stream (FrameShard)."""
         self.world = dist.get_world_size() if world is None else world
         self.rank = dist.get_rank() if rank is None else rank
         self.layout = layout = self.resolve(layout, self.world, cfg)
@@ -65,7 +67,7 @@ class NodeLayout:
         if self.world == 1:
             return
         if layout == "frame":
-            self.frame_shard = FrameShard()
+            self.frame_shard = FrameShard(overlap_chunks=overlap_chunks)
             return
         # every rank creates every group, in the same order
         kw = {} if backend is None else {"backend": backend}
@@ -73,7 +75,7 @@ class NodeLayout:
                    for h in range(2)]
         pairs = [dist.new_group([j, self.frame_ranks + j], **kw) for j in range(self.frame_ranks)]
         if self.frame_ranks > 1:
-            self.frame_shard = FrameShard(fgroups[self.half])
+            self.frame_shard = FrameShard(fgroups[self.half], overlap_chunks=overlap_chunks)
         self.cfg_shard = CfgShard(pairs[self.frame_index])
 
     @staticmethod

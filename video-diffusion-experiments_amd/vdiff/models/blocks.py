@@ -235,9 +235,7 @@ class AnimateDiffTransformer3D(nn.Module):
         if dist is None:
             h = blk.run_temporal(h, B, Fl, hw)
         else:
-            hp = dist.to_position_shards(h, B, Fl, hw, ops.block_transpose)
-            hp = blk.run_temporal(hp, B, Fl * dist.world, hw // dist.world)
-            h = dist.to_frame_shards(hp, B, Fl, hw, ops.block_transpose)
+            h = dist.temporal_window(h, B, Fl, hw, ops.block_transpose, blk.run_temporal)
         out = ops.gemm(h, self.proj_out._w, bias=self.proj_out._b, res=x.t)
         return Act(out, x.n, x.h, x.w)
 
