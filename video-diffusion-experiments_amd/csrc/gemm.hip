@@ -643,11 +643,22 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
 //  * the A (X) parts a wave group reads are DMA'd by that group only, so the
 //    stagger never lets one group overwrite rows the other has yet to read; the
 //    W parts, read by both groups, are restaged >= 2 phases after their reads.
-// Non-persistent (one output tile, or one split-K slice of it, per workgroup),
-// XCD-aware order with the N tiles of an A row-panel adjacent.
+// Persistent (round 2): a workgroup walks units lid, lid + G, ... (unit = output tile or
+// one split-K slice of it, XCD-aware order with the N tiles of an A row-panel adjacent),
+// and the K-tiles of all its units form ONE flat stream: the DMA of the next unit's first
+// two K-tiles goes out during the last K-tiles of the current one, so the prologue's HBM
+// burst and most of the epilogue's store tail overlap MFMA work (per-tile fixed cost,
+// profiles/r02_v3_k_sweep.txt: 9.4 us per 256^2 tile vs 4.8 for hipBLASLt).  At a unit
+// boundary the two wave groups re-align (group 0 one extra barrier), both run the
+// epilogue, and group 1 re-staggers (one extra barrier) before the next unit's phase 0.
+// Grid = units gives one unit per workgroup (the round-1 non-persistent kernel).
 constexpr int G3_BM = 256, G3_BN = 256, G3_NT = 512;
 constexpr int G3_A_BYTES = G3_BM * BK * 2;     // 32 KiB
 constexpr int G3_STAGE = 2 * G3_A_BYTES;       // A + W: 64 KiB
+
+struct G3Cursor {  // a position (unit, local K-tile) in the workgroup's flat K-tile stream
+  int u, t, kt0, nk, m0, n0;
+};
 
 template <int MODE>
 __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
@@ -657,14 +668,33 @@ __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, u
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
-  const int64_t M = d.M, N = d.N, K = d.K;
-  const int tiles_n = (int)((N + G3_BN - 1) / G3_BN);
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = lid / split, sp = lid % split;
-  const int64_t m0 = (int64_t)(tile / tiles_n) * G3_BM, n0 = (int64_t)(tile % tiles_n) * G3_BN;
-  const int nk_all = (int)(K / BK);
-  const int kt0 = (int)((int64_t)nk_all * sp / split), kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
-  const int nk = kt1 - kt0;
+  const int M = (int)d.M, N = (int)d.N;
+  const int tiles_n = (N + G3_BN - 1) / G3_BN;
+  const int units = ((M + G3_BM - 1) / G3_BM) * tiles_n * split;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x), G = gridDim.x;
+  const int nk_all = (int)(d.K / BK);
+
+  auto set_unit = [&](G3Cursor& c, int u) {
+    c.u = u;
+    c.t = 0;
+    if (u < units) {
+      const int tile = u / split, sp = u % split;
+      c.kt0 = (int)((int64_t)nk_all * sp / split);
+      c.nk = (int)((int64_t)nk_all * (sp + 1) / split) - c.kt0;
+      c.m0 = (tile / tiles_n) * G3_BM;
+      c.n0 = (tile % tiles_n) * G3_BN;
+    }
+  };
+  auto advance = [&](G3Cursor& c) {
+    if (++c.t == c.nk) set_unit(c, c.u + G);
+  };
+  int total = 0;  // K-tiles this workgroup streams
+  for (int u = lid; u < units; u += G) {
+    G3Cursor c;
+    set_unit(c, u);
+    total += c.nk;
+  }
+  if (total == 0) return;
 
   const int rb = lane >> 3;
   const uint32_t lc16 = (uint32_t)(((lane & 7) ^ rb) * 16);
@@ -672,41 +702,35 @@ __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, u
   const __amdgpu_buffer_rsrc_t ra1 =
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.a1 ? d.a1 : d.a0), 0, d.a1 ? a1_bytes : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, w_bytes, 0x00020000);
+  const uint32_t lda0b = (uint32_t)d.lda0 * 2, lda1b = (uint32_t)d.lda1 * 2, ldwb = (uint32_t)d.ldw * 2;
 
-  // DMA slots (wave-uniform LDS bases, per-lane source offsets): X part q, slot j covers
-  // A rows 128*wr + 64*q + 8*(2*wc + j) + 0..7; W part q, slot j covers W rows
-  // 64*c + 32*q + rr + 0..7 with (c, rr) from g = 2*wid + j.
-  uint32_t xsrc0[2][2], xsrc1[2][2], xdst[2][2], wsrc[2][2], wdst[2][2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int xr = 128 * wr + 64 * q + 8 * (2 * wc + j);
-      xdst[q][j] = (uint32_t)(xr * 128);
-      int64_t m = m0 + xr + rb;
-      m = m < M ? m : M - 1;
-      xsrc0[q][j] = (uint32_t)(m * d.lda0 * 2) + lc16;
-      xsrc1[q][j] = (uint32_t)(m * d.lda1 * 2) + lc16;
-      const int g = 2 * wid + j;
-      const int wrow = 64 * (g >> 2) + 32 * q + 8 * (g & 3);
-      wdst[q][j] = (uint32_t)(G3_A_BYTES + wrow * 128);
-      int64_t n = n0 + wrow + rb;
-      n = n < N ? n : N - 1;
-      wsrc[q][j] = (uint32_t)(n * d.ldw * 2) + lc16;
-    }
-  auto dma_x = [&](int q, int tk) {  // X part q of local K-tile tk
-    char* st = smem + (tk & 1) * G3_STAGE;
-    const int kb = (kt0 + tk) * BK;
+  // DMA slots (wave-uniform LDS offsets; per-lane source rows from the cursor's tile): X part
+  // q, slot j covers A rows 128*wr + 64*q + 8*(2*wc + j) + 0..7; W part q, slot j covers W
+  // rows 64*c + 32*q + rr + 0..7 with (c, rr) from g = 2*wid + j.
+  auto dma_x = [&](int q, const G3Cursor& c, int T) {  // X part q of flat K-tile T (at cursor c)
+    char* st = smem + (T & 1) * G3_STAGE;
+    const int kb = (c.kt0 + c.t) * BK;
     const bool s0 = kb < d.k0;
     const uint32_t koff = (uint32_t)(s0 ? kb : kb - (int)d.k0) * 2;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) dma16(s0 ? ra0 : ra1, st + xdst[q][j], (s0 ? xsrc0[q][j] : xsrc1[q][j]) + koff);
+    for (int j = 0; j < 2; ++j) {
+      const int xr = 128 * wr + 64 * q + 8 * (2 * wc + j);
+      int m = c.m0 + xr + rb;
+      m = m < M ? m : M - 1;
+      dma16(s0 ? ra0 : ra1, st + xr * 128, (uint32_t)m * (s0 ? lda0b : lda1b) + lc16 + koff);
+    }
   };
-  auto dma_w = [&](int q, int tk) {
-    char* st = smem + (tk & 1) * G3_STAGE;
-    const uint32_t koff = (uint32_t)((kt0 + tk) * BK) * 2;
+  auto dma_w = [&](int q, const G3Cursor& c, int T) {
+    char* st = smem + (T & 1) * G3_STAGE;
+    const uint32_t koff = (uint32_t)((c.kt0 + c.t) * BK) * 2;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) dma16(rw, st + wdst[q][j], wsrc[q][j] + koff);
+    for (int j = 0; j < 2; ++j) {
+      const int g = 2 * wid + j;
+      const int wrow = 64 * (g >> 2) + 32 * q + 8 * (g & 3);
+      int n = c.n0 + wrow + rb;
+      n = n < N ? n : N - 1;
+      dma16(rw, st + G3_A_BYTES + wrow * 128, (uint32_t)n * ldwb + lc16 + koff);
+    }
   };
 
   // fragment LDS offsets (bytes within a stage): rows differ by multiples of 16
@@ -727,25 +751,30 @@ __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, u
 #pragma unroll
     for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // cursors of flat K-tiles T (compute), T+1 and T+2 (DMA)
+  G3Cursor c0, c1, c2;
+  set_unit(c0, lid);
+  c1 = c0;
+  advance(c1);
+  c2 = c1;
+  advance(c2);
   // ---- prologue: K-tile 0 complete, K-tile 1's X0/W0/W1 in flight
-  if (nk > 0) {
-    dma_x(0, 0); dma_w(0, 0); dma_w(1, 0); dma_x(1, 0);
-    if (nk > 1) {
-      dma_x(0, 1); dma_w(0, 1); dma_w(1, 1);
-      wait_vm<10>();
-    } else {
-      wait_vm<0>();
-    }
+  dma_x(0, c0, 0); dma_w(0, c0, 0); dma_w(1, c0, 0); dma_x(1, c0, 0);
+  if (total > 1) {
+    dma_x(0, c1, 1); dma_w(0, c1, 1); dma_w(1, c1, 1);
+    wait_vm<10>();
+  } else {
+    wait_vm<0>();
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger
 
   bf16x8 w0f[2][2], w1f[2][2], xf[4][2];
-  for (int t = 0; t < nk; ++t) {
-    const char* st = smem + (t & 1) * G3_STAGE;
-    const bool deep = t + 2 < nk;
-#define G3_SYNC_MFMA(H, G, WF)                                                                     \
+  for (int T = 0; T < total; ++T) {
+    const char* st = smem + (T & 1) * G3_STAGE;
+    const bool deep = T + 2 < total;
+#define G3_SYNC_MFMA(H, G_, WF)                                                                    \
     if (deep) wait_vm<10>(); else wait_vm<0>();                                                     \
     __builtin_amdgcn_s_barrier();                                                                   \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                              \
@@ -753,11 +782,11 @@ __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, u
     _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                \
       _Pragma("unroll") for (int a = 0; a < 2; ++a)                                                 \
         _Pragma("unroll") for (int b = 0; b < 4; ++b)                                               \
-          acc[2 * (G) + a][4 * (H) + b] =                                                           \
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(WF[a][ks], xf[b][ks], acc[2 * (G) + a][4 * (H) + b], 0, 0, 0); \
+          acc[2 * (G_) + a][4 * (H) + b] =                                                          \
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(WF[a][ks], xf[b][ks], acc[2 * (G_) + a][4 * (H) + b], 0, 0, 0); \
     __builtin_amdgcn_s_setprio(0);                                                                  \
     __builtin_amdgcn_s_barrier();
-    // ---- phase 0: read W0, X0; DMA X1 of t+1; Q(x0, w0)
+    // ---- phase 0: read W0, X0; DMA X1 of T+1; Q(x0, w0)
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -767,44 +796,53 @@ __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, u
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) xf[b][ks] = *(const bf16x8*)(st + xl[0][ks] + b * 16 * BK * 2);
-    if (t + 1 < nk) dma_x(1, t + 1);
+    if (T + 1 < total) dma_x(1, c1, T + 1);
     G3_SYNC_MFMA(0, 0, w0f)
-    // ---- phase 1: read W1; DMA X0 of t+2; Q(x0, w1)
+    // ---- phase 1: read W1; DMA X0 of T+2; Q(x0, w1)
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) w1f[a][ks] = *(const bf16x8*)(st + wl[1][ks] + a * 16 * BK * 2);
-    if (deep) dma_x(0, t + 2);
+    if (deep) dma_x(0, c2, T + 2);
     G3_SYNC_MFMA(0, 1, w1f)
-    // ---- phase 2: read X1; DMA W0 of t+2; Q(x1, w1)
+    // ---- phase 2: read X1; DMA W0 of T+2; Q(x1, w1)
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) xf[b][ks] = *(const bf16x8*)(st + xl[1][ks] + b * 16 * BK * 2);
-    if (deep) dma_w(0, t + 2);
+    if (deep) dma_w(0, c2, T + 2);
     G3_SYNC_MFMA(1, 1, w1f)
-    // ---- phase 3: DMA W1 of t+2; Q(x1, w0)
-    if (deep) dma_w(1, t + 2);
+    // ---- phase 3: DMA W1 of T+2; Q(x1, w0)
+    if (deep) dma_w(1, c2, T + 2);
     G3_SYNC_MFMA(1, 0, w0f)
 #undef G3_SYNC_MFMA
-  }
-  if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
-
-  const int mbase = (int)m0 + 128 * wr, nbase = (int)n0 + 64 * wc;
-  if (split == 1) {
-    gemm_epilogue<8, 4>(d, acc, mbase, nbase, lane);
-  } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
-    float* slab = (float*)d.ws + (int64_t)sp * M * N;
+    if (c0.t + 1 == c0.nk) {  // unit finished
+      if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+      const int mbase = c0.m0 + 128 * wr, nbase = c0.n0 + 64 * wc;
+      if (split == 1) {
+        gemm_epilogue<8, 4>(d, acc, mbase, nbase, lane);
+      } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
+        float* slab = (float*)d.ws + (int64_t)(c0.u % split) * d.M * d.N;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int64_t n = nbase + a * 16 + 4 * fq;
-      if (n >= N) continue;
+        for (int a = 0; a < 4; ++a) {
+          const int64_t n = nbase + a * 16 + 4 * fq;
+          if (n >= N) continue;
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const int64_t m = mbase + b * 16 + fr;
-        if (m < M) *(float4*)(slab + m * N + n) = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+          for (int b = 0; b < 8; ++b) {
+            const int64_t m = mbase + b * 16 + fr;
+            if (m < M) *(float4*)(slab + m * d.N + n) = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+          }
+        }
       }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (wr == 1 && T + 1 < total) __builtin_amdgcn_s_barrier();  // re-stagger
     }
+    advance(c0);
+    advance(c1);
+    advance(c2);
   }
 }
 
@@ -1609,10 +1647,14 @@ int launch6(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   return vd_launch_status();
 }
 
-int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
+int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split,
+            bool persistent) {
   const int64_t units = ((d.M + G3_BM - 1) / G3_BM) * ((d.N + G3_BN - 1) / G3_BN) * split;
   if (units > 0x7fffffff) return VD_EINVAL;
-  hipLaunchKernelGGL((gemm3_kernel<VD_A_DENSE>), dim3((unsigned)units), dim3(G3_NT), 0, s, d, a0b, a1b, wb, split);
+  // persistent: one workgroup per CU, ceil(units / CUs) units each, balanced grid
+  const int64_t rounds = persistent ? (units + g_num_cus - 1) / g_num_cus : 1;
+  const int64_t grid = (units + rounds - 1) / rounds;
+  hipLaunchKernelGGL((gemm3_kernel<VD_A_DENSE>), dim3((unsigned)grid), dim3(G3_NT), 0, s, d, a0b, a1b, wb, split);
   int rc = vd_launch_status();
   if (rc != VD_OK || split == 1) return rc;
   const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
@@ -1624,11 +1666,13 @@ int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
 int g_path = 0;  // 0 auto, 1 v1, 2 v2, 3 v3, 5 v5, 6 v6, 7 auto without v6, 8 v6 unsplit,
-                  // 9 auto with split-K cap 8 (tests / benchmarks)
+                  // 9 auto with split-K cap 8, 10 v3 one unit per workgroup, 11 auto with v3
+                  // one unit per workgroup (tests / benchmarks)
 
 struct Plan {
   int ver = 1;
   int bn = 128, split = 1;
+  bool persist = true;  // v3: persistent flat K-tile stream
   uint32_t a0b = 0, a1b = 0, wb = 0;
   int64_t ws_bytes = 0;
 };
@@ -1675,7 +1719,7 @@ Plan plan(const vd_gemm_desc& d) {
   // fewer rows than one 256-row tile (the deep levels of a 1-2 image rank): 64 x 64 tiles
   // (v1's 128-row tiles left L4's K = 11520 convs on 8 workgroups: 453 us vs ~30)
   if (d.M < G2_BM) {
-    if (!k64 || d.kt > 1 || d.ks == 1 || (g_path != 0 && g_path != 6 && g_path != 8)) return p;  // v6: 2-D 3x3 taps
+    if (!k64 || d.kt > 1 || d.ks == 1 || (g_path != 0 && g_path != 6 && g_path != 8 && g_path != 11)) return p;  // v6: 2-D 3x3 taps
     p.ver = 6;
     p.bn = 64;
     return p;
@@ -1693,7 +1737,7 @@ Plan plan(const vd_gemm_desc& d) {
   // it wins (tools/kbench.py: the L1 attention QKV projection M 131072 x N 960 x K 320)
   const bool v5auto = d.a_mode == VD_A_DENSE && d.M >= 65536 && d.K <= 320 && d.N % 320 == 0 && d.N >= 640 &&
                       d.N < 2560 && !d.res && !d.rowbias && d.act != VD_ACT_GEGLU;
-  if (g_path == 5 || ((g_path == 0 || g_path == 7) && (!k64 || v5auto))) {
+  if (g_path == 5 || ((g_path == 0 || g_path == 7 || g_path == 11) && (!k64 || v5auto))) {
     if (!cin32) return p;
     p.ver = 5;
     p.bn = 320;
@@ -1716,7 +1760,7 @@ Plan plan(const vd_gemm_desc& d) {
     const bool v6auto = tiles256 < g_num_cus && (d.N <= 1280 || tiles6 <= 4 * g_num_cus) &&
                         (d.act != VD_ACT_GEGLU || 2 * tiles256 <= g_num_cus) &&
                         (d.K <= 1280 || (d.K <= 2560 && tiles6 >= 2 * g_num_cus));
-    if (g_path == 6 || g_path == 8 || (g_path == 0 && v6auto)) {
+    if (g_path == 6 || g_path == 8 || ((g_path == 0 || g_path == 11) && v6auto)) {
       p.ver = 6;
       p.bn = 64;
       int64_t sp = 1;
@@ -1730,6 +1774,7 @@ Plan plan(const vd_gemm_desc& d) {
     }
   }
   const bool v3ok = d.a_mode == VD_A_DENSE && d.N >= 256 && g_path != 2;
+  p.persist = g_path != 10 && g_path != 11;
   const int64_t p256 = (d.N + 255) / 256 * 256;
   // measured (tools/kbench.py): v3 wins on the wide projections (qkv, GEGLU) once the
   // grid fills the chip without split-K; v2's persistent stream wins on N <= 640 and
@@ -1737,9 +1782,11 @@ Plan plan(const vd_gemm_desc& d) {
   // DiT (tools/dit_kbench.py, M 147456): N 1152 = 4.5 tiles still wins on v3 at K >= 1024
   // (426 vs 500 us at K 1152, 1431 vs 1666 us at K 4608), so the padding bound loosens to
   // 1/8 there; no UNet shape has N >= 768 with K >= 1024 at M >= 65536
-  const bool v3pad = (p256 - d.N) * 16 <= d.N || (d.K >= 1024 && d.M >= 65536 && (p256 - d.N) * 8 <= d.N);
+  // persistent v3 (round 2) also wins at 1/8 padding with short K: L2 qkv N 1920 -> 2048,
+  // K 640: 98 vs 109 us on v2 (profiles/r02_gemm3_persistent.txt)
+  const bool v3pad = (p256 - d.N) * 8 <= d.N;
   const bool v3auto = v3ok && d.N >= 768 && v3pad && ((d.M + G3_BM - 1) / G3_BM) * (p256 / 256) >= 256;
-  if (g_path == 3 ? v3ok : v3auto) {
+  if (g_path == 3 || g_path == 10 ? v3ok : v3auto) {
     p.ver = 3;
     p.bn = 256;
     p.split = split_for(((d.M + G3_BM - 1) / G3_BM) * (p256 / 256), nk);
@@ -1776,7 +1823,7 @@ extern "C" int vd_gemm_force_v1(int32_t on) {
   return VD_OK;
 }
 extern "C" int vd_gemm_select_path(int32_t path) {
-  if (path < 0 || path > 9 || path == 4) return VD_EINVAL;
+  if (path < 0 || path > 11 || path == 4) return VD_EINVAL;
   g_split_cap = path == 9 ? 8 : 32;
   g_path = path == 9 ? 0 : path;
   return VD_OK;
@@ -1826,7 +1873,7 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   if (d.act == VD_ACT_GEGLU) VD_CHECK_ARG(d.N % 32 == 0 && !d.res && !d.rowbias && !d.out_f32);
   const Plan p = plan(d);
   if (p.ver >= 2 && p.split > 1) VD_CHECK_ARG(d.ws && al16(d.ws) && d.ws_bytes >= p.ws_bytes);
-  if (p.ver == 3) return launch3(d, s, p.a0b, p.a1b, p.wb, p.split);
+  if (p.ver == 3) return launch3(d, s, p.a0b, p.a1b, p.wb, p.split, p.persist);
   if (p.ver == 6) return launch6(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 5) return launch4<320, 4, 2, 4>(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 2)
