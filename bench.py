@@ -145,6 +145,9 @@ def main():
     ap.add_argument("--overlap", type=int, default=1,
                     help="N>1: chunk each motion module's all-to-alls over positions and overlap them with "
                          "the transformer block on a second stream (vdiff.dist.FrameShard overlap_chunks)")
+    ap.add_argument("--window", default="a2a", choices=["a2a", "kv-gather"],
+                    help="N>1: motion-module temporal window — all-to-all re-shard (default) or the north "
+                         "star's K/V all-gather over the frame shards (vdiff.dist.FrameShard window)")
     ap.add_argument("--layout", default="auto", choices=["auto", "frame", "cfg-frame"],
                     help="N>1 placement (vdiff.dist.layout): auto = cfg-frame at 2 GPUs, frame otherwise")
     args = ap.parse_args()
@@ -164,7 +167,8 @@ def main():
     frames = args.frames or (16 if cfg_name == "full" else 4)
     t0 = time.time()
     from vdiff.dist import NodeLayout
-    lay = NodeLayout(args.layout, frames, cfg=True, world=world, rank=rank, overlap_chunks=args.overlap)
+    lay = NodeLayout(args.layout, frames, cfg=True, world=world, rank=rank, overlap_chunks=args.overlap,
+                     window=args.window)
     unet = materialize_synthetic(cfg_name, device="cuda", seed=0)
     unet.dist = lay.frame_shard
     unet.prepare()
@@ -210,7 +214,8 @@ def main():
     if not args.no_nocfg:
         # no CFG pair to split: frame-shard over all ranks
         del loop
-        lay1 = lay if lay.layout == "frame" else NodeLayout("frame", frames, cfg=False, world=world, rank=rank)
+        lay1 = lay if lay.layout == "frame" else NodeLayout("frame", frames, cfg=False, world=world, rank=rank,
+                                                             overlap_chunks=args.overlap, window=args.window)
         unet.dist = lay1.frame_shard
         lat1 = lat_all[:, :, lay1.frame_slice()].cuda()
         loop1 = DenoiseLoop(unet, sched, lat1, ehs[1:].cuda(), 1.0, timesteps=ts, use_graph=not args.no_graph)

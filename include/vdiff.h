@@ -193,6 +193,18 @@ int vd_temporal_attention(const void* q, const void* k, const void* v, int64_t l
                           void* o, int64_t ldo, int64_t batch, int32_t frames,
                           int64_t positions, int32_t heads, int32_t d, float scale,
                           vd_stream_t stream);
+/* Temporal attention of a frame-sharded rank under the K/V all-gather layout (SURVEY.md §8e,
+ * the north star's "RCCL all-gather for the temporal-attention window"): the rank's own
+ * qframes query frames, rows (b*qframes + f)*positions + p of q (stride ldq) and o (stride
+ * ldo), against all kframes key frames gathered from every rank, rows
+ * (b*kframes + f)*positions + p of k and v (stride ldkv).  Replaces, for the rank's frames,
+ * the rows of diffusers' temporal Attention (motion_module.py: attention over the
+ * (B*H*W, F, C) sequence; 03_trace_forward_pass.py:160-169).  qframes <= kframes <= 16;
+ * d in {32, 40, 64, 80, 160} (else VD_EUNSUPPORTED). */
+int vd_temporal_attention_kv(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv,
+                             void* o, int64_t ldo, int64_t batch, int32_t qframes, int32_t kframes,
+                             int64_t positions, int32_t heads, int32_t d, float scale,
+                             vd_stream_t stream);
 /* vd_temporal_attention for the DiT's temporal blocks (d = 64, 17..32 frames) with the 1-D
  * temporal RoPE (vd_rope_qk mode 1, angle by frame) applied to q/k inside the kernel as they
  * are loaded; q and k are read un-rotated and left unchanged.  Returns VD_EUNSUPPORTED while
@@ -202,7 +214,7 @@ int vd_temporal_attention_rope(const void* q, const void* k, const void* v, int6
                                int32_t heads, int32_t d, float scale, float theta,
                                vd_stream_t stream);
 /* Test/benchmark hook: on != 0 forces the VALU temporal kernel (default: the MFMA kernel
- * for frames <= 16 and d in {40, 80, 160}). */
+ * for frames <= 16 and d in {32, 40, 64, 80, 160}, frames 17..32 and d in {40, 64, 80, 160}). */
 int vd_temporal_force_valu(int32_t on);
 
 /* Row softmax over fp32 scores in log2 units (p = exp2(s - max) / sum, bf16 out):

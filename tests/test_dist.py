@@ -98,6 +98,10 @@ def _worker(rank, world, port, errq):
         assert torch.equal(plain, over), "overlapped temporal window"
         full_mix = mix(base, B, F, HW2).reshape(B, F, HW2, 8)[:, rank * Fl:(rank + 1) * Fl].reshape(-1, 8)
         assert torch.allclose(plain, full_mix, atol=1e-5), "temporal window content"
+        # ---- 1c. the K/V all-gather window (FrameShard(window="kv-gather")): every rank ends
+        # with the rows (b, f, p) of ALL frames, in the unsharded order
+        kvfs = FrameShard(window="kv-gather")
+        assert torch.equal(kvfs.gather_kv_frames(loc2, B, Fl, HW2, bt), base), "gather_kv_frames content"
         # ---- 2. sharded motion module == unsharded oracle
         sd = {}
         p = "m"

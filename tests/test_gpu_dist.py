@@ -56,10 +56,13 @@ def test_sharded_loop_world1_matches_unsharded(pg):
     assert torch.equal(out, ref)
 
 
-def test_overlapped_window_world1_rccl_graph(pg):
-    """FrameShard(overlap_chunks=2) on the real RCCL backend: the chunked all-to-alls run on a
-    side stream joined by events, all captured into the step's hipGraph; at world size 1 every
-    all-to-all is an identity, so the loop must equal the unsharded one bit for bit."""
+@pytest.mark.parametrize("kw", [dict(overlap_chunks=2), dict(window="kv-gather")])
+def test_overlapped_window_world1_rccl_graph(pg, kw):
+    """FrameShard(overlap_chunks=2) on the real RCCL backend: the chunked motion blocks run on a
+    side stream joined by events, all captured into the step's hipGraph; FrameShard(window=
+    "kv-gather"): the K/V all-gathers (RCCL all_gather_into_tensor) captured likewise.  At world
+    size 1 every collective is an identity, so the loop must equal the unsharded one bit for bit
+    (kv-gather splits the QKV GEMM into Q and KV GEMMs: same products, same fp32 sums)."""
     torch.manual_seed(0)
     unet = init_synthetic_(UNetMotionModel("tiny"), seed=3).to("cuda", torch.bfloat16).prepare()
     lat = torch.randn(1, 4, 4, 64, 64, device="cuda")
@@ -67,7 +70,7 @@ def test_overlapped_window_world1_rccl_graph(pg):
     s = DDIMScheduler(beta_schedule="linear", steps_offset=1, clip_sample=False)
     s.set_timesteps(50)
     ref = DenoiseLoop(unet, s, lat, ehs, 7.5, use_graph=True).prime().run(2).clone()
-    fs = FrameShard(overlap_chunks=2)
+    fs = FrameShard(**kw)
     unet.dist = fs
     try:
         loop = DenoiseLoop(unet, s, lat, ehs, 7.5, use_graph=True).prime()

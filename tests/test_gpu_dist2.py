@@ -57,7 +57,7 @@ def _sched():
     return s
 
 
-def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2, overlap=1):
+def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2, overlap=1, window="a2a"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -74,6 +74,9 @@ def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2, ov
             got = super()._a2a(x.cpu()).to(x.device)
             return got if out is None else out.copy_(got)
 
+        def _all_gather(self, x):
+            return super()._all_gather(x.cpu()).to(x.device)
+
         def all_gather_frames(self, x):
             return super().all_gather_frames(x.cpu())
 
@@ -84,7 +87,7 @@ def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2, ov
     try:
         unet = _model(cfg)
         lay = NodeLayout(layout, FRAMES if cfg == "tiny" else FULL_FRAMES, world=world, rank=rank)
-        fs = (HostStagedShard(lay.frame_shard.group, overlap_chunks=overlap)
+        fs = (HostStagedShard(lay.frame_shard.group, overlap_chunks=overlap, window=window)
               if lay.frame_shard is not None else None)
         cs = HostStagedCfg(lay.cfg_shard.group) if lay.cfg_shard is not None else None
         unet.dist = fs
@@ -110,17 +113,20 @@ def unsharded_ref(cuda):
     return DenoiseLoop(_model(), _sched(), lat.cuda(), ehs.cuda(), 7.5, use_graph=False).prime().run(2).cpu()
 
 
-@pytest.mark.parametrize("world,layout,overlap", [(2, "frame", 1), (4, "frame", 1), (8, "frame", 1),
-                                                  (2, "cfg-frame", 1), (4, "cfg-frame", 1), (8, "cfg-frame", 1),
-                                                  (2, "frame", 2), (4, "cfg-frame", 4)])
-def test_ranks_on_one_gpu_match_unsharded(unsharded_ref, world, layout, overlap):
+@pytest.mark.parametrize("world,layout,overlap,window",
+                         [(2, "frame", 1, "a2a"), (4, "frame", 1, "a2a"), (8, "frame", 1, "a2a"),
+                          (2, "cfg-frame", 1, "a2a"), (4, "cfg-frame", 1, "a2a"), (8, "cfg-frame", 1, "a2a"),
+                          (2, "frame", 2, "a2a"), (4, "cfg-frame", 4, "a2a"),
+                          (2, "frame", 1, "kv-gather"), (4, "frame", 1, "kv-gather"), (8, "cfg-frame", 1, "kv-gather")])
+def test_ranks_on_one_gpu_match_unsharded(unsharded_ref, world, layout, overlap, window):
     """layout "cfg-frame" (SURVEY §8e (ii)): the two CFG halves on two rank groups, eps
     swapped between CFG pairs before the update; at world 2 no motion-module collective.
-    overlap > 1: the motion modules' all-to-alls chunked over positions on a side stream."""
+    overlap > 1: the motion modules' all-to-alls chunked over positions on a side stream.
+    window "kv-gather": rows stay frame-sharded, every temporal attention's K/V all-gathered."""
     ref = unsharded_ref
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "out.pt")
-        mp.start_processes(_worker, args=(world, _port(), path, layout, "tiny", 2, overlap), nprocs=world,
+        mp.start_processes(_worker, args=(world, _port(), path, layout, "tiny", 2, overlap, window), nprocs=world,
                            join=True, start_method="spawn")
         got = torch.load(path, weights_only=True)
     assert got.shape == ref.shape

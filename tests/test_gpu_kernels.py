@@ -667,7 +667,7 @@ def temporal_path(request, cuda):
 
 @pytest.mark.parametrize("frames,d,scale", [(16, 40, None), (16, 80, None), (16, 160, None), (5, 40, None),
                                             (1, 80, None), (12, 160, None), (16, 40, "unit"), (4, 32, None),
-                                            (32, 80, None), (5, 64, None)])
+                                            (16, 32, None), (32, 80, None), (5, 64, None)])
 def test_temporal_attention(temporal_path, frames, d, scale):
     batch, pos, heads = 2, 37, 3
     C = heads * d
@@ -684,6 +684,29 @@ def test_temporal_attention(temporal_path, frames, d, scale):
     want = sdpa_ref(tok(q), tok(k), tok(v), batch * pos, heads, frames, frames, d)
     want = want.reshape(batch, pos, frames, C).permute(0, 2, 1, 3).reshape(-1, C)
     close_bf16(got, want)
+
+
+@pytest.mark.parametrize("d", [32, 40, 80, 160])
+@pytest.mark.parametrize("frames,qf,f0", [(16, 2, 6), (16, 4, 12), (8, 8, 0), (16, 1, 15)])
+def test_temporal_attention_kv(cuda, frames, qf, f0, d):
+    """vd_temporal_attention_kv (the K/V all-gather window): a rank's qf query frames
+    [f0, f0 + qf) in their own rows against all frames' K/V equals those frames' rows of the
+    full self-attention bit for bit (same MFMA operands and order), and fp64 SDPA."""
+    batch, pos, heads = 2, 37, 2
+    C = heads * d
+    qkv = rnd(batch * frames * pos, 3 * C, std=1.5)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    full = ops.temporal_attention(q, k, v, batch, frames, pos, heads, d)
+    mine = lambda t: t.reshape(batch, frames, pos, -1)[:, f0:f0 + qf].reshape(-1, t.shape[1]).contiguous()
+    kv = torch.cat([k, v], 1)   # the gathered [rows][2C] buffer
+    got = ops.temporal_attention_kv(mine(q), kv[:, :C], kv[:, C:], batch, qf, frames, pos, heads, d)
+    assert torch.equal(got, mine(full))
+
+    def tok(t, f):
+        return t.double().reshape(batch, f, pos, C).permute(0, 2, 1, 3).reshape(batch * pos, f, C)
+
+    want = sdpa_ref(tok(mine(q), qf), tok(k, frames), tok(v, frames), batch * pos, heads, qf, frames, d)
+    close_bf16(got, want.reshape(batch, pos, qf, C).permute(0, 2, 1, 3).reshape(-1, C))
 
 
 # ---------------------------------------------------------------- step glue

@@ -29,8 +29,8 @@ from vdiff.weights import materialize_synthetic  # noqa: E402
 
 
 class EmulatedShard(FrameShard):
-    def __init__(self, world, chunks, comm):
-        self.group, self.world, self.rank, self.chunks = None, world, 0, chunks
+    def __init__(self, world, chunks, comm, window="a2a"):
+        self.group, self.world, self.rank, self.chunks, self.window = None, world, 0, chunks, window
         self._side = {}
         self.comm = comm
 
@@ -38,6 +38,12 @@ class EmulatedShard(FrameShard):
         out = torch.empty_like(x) if out is None else out
         if self.comm == "copy":
             out.copy_(x)
+        return out
+
+    def _all_gather(self, x):
+        out = torch.empty((self.world * x.shape[0],) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+        if self.comm == "copy":
+            out.view(self.world, *x.shape).copy_(x.unsqueeze(0).expand(self.world, *x.shape))
         return out
 
     def gather_gn_partials(self, ws):
@@ -53,6 +59,7 @@ def main():
     ap.add_argument("--chunks", type=int, nargs="+", default=[1, 2, 4])
     ap.add_argument("--comm", default="copy", choices=["copy", "none"])
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--window", default="a2a", choices=["a2a", "kv-gather"])
     ap.add_argument("--frames", type=int, default=16)
     args = ap.parse_args()
     unet = materialize_synthetic("full", device="cuda", seed=0)
@@ -64,7 +71,7 @@ def main():
     ts = s.timesteps.repeat(2)
     res = {}
     for c in args.chunks:
-        unet.dist = EmulatedShard(args.world, c, args.comm) if args.world > 1 else None
+        unet.dist = EmulatedShard(args.world, c, args.comm, args.window) if args.world > 1 else None
         unet.prepare()
         loop = DenoiseLoop(unet, s, lat, ehs, 7.5, timesteps=ts, use_graph=True).prime()
         assert loop.graph is not None, loop.graph_error
@@ -75,9 +82,11 @@ def main():
         torch.cuda.synchronize()
         ms = 1e3 * (time.perf_counter() - t0) / args.steps
         res[c] = round(ms, 3)
-        print(f"world {args.world} frames/rank {fl} chunks {c} comm {args.comm}: {ms:.3f} ms/step", flush=True)
+        print(f"world {args.world} frames/rank {fl} window {args.window} chunks {c} comm {args.comm}: {ms:.3f} ms/step",
+              flush=True)
         del loop
-    print(json.dumps({"world": args.world, "frames_local": fl, "comm": args.comm, "ms_per_step": res}))
+    print(json.dumps({"world": args.world, "frames_local": fl, "window": args.window, "comm": args.comm,
+                      "ms_per_step": res}))
 
 
 if __name__ == "__main__":

@@ -1378,11 +1378,15 @@ struct TmCfg {
   static constexpr int DCH = D / 8;
 };
 
+// Query and key frames may differ (vd_temporal_attention_kv: a frame-sharded rank's own
+// qframes queries against all kframes keys gathered from every rank, SURVEY §8e's K/V
+// all-gather); q/o rows are (b, qframes, p) at stride ldq/ldo, k/v rows (b, kframes, p) at
+// stride ldkv.  The self-attention call passes qframes == kframes and one stride.
 template <int D>
 __global__ __launch_bounds__(NT) void temporal_mfma_kernel(
-    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, int64_t ld,
-    bf16_t* __restrict__ o, int64_t ldo, int64_t batch, int frames, int64_t positions, int heads,
-    float c) {
+    const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    int64_t ldkv, bf16_t* __restrict__ o, int64_t ldo, int64_t batch, int qframes, int frames, int64_t positions,
+    int heads, float c) {
   using C = TmCfg<D>;
   __shared__ __attribute__((aligned(16))) bf16_t vimg[4][16 * C::VS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1405,15 +1409,17 @@ __global__ __launch_bounds__(NT) void temporal_mfma_kernel(
     const int h = (int)(item % heads);
     const int64_t bp = item / heads;
     const int64_t p = bp % positions, b = bp / positions;
-    const int64_t row0 = b * frames * positions + p;  // row of frame 0; frame f at + f * positions
-    const bool fok = fr < frames;
-    const int64_t rf = (row0 + (fok ? fr : 0) * positions) * ld + (int64_t)h * D;
+    const int64_t row0 = b * frames * positions + p;   // key row of frame 0; frame f at + f * positions
+    const int64_t qrow0 = b * qframes * positions + p;  // query / output row of frame 0
+    const bool fok = fr < frames, qok = fr < qframes;
+    const int64_t rf = (row0 + (fok ? fr : 0) * positions) * ldkv + (int64_t)h * D;
+    const int64_t rq = (qrow0 + (qok ? fr : 0) * positions) * ldq + (int64_t)h * D;
     // ---- V rows -> LDS (d < D only)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous item's tr reads done
     for (int idx = lane; idx < frames * C::DCH; idx += 64) {
       const int f = idx / C::DCH, cc = idx - f * C::DCH;
       *(uint4*)(vl + f * C::VS + cc * 8) =
-          *(const uint4*)(v + (row0 + (int64_t)f * positions) * ld + (int64_t)h * D + cc * 8);
+          *(const uint4*)(v + (row0 + (int64_t)f * positions) * ldkv + (int64_t)h * D + cc * 8);
     }
     // ---- S^T = K . Q^T
     f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1421,9 +1427,9 @@ __global__ __launch_bounds__(NT) void temporal_mfma_kernel(
     for (int ks = 0; ks < C::KSTEPS; ++ks) {
       const int dd = ks * 32 + 8 * fq;
       uint4 kq = make_uint4(0, 0, 0, 0), qq = make_uint4(0, 0, 0, 0);
-      if (dd < D && fok) {
-        kq = *(const uint4*)(k + rf + dd);
-        qq = *(const uint4*)(q + rf + dd);
+      if (dd < D) {
+        if (fok) kq = *(const uint4*)(k + rf + dd);
+        if (qok) qq = *(const uint4*)(q + rq + dd);
       }
       s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kq), __builtin_bit_cast(bf16x8, qq), s,
                                                   0, 0, 0);
@@ -1458,8 +1464,8 @@ __global__ __launch_bounds__(NT) void temporal_mfma_kernel(
     // row sum = O^T row D: block D/16, lane group (D%16)/4, element D%4
     const float l = __shfl(ot[D / 16][(D % 16) % 4], ((D % 16) / 4) * 16 + fr, 64);
     const float inv = __builtin_amdgcn_rcpf(l);
-    if (fok) {
-      bf16_t* orow = o + (row0 + (int64_t)fr * positions) * ldo + (int64_t)h * D;
+    if (qok) {
+      bf16_t* orow = o + (qrow0 + (int64_t)fr * positions) * ldo + (int64_t)h * D;
 #pragma unroll
       for (int a = 0; a < C::DB; ++a) {
         const int dd = 16 * a + 4 * fq;
@@ -1746,14 +1752,16 @@ extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v
   const unsigned grid = (unsigned)((items + 3) / 4);
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  if (!g_temporal_valu && (d == 40 || d == 64 || d == 80 || d == 160) && ld % 8 == 0 && ldo % 4 == 0) {
+  if (!g_temporal_valu && (d == 40 || d == 64 || d == 80 || d == 160 || (d == 32 && frames <= 16)) && ld % 8 == 0 &&
+      ldo % 4 == 0) {
     const int64_t g = (items + 3) / 4;
     const unsigned grid2 = (unsigned)(g < 8192 ? g : 8192);
 #define TM_LAUNCH(KERN, DD)                                                                                 \
-    hipLaunchKernelGGL(KERN<DD>, dim3(grid2), dim3(NT), 0, s, (const bf16_t*)q, (const bf16_t*)k,           \
-                       (const bf16_t*)v, ld, (bf16_t*)o, ldo, batch, frames, positions, heads, sl2)
+    hipLaunchKernelGGL(KERN<DD>, dim3(grid2), dim3(NT), 0, s, (const bf16_t*)q, ld, (const bf16_t*)k,       \
+                       (const bf16_t*)v, ld, (bf16_t*)o, ldo, batch, frames, frames, positions, heads, sl2)
     if (frames <= 16) {
-      if (d == 40) TM_LAUNCH(temporal_mfma_kernel, 40);
+      if (d == 32) TM_LAUNCH(temporal_mfma_kernel, 32);
+      else if (d == 40) TM_LAUNCH(temporal_mfma_kernel, 40);
       else if (d == 64) TM_LAUNCH(temporal_mfma_kernel, 64);
       else if (d == 80) TM_LAUNCH(temporal_mfma_kernel, 80);
       else TM_LAUNCH(temporal_mfma_kernel, 160);
@@ -1783,6 +1791,31 @@ extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v
     hipLaunchKernelGGL(temporal_attn_kernel<32>, dim3(grid), dim3(NT), 0, s, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, ld, (bf16_t*)o, ldo, batch, frames,
                        positions, heads, d, sl2);
+  return vd_launch_status();
+}
+
+extern "C" int vd_temporal_attention_kv(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv,
+                                        void* o, int64_t ldo, int64_t batch, int32_t qframes, int32_t kframes,
+                                        int64_t positions, int32_t heads, int32_t d, float scale,
+                                        vd_stream_t stream) {
+  VD_CHECK_ARG(q && k && v && o && al16(q) && al16(k) && al16(v) && al16(o));
+  VD_CHECK_ARG(ldq % 8 == 0 && ldkv % 8 == 0 && ldo % 4 == 0);
+  VD_CHECK_ARG(qframes >= 1 && qframes <= kframes && kframes <= 16 && batch > 0 && positions > 0 && heads > 0);
+  if (!(d == 32 || d == 40 || d == 64 || d == 80 || d == 160)) return VD_EUNSUPPORTED;
+  const int64_t g = (batch * positions * heads + 3) / 4;
+  const unsigned grid = (unsigned)(g < 8192 ? g : 8192);
+  const float sl2 = scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+#define TKV_LAUNCH(DD)                                                                                      \
+  hipLaunchKernelGGL(temporal_mfma_kernel<DD>, dim3(grid), dim3(NT), 0, s, (const bf16_t*)q, ldq,           \
+                     (const bf16_t*)k, (const bf16_t*)v, ldkv, (bf16_t*)o, ldo, batch, qframes, kframes,       \
+                     positions, heads, sl2)
+  if (d == 32) TKV_LAUNCH(32);
+  else if (d == 40) TKV_LAUNCH(40);
+  else if (d == 64) TKV_LAUNCH(64);
+  else if (d == 80) TKV_LAUNCH(80);
+  else TKV_LAUNCH(160);
+#undef TKV_LAUNCH
   return vd_launch_status();
 }
 

@@ -34,13 +34,23 @@ import torch.distributed as dist
 
 
 class FrameShard:
-    def __init__(self, group=None, overlap_chunks: int = 1):
+    WINDOWS = ("a2a", "kv-gather")
+
+    def __init__(self, group=None, overlap_chunks: int = 1, window: str = "a2a"):
+        """window: how a motion module sees all frames — "a2a" re-shards rows frame ->
+        position shards and back (two all-to-alls per transformer block, the default), or
+        "kv-gather" keeps the rows frame-sharded and all-gathers every temporal attention's
+        K/V over the frame shards (SURVEY §8e's north-star collective: each rank's queries
+        against all frames' keys; 2 all-gathers per block, ≈ 8x the a2a bytes at N = 8)."""
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         if overlap_chunks < 1:
             raise ValueError("overlap_chunks must be >= 1")
+        if window not in self.WINDOWS:
+            raise ValueError(f"window must be one of {self.WINDOWS}")
         self.chunks = overlap_chunks
+        self.window = window
         self._side = {}  # device -> compute stream of the overlapped temporal window
 
     def frames_local(self, frames: int) -> int:
@@ -60,6 +70,18 @@ class FrameShard:
         out = torch.empty_like(x) if out is None else out
         dist.all_to_all_single(out, x, group=self.group)
         return out
+
+    def _all_gather(self, x: torch.Tensor) -> torch.Tensor:
+        """[R, w] per rank -> [world*R, w], rank-major (RCCL all-gather over xGMI)."""
+        out = torch.empty((self.world * x.shape[0],) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+        dist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
+        return out
+
+    def gather_kv_frames(self, kv, batch, frames_local, hw, transpose):
+        """rows (b, f_loc, p) of this rank's frames -> rows (b, f, p) of ALL frames (the
+        temporal K/V window of the "kv-gather" layout)."""
+        allr = self._all_gather(kv)                                  # (r, b, f_loc, p)
+        return transpose(allr, self.world, batch, frames_local * hw)  # (b, r, f_loc, p) = (b, f, p)
 
     def to_position_shards(self, h, batch, frames_local, hw, transpose):
         """rows (b, f_loc, p) of this rank's frames -> rows (b, f, p_loc) of this rank's

@@ -49,9 +49,10 @@ class NodeLayout:
     """Group construction for a layout; every rank must build it (new_group is collective)."""
 
     def __init__(self, layout: str = "auto", frames: int = 16, cfg: bool = True, world=None, rank=None,
-                 backend=None, overlap_chunks: int = 1):
+                 backend=None, overlap_chunks: int = 1, window: str = "a2a"):
         """overlap_chunks > 1: the motion modules' all-to-alls are chunked over positions and
-        overlapped with the transformer blocks on a second stream (FrameShard)."""
+        overlapped with the transformer blocks on a second stream (FrameShard).  window:
+        "a2a" (default) or "kv-gather" (FrameShard: the north star's K/V all-gather)."""
         self.world = dist.get_world_size() if world is None else world
         self.rank = dist.get_rank() if rank is None else rank
         self.layout = layout = self.resolve(layout, self.world, cfg)
@@ -67,7 +68,7 @@ class NodeLayout:
         if self.world == 1:
             return
         if layout == "frame":
-            self.frame_shard = FrameShard(overlap_chunks=overlap_chunks)
+            self.frame_shard = FrameShard(overlap_chunks=overlap_chunks, window=window)
             return
         # every rank creates every group, in the same order
         kw = {} if backend is None else {"backend": backend}
@@ -75,7 +76,7 @@ class NodeLayout:
                    for h in range(2)]
         pairs = [dist.new_group([j, self.frame_ranks + j], **kw) for j in range(self.frame_ranks)]
         if self.frame_ranks > 1:
-            self.frame_shard = FrameShard(fgroups[self.half], overlap_chunks=overlap_chunks)
+            self.frame_shard = FrameShard(fgroups[self.half], overlap_chunks=overlap_chunks, window=window)
         self.cfg_shard = CfgShard(pairs[self.frame_index])
 
     @staticmethod
@@ -95,6 +96,9 @@ class NodeLayout:
     def describe(self) -> str:
         if self.world == 1:
             return "single-GPU"
+        win = ""
+        if self.frame_shard is not None:
+            win = f" ({self.frame_shard.window}" + (f", overlap {self.frame_shard.chunks}" if self.frame_shard.chunks > 1 else "") + ")"
         if self.layout == "frame":
-            return f"frame-shard x{self.world}"
-        return f"cfg x2, frame-shard x{self.frame_ranks}"
+            return f"frame-shard x{self.world}{win}"
+        return f"cfg x2, frame-shard x{self.frame_ranks}{win}"

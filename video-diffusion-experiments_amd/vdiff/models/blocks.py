@@ -157,6 +157,26 @@ class BasicTransformerBlock(nn.Module):
         n = ops.layer_norm(h, *self._nrm(3))
         return self.ff.forward_rows(n, h)
 
+    def run_temporal_gathered(self, h, batch, frames_local, positions, dist):
+        """run_temporal on a frame-sharded rank's rows (b, f_loc, p) under the K/V all-gather
+        window (FrameShard(window="kv-gather")): q from the rank's own frames, K/V of every
+        frame all-gathered over the frame shards; the positional encoding indexed by the
+        global frame rank*f_loc + f."""
+        C = h.shape[1]
+        d = self.dim_head
+        pe = self.pos_embed._pe[dist.rank * frames_local:]
+        frames = frames_local * dist.world
+        for attn, i in ((self.attn1, 1), (self.attn2, 2)):
+            n = ops.layer_norm(h, *self._nrm(i), pe=pe, pe_div=positions, pe_period=frames_local)
+            q = ops.gemm(n, attn._wqkv[:C])
+            kv = dist.gather_kv_frames(ops.gemm(n, attn._wqkv[C:]), batch, frames_local, positions,
+                                       ops.block_transpose)
+            a = ops.temporal_attention_kv(q, kv[:, :C], kv[:, C:], batch, frames_local, frames, positions,
+                                          self.heads, d, scale=attn.attn_scale)
+            h = ops.gemm(a, attn._wo, bias=attn._bo, res=h)
+        n = ops.layer_norm(h, *self._nrm(3))
+        return self.ff.forward_rows(n, h)
+
     def forward(self, hidden_states, attention_mask=None, encoder_hidden_states=None,
                 encoder_attention_mask=None, timestep=None, cross_attention_kwargs=None,
                 class_labels=None, added_cond_kwargs=None):
@@ -235,7 +255,10 @@ class AnimateDiffTransformer3D(nn.Module):
         if dist is None:
             h = blk.run_temporal(h, B, Fl, hw)
         else:
-            h = dist.temporal_window(h, B, Fl, hw, ops.block_transpose, blk.run_temporal)
+            if dist.window == "kv-gather":
+                h = blk.run_temporal_gathered(h, B, Fl, hw, dist)
+            else:
+                h = dist.temporal_window(h, B, Fl, hw, ops.block_transpose, blk.run_temporal)
         out = ops.gemm(h, self.proj_out._w, bias=self.proj_out._b, res=x.t)
         return Act(out, x.n, x.h, x.w)
 

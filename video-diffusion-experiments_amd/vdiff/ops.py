@@ -269,6 +269,21 @@ def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, 
     return out
 
 
+def temporal_attention_kv(q, k, v, batch, qframes, kframes, positions, heads, d, scale=None, out=None):
+    """A rank's own `qframes` query frames (rows (b, qframes, p) of q) against `kframes` key
+    frames (rows (b, kframes, p) of k/v, e.g. all-gathered from every frame shard)."""
+    _dev(q, k, v, out)
+    if k.stride(0) != v.stride(0):
+        raise ValueError("k/v must share a row stride")
+    if out is None:
+        out = torch.empty(q.shape[0], heads * d, device=q.device, dtype=BF16)
+    scale = d ** -0.5 if scale is None else scale
+    check(lib().vd_temporal_attention_kv(_p(q), q.stride(0), _p(k), _p(v), k.stride(0), _p(out), out.stride(0),
+                                         batch, qframes, kframes, positions, heads, d, scale, _stream()),
+          "vd_temporal_attention_kv")
+    return out
+
+
 def softmax_rows(s, out=None):
     """fp32 scores [rows, cols] in log2 units -> bf16 probabilities (row softmax)."""
     _dev(s, out)
