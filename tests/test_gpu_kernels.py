@@ -281,6 +281,30 @@ def test_conv3x3_large(gemm_path, case):
     close_bf16(out, want)
 
 
+@pytest.mark.parametrize("co,out_f32,M", [(4, True, 32768), (4, False, 1000), (24, False, 32768), (32, True, 600)])
+def test_conv3x3_small_n(cuda, co, out_f32, M):
+    """conv_out-shaped convs (N <= 32: the 256 x 32 v2 tiles; M < 256 falls back to v1):
+    ragged M, N % 8 == 4, fp32 output (the UNet's eps), bias."""
+    n = 8 if M == 32768 else 1
+    h = w = 64 if M == 32768 else (32 if M == 1000 else 24)
+    if M == 1000:
+        n, h, w = 1, 25, 40
+    if M == 600:
+        n, h, w = 1, 20, 30
+    ci = 320
+    x0 = rnd(n * h * w, ci)
+    wt = bf(torch.randn(co, ci, 3, 3, device="cuda") * 0.02)
+    b = torch.randn(co, device="cuda")
+    out = torch.empty(n * h * w, co, device="cuda", dtype=torch.float32 if out_f32 else torch.bfloat16)
+    ops.conv3x3(x0, n, h, w, pack_conv3x3(wt), bias=b, out=out, out_f32=out_f32)
+    img = x0.double().reshape(n, h, w, -1).permute(0, 3, 1, 2)
+    want = F.conv2d(img, wt.double(), b.double(), padding=1).permute(0, 2, 3, 1).reshape(-1, co)
+    if out_f32:
+        close_f32(out, want, rtol=1e-3, atol=1e-4)
+    else:
+        close_bf16(out, want)
+
+
 def test_gemm_splitk_dense(cuda):
     """Few output tiles + long K (the 8x8 level): split-K slabs + reduce epilogue."""
     M, N, K = 2048, 1280, 2560

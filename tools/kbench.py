@@ -52,7 +52,8 @@ cases += [("big 4096^3", "dense", 4096, 4096, 4096, False), ("big 8192^3", "dens
           ("big M=32768 N=4096 K=1280", "dense", 32768, 4096, 1280, False)]
 convs = [("L1 conv 320->320", IMGS, 64, 320, 320), ("L2 conv 640->640", IMGS, 32, 640, 640),
          ("L3 conv 1280->1280", IMGS, 16, 1280, 1280), ("L4 conv 1280->1280", IMGS, 8, 1280, 1280),
-         ("L4 conv 2560->1280", IMGS, 8, 2560, 1280), ("L1 conv 640->320", IMGS, 64, 640, 320)]
+         ("L4 conv 2560->1280", IMGS, 8, 2560, 1280), ("L1 conv 640->320", IMGS, 64, 640, 320),
+         ("L1 conv_out 320->4", IMGS, 64, 320, 4)]
 
 for name, kind, M, N, K, res in cases:
     if flt not in name:

@@ -1707,7 +1707,7 @@ void read_num_cus() {  // once per process: the plan (and the workspace size) de
 Plan plan(const vd_gemm_desc& d) {
   read_num_cus();
   Plan p;
-  if (g_path == 1 || d.K % G4_BK || d.k0 % G4_BK || d.M < G6_BM || d.N < 64) return p;
+  if (g_path == 1 || d.K % G4_BK || d.k0 % G4_BK || d.M < G6_BM || (d.N < 64 && d.N > 32)) return p;
   const int64_t a_rows = d.a_mode == VD_A_CONV3X3
                              ? (int64_t)d.n_img / d.frames_out * d.frames_in * d.h_in * d.w_in : d.M;
   const int64_t a0b = a_rows * d.lda0 * 2, a1b = d.a1 ? a_rows * d.lda1 * 2 : 0, wb = d.N * d.ldw * 2;
@@ -1716,6 +1716,16 @@ Plan plan(const vd_gemm_desc& d) {
   const bool cin32 = d.a_mode != VD_A_CONV3X3 || (d.K / 9) % G4_BK == 0;
   const bool k64 = d.K % BK == 0 && d.k0 % BK == 0 &&
                    (d.a_mode != VD_A_CONV3X3 || (d.K / (d.ks * d.ks * d.kt)) % BK == 0);
+  // N <= 32 (conv_out, N = 4): 256 x 32 v2 tiles — v1's 128 x 64 tiles ran the full-size
+  // conv_out (M 131072, K 2880) in 177 us (profiles/r02b_step_breakdown_f16.txt)
+  if (d.N <= 32) {
+    if (!k64 || d.M < G2_BM || d.act == VD_ACT_GEGLU || (g_path != 0 && g_path != 2 && g_path != 11)) return p;
+    p.ver = 2;
+    p.bn = 32;
+    p.split = split_for((d.M + G2_BM - 1) / G2_BM, d.K / BK);
+    p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 : 0;
+    return p;
+  }
   // fewer rows than one 256-row tile (the deep levels of a 1-2 image rank): 64 x 64 tiles
   // (v1's 128-row tiles left L4's K = 11520 convs on 8 workgroups: 453 us vs ~30)
   if (d.M < G2_BM) {
@@ -1735,8 +1745,10 @@ Plan plan(const vd_gemm_desc& d) {
   }
   // v5 (256 x 320, BK 32): forced, where K or k0 is not a multiple of 64, and on the shape
   // it wins (tools/kbench.py: the L1 attention QKV projection M 131072 x N 960 x K 320)
-  const bool v5auto = d.a_mode == VD_A_DENSE && d.M >= 65536 && d.K <= 320 && d.N % 320 == 0 && d.N >= 640 &&
-                      d.N < 2560 && !d.res && !d.rowbias && d.act != VD_ACT_GEGLU;
+  // (round 2) and the L1 projections N = K = 320 with or without a residual: one 320-column
+  // tile covers the whole row (+res 75 vs 85 us on v2, profiles/r02_gemm_paths_vs_hipblaslt_miopen.txt)
+  const bool v5auto = d.a_mode == VD_A_DENSE && d.M >= 65536 && d.K <= 320 && !d.rowbias && d.act != VD_ACT_GEGLU &&
+                      ((d.N % 320 == 0 && d.N >= 640 && d.N < 2560 && !d.res) || d.N == 320);
   if (g_path == 5 || ((g_path == 0 || g_path == 7 || g_path == 11) && (!k64 || v5auto))) {
     if (!cin32) return p;
     p.ver = 5;
@@ -1878,7 +1890,8 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   if (p.ver == 5) return launch4<320, 4, 2, 4>(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 2)
     return p.bn == 160 ? launch2<160>(d, s, p.a0b, p.a1b, p.wb, p.split)
-                       : launch2<128>(d, s, p.a0b, p.a1b, p.wb, p.split);
+           : p.bn == 32 ? launch2<32>(d, s, p.a0b, p.a1b, p.wb, p.split)
+                        : launch2<128>(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (d.act == VD_ACT_GEGLU) return launch<128, 128>(d, s);
   // N tile: least padding, then fewer tiles.
   if (d.N <= 64) return launch<128, 64>(d, s);
