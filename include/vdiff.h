@@ -93,6 +93,16 @@ typedef struct vd_gemm_desc {
    * zero padding; a frame-sharded rank passes its halo'd frames with frames_in =
    * frames_out + 2, t_off = 1).  n_img counts OUTPUT images. */
   int32_t kt, ks, frames_in, frames_out, t_off;
+  /* Fused LayerNorm of the output rows (BasicTransformerBlock norm1/2/3 after the GEMM that
+   * produces the residual stream: proj_in, attn out-proj + residual): when ln_out != NULL,
+   * also ln_out[m] = (out[m] - mean) * rstd * ln_gamma + ln_beta
+   * (+ ln_pe[((m / ln_pe_div) % ln_pe_period) * N .. ], the motion block's sinusoidal PE),
+   * statistics over the N bf16-rounded outputs of row m (vd_layernorm's arithmetic).  Fused
+   * into the 256 x 320 GEMM's epilogue when N == 320 (one tile owns whole rows); otherwise
+   * vd_gemm runs vd_layernorm on the output after the GEMM.  bf16 outputs only. */
+  const float* ln_gamma; const float* ln_beta; float ln_eps;
+  const float* ln_pe; int64_t ln_pe_div; int64_t ln_pe_period;
+  void* ln_out; int64_t ld_ln;
 } vd_gemm_desc;
 
 int vd_gemm(const vd_gemm_desc* d, vd_stream_t stream);

@@ -305,6 +305,41 @@ def test_conv3x3_small_n(cuda, co, out_f32, M):
         close_bf16(out, want)
 
 
+@pytest.mark.parametrize("M,N,res,pe", [(32768 + 77, 320, True, False), (131072, 320, False, True),
+                                         (40000, 320, True, True), (3000, 320, True, True), (32768, 640, True, False)])
+def test_gemm_ln(cuda, M, N, res, pe):
+    """vd_gemm with ln_out: the LayerNorm fused into the 256 x 320 GEMM epilogue (N = 320,
+    >= 128 row tiles) or run after the GEMM (smaller M, other N): out equals the plain GEMM
+    and ln_out the LayerNorm of out (+ PE by frame) to bf16 rounding."""
+    from vdiff._lib import lib
+    K, frames, pos = 320, 16, 64
+    a = rnd(M, K)
+    w = rnd(N, K, std=K ** -0.5)
+    b = torch.randn(N, device=cuda) * 0.1
+    r = rnd(M, N) if res else None
+    g = 1 + 0.1 * torch.randn(N, device=cuda)
+    be = 0.1 * torch.randn(N, device=cuda)
+    pet = torch.randn(32, N, device=cuda) if pe else None
+    kw = dict(pe=pet, pe_div=pos, pe_period=frames) if pe else {}
+    out, ln = ops.gemm_ln(a, w, g, be, bias=b, res=r, **kw)
+    plain = ops.gemm(a, w, bias=b, res=r)
+    assert torch.equal(out, plain)
+    want = ops.layer_norm(plain, g, be, **kw)
+    close_bf16(ln, want)
+    x = plain.double()
+    ref = F.layer_norm(x, (N,), g.double(), be.double(), eps=1e-5)
+    if pe:
+        ref = ref + pet.double()[(torch.arange(M, device=cuda) // pos) % frames]
+    close_bf16(ln, ref)
+    lib().vd_gemm_select_path(2)  # unfused reference path: GEMM + vd_layernorm
+    try:
+        out2, ln2 = ops.gemm_ln(a, w, g, be, bias=b, res=r, **kw)
+    finally:
+        lib().vd_gemm_select_path(0)
+    assert torch.equal(ln2, want)
+    assert (ln.float() - ln2.float()).abs().max().item() <= 2 ** -6 * (ln2.float().abs().max().item() + 1)
+
+
 def test_gemm_splitk_dense(cuda):
     """Few output tiles + long K (the 8x8 level): split-K slabs + reduce epilogue."""
     M, N, K = 2048, 1280, 2560

@@ -1,6 +1,8 @@
 """A/B of a host-side policy on the full denoising step, in one process on one box (box-to-box
-variance is ~3 %): python tools/ab_step.py gn [frames]  — alternates the GroupNorm policy
-(two-launch image norms vs partial/finalize/apply everywhere) over captured-graph steps."""
+variance is ~3 %): python tools/ab_step.py MODE [frames] — alternates two captured-graph loops:
+  gn   GroupNorm policy (two-launch image norms vs partial/finalize/apply everywhere)
+  ln   LayerNorm fused into the residual GEMM's epilogue (ops.gemm_ln) vs GEMM + vd_layernorm
+  v3p  persistent v3 GEMM vs one unit per workgroup (vd_gemm_select_path 0 vs 11)"""
 import sys
 import time
 from pathlib import Path
@@ -19,20 +21,38 @@ lat = torch.randn((1, 4, frames, 64, 64), generator=torch.Generator().manual_see
 ehs = torch.randn((2, 77, 768), generator=torch.Generator().manual_seed(1)).cuda()
 sched = DDIMScheduler(beta_schedule="linear", steps_offset=1, clip_sample=False)
 sched.set_timesteps(50)
-orig = ops.group_norm
-
-
-def four_pass(*a, **k):
-    k["two_pass"] = False
-    return orig(*a, **k)
-
-
+mode = sys.argv[1] if len(sys.argv) > 1 else "gn"
 loops = {}
-for name, fn in (("two-launch", orig), ("four-launch", four_pass)):
-    ops.group_norm = fn
-    import vdiff.models.blocks as B  # noqa: E402  (modules hold `ops`, so patching ops is enough)
-    loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
-ops.group_norm = orig
+if mode == "gn":
+    orig = ops.group_norm
+
+    def four_pass(*a, **k):
+        k["two_pass"] = False
+        return orig(*a, **k)
+
+    for name, fn in (("two-launch", orig), ("four-launch", four_pass)):
+        ops.group_norm = fn  # modules hold `ops`, so patching ops is enough
+        loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
+    ops.group_norm = orig
+elif mode == "ln":
+    orig = ops.gemm_ln
+
+    def unfused(a, w, gamma, beta, *, eps=1e-5, pe=None, pe_div=1, pe_period=1, bias=None, res=None, **k):
+        out = ops.gemm(a, w, bias=bias, res=res)
+        return out, ops.layer_norm(out, gamma, beta, eps, pe=pe, pe_div=pe_div, pe_period=pe_period)
+
+    for name, fn in (("ln-fused", orig), ("ln-separate", unfused)):
+        ops.gemm_ln = fn
+        loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
+    ops.gemm_ln = orig
+elif mode == "v3p":
+    from vdiff._lib import lib
+    for name, path in (("v3-persistent", 0), ("v3-per-tile", 11)):
+        lib().vd_gemm_select_path(path)  # the plan is fixed at capture
+        loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
+    lib().vd_gemm_select_path(0)
+else:
+    sys.exit(f"unknown mode {mode}")
 res = {k: [] for k in loops}
 for rep in range(4):
     for name, lp in loops.items():

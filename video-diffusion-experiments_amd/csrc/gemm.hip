@@ -1010,7 +1010,135 @@ __device__ __forceinline__ int epi_fast(const vd_gemm_desc& d, f32x4 (&acc)[NB][
   return nst;
 }
 
-template <int BN, int WM, int WN, int STAGES, int MODE>
+// Epilogue with the next LayerNorm fused (vd_gemm_desc.ln_out; v5 with N == BN == 320, so
+// the workgroup's tile owns whole rows): x = bf16(acc + bias (+ res)) is stored as usual and
+// kept in registers; row sums of the rounded x (lane: 4 columns x NB blocks; then the 4 lanes
+// of a row by xor shuffles; then the WN = 2 column waves through `red` in LDS), mean, the
+// two-pass variance the same way, and ln_out = fmaf((x - mean) * rstd, gamma, beta) (+ pe)
+// — vd_layernorm's arithmetic on the same bf16 x (only the fp32 summation order differs).
+// Every wave of the workgroup runs it (two s_barriers).
+template <int MB, int NB>
+__device__ __forceinline__ void epi_ln(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], int mbase, int nbase, int lane,
+                                       int rloc, int wn, float* red) {
+  static_assert(NB % 2 == 0, "epi_ln: whole 16-column pairs");
+  const int M = (int)d.M, N = (int)d.N;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int wcol = 16 * (fq & 1) + 8 * (fq >> 1);  // lane's first column inside a swapped pair
+  bf16_t* out = (bf16_t*)d.out;
+  // x: v_permlane16_swap of blocks (a, a+1) leaves each lane 8 consecutive columns of its row
+  // (16-B residual loads and stores, as gemm_epilogue's wide path); the rounded x stays in acc
+  // in that swapped order (a row's statistics do not depend on it)
+#pragma unroll
+  for (int a = 0; a < NB; a += 2) {
+    const int n = nbase + a * 16 + wcol;
+    float bv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (d.bias) {
+      const float4 t0 = *(const float4*)(d.bias + n), t1 = *(const float4*)(d.bias + n + 4);
+      bv[0] = t0.x; bv[1] = t0.y; bv[2] = t0.z; bv[3] = t0.w;
+      bv[4] = t1.x; bv[5] = t1.y; bv[6] = t1.z; bv[7] = t1.w;
+    }
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      const int m = mbase + b * 16 + fr;
+      const bool mok = m < M;
+      const int mrow = mok ? m : 0;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[a][b][j]), __float_as_uint(acc[a + 1][b][j]),
+                                                  false, false);
+        o[j] = __uint_as_float(r[0]) + bv[j];
+        o[4 + j] = __uint_as_float(r[1]) + bv[4 + j];
+      }
+      if (d.res) {
+        float rf[8];
+        unpack8(*(const uint4*)((const bf16_t*)d.res + (uint32_t)(mrow * (int)d.ld_res + n)), rf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += rf[j];
+      }
+      const uint4 pk = pack8(o);
+      if (mok) *(uint4*)(out + (uint32_t)(mrow * (int)d.ldc + n)) = pk;
+      float x8[8];
+      unpack8(pk, x8);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[a][b][j] = x8[j];
+        acc[a + 1][b][j] = x8[4 + j];
+      }
+    }
+  }
+  float mean[MB], rstd[MB];
+#pragma unroll
+  for (int b = 0; b < MB; ++b) {
+    float sm = 0.f;
+#pragma unroll
+    for (int a = 0; a < NB; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sm += acc[a][b][j];
+    sm += __shfl_xor(sm, 16, 64);
+    sm += __shfl_xor(sm, 32, 64);
+    mean[b] = sm;
+    if (fq == 0) red[wn * 256 + rloc + b * 16 + fr] = sm;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int b = 0; b < MB; ++b) mean[b] = (mean[b] + red[(1 - wn) * 256 + rloc + b * 16 + fr]) / (float)N;
+#pragma unroll
+  for (int b = 0; b < MB; ++b) {
+    float s2 = 0.f;
+#pragma unroll
+    for (int a = 0; a < NB; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float t = acc[a][b][j] - mean[b];
+        s2 = fmaf(t, t, s2);
+      }
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    rstd[b] = s2;
+    if (fq == 0) red[512 + wn * 256 + rloc + b * 16 + fr] = s2;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int b = 0; b < MB; ++b)
+    rstd[b] = rsqrtf((rstd[b] + red[512 + (1 - wn) * 256 + rloc + b * 16 + fr]) / (float)N + d.ln_eps);
+  bf16_t* y = (bf16_t*)d.ln_out;
+  int perow[MB];  // element offset of row m's PE row (m clamped; unused without ln_pe)
+#pragma unroll
+  for (int b = 0; b < MB; ++b) {
+    const int m = mbase + b * 16 + fr;
+    perow[b] = d.ln_pe ? ((m < M ? m : 0) / (int)d.ln_pe_div) % (int)d.ln_pe_period * N : 0;
+  }
+#pragma unroll
+  for (int a = 0; a < NB; a += 2) {
+    const int n = nbase + a * 16 + wcol;
+    const float4 g0 = *(const float4*)(d.ln_gamma + n), g1 = *(const float4*)(d.ln_gamma + n + 4);
+    const float4 b0 = *(const float4*)(d.ln_beta + n), b1 = *(const float4*)(d.ln_beta + n + 4);
+    const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      const int m = mbase + b * 16 + fr;
+      if (m >= M) continue;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = fmaf((acc[a][b][j] - mean[b]) * rstd[b], gg[j], bb[j]);
+        o[4 + j] = fmaf((acc[a + 1][b][j] - mean[b]) * rstd[b], gg[4 + j], bb[4 + j]);
+      }
+      if (d.ln_pe) {
+        const float4 t0 = *(const float4*)(d.ln_pe + perow[b] + n), t1 = *(const float4*)(d.ln_pe + perow[b] + n + 4);
+        o[0] += t0.x; o[1] += t0.y; o[2] += t0.z; o[3] += t0.w;
+        o[4] += t1.x; o[5] += t1.y; o[6] += t1.z; o[7] += t1.w;
+      }
+      *(uint4*)(y + (uint32_t)(m * (int)d.ld_ln + n)) = pack8(o);
+    }
+  }
+}
+
+template <int BN, int WM, int WN, int STAGES, int MODE, bool LN = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_waves_per_eu(2))) void gemm4_kernel(
     const vd_gemm_desc d, uint32_t a0_bytes, uint32_t a1_bytes, uint32_t w_bytes, int split) {
   using C = G4<BN, WM, WN, STAGES>;
@@ -1040,7 +1168,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
   const int hgrid = d.upsample ? 2 * d.h_in : d.h_in;
   const int wgrid = d.upsample ? 2 * d.w_in : d.w_in;
   // load-free epilogue (epi_fast) for plain bf16 outputs
-  const bool fast = split == 1 && !d.res && !d.rowbias && !d.out_f32 && (N % 8) == 0 &&
+  const bool fast = !LN && split == 1 && !d.res && !d.rowbias && !d.out_f32 && (N % 8) == 0 &&
                     (d.ldc % 8) == 0 && (((uintptr_t)d.out) & 15) == 0;
   const __amdgpu_buffer_rsrc_t rbias = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(d.bias ? d.bias : (const float*)d.a0), 0, d.bias ? (uint32_t)(N * 4) : 0u, 0x00020000);
@@ -1232,15 +1360,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
       const int tile = cu / split, sp = cu % split;
       const int64_t m0 = (int64_t)(tile / tiles_n) * G4_BM, n0 = (int64_t)(tile % tiles_n) * BN;
       bool done = false;
-      {
-        if (fast) {
-          const float* bsl = (const float*)(smem + STAGES * C::STAGE + (cun & (C::BIAS_SLOTS - 1)) * 2048);
-          st1 = epi_fast<C::MB, C::NB>(d, acc, (int)m0 + wm * C::WROWS, (int)n0 + wn * C::WCOLS, lane, bsl,
-                                       (int)n0, rout);
-          done = true;
-        }
+      if constexpr (LN) {  // plan: N == BN, split == 1; the bias slots (unused without `fast`) hold `red`
+        static_assert(WN == 2 && C::BIAS_SLOTS * 2048 >= 4096, "epi_ln: two column waves, 4 KiB of LDS");
+        epi_ln<C::MB, C::NB>(d, acc, (int)m0 + wm * C::WROWS, (int)n0 + wn * C::WCOLS, lane, wm * C::WROWS, wn,
+                             (float*)(smem + STAGES * C::STAGE));
+        done = true;
+      } else if (fast) {
+        const float* bsl = (const float*)(smem + STAGES * C::STAGE + (cun & (C::BIAS_SLOTS - 1)) * 2048);
+        st1 = epi_fast<C::MB, C::NB>(d, acc, (int)m0 + wm * C::WROWS, (int)n0 + wn * C::WCOLS, lane, bsl,
+                                     (int)n0, rout);
+        done = true;
       }
-      if (!done) {
+      if (!LN && !done) {
         if (split == 1) {
           gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::WROWS, (int)n0 + wn * C::WCOLS, lane);
         } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
@@ -1611,6 +1742,9 @@ int launch4(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   if (d.a_mode == VD_A_CONV3X3)
     hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_CONV3X3>), dim3((unsigned)grid), dim3(C::NT), 0,
                        s, d, a0b, a1b, wb, split);
+  else if (d.ln_out)  // plan() only lets a fusable descriptor keep ln_out
+    hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_DENSE, true>), dim3((unsigned)grid), dim3(C::NT), 0,
+                       s, d, a0b, a1b, wb, split);
   else
     hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_DENSE>), dim3((unsigned)grid), dim3(C::NT), 0, s,
                        d, a0b, a1b, wb, split);
@@ -1673,6 +1807,7 @@ struct Plan {
   int ver = 1;
   int bn = 128, split = 1;
   bool persist = true;  // v3: persistent flat K-tile stream
+  bool ln_fused = false;  // v5 writes ln_out in its epilogue
   uint32_t a0b = 0, a1b = 0, wb = 0;
   int64_t ws_bytes = 0;
 };
@@ -1716,6 +1851,20 @@ Plan plan(const vd_gemm_desc& d) {
   const bool cin32 = d.a_mode != VD_A_CONV3X3 || (d.K / 9) % G4_BK == 0;
   const bool k64 = d.K % BK == 0 && d.k0 % BK == 0 &&
                    (d.a_mode != VD_A_CONV3X3 || (d.K / (d.ks * d.ks * d.kt)) % BK == 0);
+  // fused LayerNorm epilogue: one 256 x 320 tile owns whole rows (v5, unsplit; >= 128 tiles so
+  // the unsplit grid fills half the chip — smaller M runs the GEMM + vd_layernorm instead)
+  if (d.ln_out) {
+    p.ln_fused = d.a_mode == VD_A_DENSE && d.N == 320 && d.K % G4_BK == 0 && d.k0 == d.K && !d.a1 &&
+                 d.ldc % 8 == 0 && d.ld_ln % 8 == 0 && ((uintptr_t)d.out & 15) == 0 && ((uintptr_t)d.ln_out & 15) == 0 &&
+                 (!d.res || (d.ld_res % 8 == 0 && ((uintptr_t)d.res & 15) == 0)) &&
+                 (d.M + G4_BM - 1) / G4_BM >= 128 && !d.rowbias && d.act == VD_ACT_NONE && !d.out_f32 &&
+                 (g_path == 0 || g_path == 5 || g_path == 11);
+    if (p.ln_fused) {
+      p.ver = 5;
+      p.bn = 320;
+      return p;
+    }
+  }
   // N <= 32 (conv_out, N = 4): 256 x 32 v2 tiles — v1's 128 x 64 tiles ran the full-size
   // conv_out (M 131072, K 2880) in 177 us (profiles/r02b_step_breakdown_f16.txt)
   if (d.N <= 32) {
@@ -1883,8 +2032,21 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
     if (d.k0 < d.K) VD_CHECK_ARG(d.a1 != nullptr);
   }
   if (d.act == VD_ACT_GEGLU) VD_CHECK_ARG(d.N % 32 == 0 && !d.res && !d.rowbias && !d.out_f32);
+  if (d.ln_out) {
+    VD_CHECK_ARG(!d.out_f32 && d.act != VD_ACT_GEGLU && d.ln_gamma && d.ln_beta && al16(d.ln_gamma) &&
+                 al16(d.ln_beta) && d.ld_ln % 4 == 0 && al8(d.ln_out) && d.N % 4 == 0);
+    if (d.ln_pe) VD_CHECK_ARG(al16(d.ln_pe) && d.ln_pe_div > 0 && d.ln_pe_period > 0);
+  }
   const Plan p = plan(d);
   if (p.ver >= 2 && p.split > 1) VD_CHECK_ARG(d.ws && al16(d.ws) && d.ws_bytes >= p.ws_bytes);
+  if (d.ln_out && !p.ln_fused) {  // the GEMM, then vd_layernorm over its output
+    vd_gemm_desc g = d;
+    g.ln_out = nullptr;
+    const int rc = vd_gemm(&g, stream);
+    if (rc != VD_OK) return rc;
+    return vd_layernorm(d.out, d.ldc, d.M, d.N, d.ln_gamma, d.ln_beta, d.ln_eps, d.ln_pe, d.ln_pe_div,
+                        d.ln_pe_period, d.ln_out, d.ld_ln, stream);
+  }
   if (p.ver == 3) return launch3(d, s, p.a0b, p.a1b, p.wb, p.split, p.persist);
   if (p.ver == 6) return launch6(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 5) return launch4<320, 4, 2, 4>(d, s, p.a0b, p.a1b, p.wb, p.split);

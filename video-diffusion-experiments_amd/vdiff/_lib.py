@@ -87,6 +87,9 @@ class GemmDesc(C.Structure):
         ("out", c_vp), ("ldc", c_i64), ("out_f32", c_i32),
         ("ws", c_vp), ("ws_bytes", c_i64),
         ("kt", c_i32), ("ks", c_i32), ("frames_in", c_i32), ("frames_out", c_i32), ("t_off", c_i32),
+        ("ln_gamma", c_vp), ("ln_beta", c_vp), ("ln_eps", c_f32),
+        ("ln_pe", c_vp), ("ln_pe_div", c_i64), ("ln_pe_period", c_i64),
+        ("ln_out", c_vp), ("ld_ln", c_i64),
     ]
 
 

@@ -122,15 +122,17 @@ class BasicTransformerBlock(nn.Module):
         return m._g, m._b
 
     # spatial: tokens are (image, pixel) rows
-    def run_spatial(self, h, n_img, hw, ctx: Ctx):
+    # run_*: `n` = norm1(h) when the caller's GEMM already produced it (ops.gemm_ln: the
+    # LayerNorm fused into the epilogue of the GEMM writing h, or run right after it)
+    def run_spatial(self, h, n_img, hw, ctx: Ctx, n=None):
         C = h.shape[1]
         d = self.dim_head
-        n = ops.layer_norm(h, *self._nrm(1))
+        if n is None:
+            n = ops.layer_norm(h, *self._nrm(1))
         qkv = ops.gemm(n, self.attn1._wqkv)
         a = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], n_img, self.heads, hw, hw, d,
                           scale=self.attn1.attn_scale)
-        h = ops.gemm(a, self.attn1._wo, bias=self.attn1._bo, res=h)
-        n = ops.layer_norm(h, *self._nrm(2))
+        h, n = ops.gemm_ln(a, self.attn1._wo, *self._nrm(2), bias=self.attn1._bo, res=h)
         q = ops.gemm(n, self.attn2._wq)
         kv = None if ctx.kv_cache is None else ctx.kv_cache.get(id(self.attn2))
         if kv is None:
@@ -139,22 +141,23 @@ class BasicTransformerBlock(nn.Module):
                 ctx.kv_cache[id(self.attn2)] = kv
         a = ops.attention(q, kv[:, :C], kv[:, C:], n_img, self.heads, hw, ctx.ctx_len, d,
                           kv_div=ctx.frames, scale=self.attn2.attn_scale)
-        h = ops.gemm(a, self.attn2._wo, bias=self.attn2._bo, res=h)
-        n = ops.layer_norm(h, *self._nrm(3))
+        h, n = ops.gemm_ln(a, self.attn2._wo, *self._nrm(3), bias=self.attn2._bo, res=h)
         return self.ff.forward_rows(n, h)
 
     # temporal: tokens are (video, frame, position) rows; attention over frames
-    def run_temporal(self, h, batch, frames, positions):
+    def run_temporal(self, h, batch, frames, positions, n=None):
         C = h.shape[1]
         d = self.dim_head
         pe = self.pos_embed._pe
+        if n is None:
+            n = ops.layer_norm(h, *self._nrm(1), pe=pe, pe_div=positions, pe_period=frames)
         for attn, i in ((self.attn1, 1), (self.attn2, 2)):
-            n = ops.layer_norm(h, *self._nrm(i), pe=pe, pe_div=positions, pe_period=frames)
             qkv = ops.gemm(n, attn._wqkv)
             a = ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch, frames,
                                        positions, self.heads, d, scale=attn.attn_scale)
-            h = ops.gemm(a, attn._wo, bias=attn._bo, res=h)
-        n = ops.layer_norm(h, *self._nrm(3))
+            # norm2 (+ PE) after attn1, norm3 after attn2
+            h, n = ops.gemm_ln(a, attn._wo, *self._nrm(i + 1), bias=attn._bo, res=h,
+                               pe=pe if i == 1 else None, pe_div=positions, pe_period=frames)
         return self.ff.forward_rows(n, h)
 
     def run_temporal_gathered(self, h, batch, frames_local, positions, dist):
@@ -166,15 +169,15 @@ class BasicTransformerBlock(nn.Module):
         d = self.dim_head
         pe = self.pos_embed._pe[dist.rank * frames_local:]
         frames = frames_local * dist.world
+        n = ops.layer_norm(h, *self._nrm(1), pe=pe, pe_div=positions, pe_period=frames_local)
         for attn, i in ((self.attn1, 1), (self.attn2, 2)):
-            n = ops.layer_norm(h, *self._nrm(i), pe=pe, pe_div=positions, pe_period=frames_local)
             q = ops.gemm(n, attn._wqkv[:C])
             kv = dist.gather_kv_frames(ops.gemm(n, attn._wqkv[C:]), batch, frames_local, positions,
                                        ops.block_transpose)
             a = ops.temporal_attention_kv(q, kv[:, :C], kv[:, C:], batch, frames_local, frames, positions,
                                           self.heads, d, scale=attn.attn_scale)
-            h = ops.gemm(a, attn._wo, bias=attn._bo, res=h)
-        n = ops.layer_norm(h, *self._nrm(3))
+            h, n = ops.gemm_ln(a, attn._wo, *self._nrm(i + 1), bias=attn._bo, res=h,
+                               pe=pe if i == 1 else None, pe_div=positions, pe_period=frames_local)
         return self.ff.forward_rows(n, h)
 
     def forward(self, hidden_states, attention_mask=None, encoder_hidden_states=None,
@@ -209,8 +212,9 @@ class Transformer2DModel(nn.Module):
     def run(self, x: Act, ctx: Ctx) -> Act:
         hw = x.h * x.w
         hn = ops.group_norm(x.t, x.n, hw, self.groups, 1e-6, self.norm._g, self.norm._b)
-        h = ops.gemm(hn, self.proj_in._w, bias=self.proj_in._b)
-        h = self.transformer_blocks[0].run_spatial(h, x.n, hw, ctx)
+        blk = self.transformer_blocks[0]
+        h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b)
+        h = blk.run_spatial(h, x.n, hw, ctx, n=n)
         out = ops.gemm(h, self.proj_out._w, bias=self.proj_out._b, res=x.t)
         return Act(out, x.n, x.h, x.w)
 
@@ -250,11 +254,13 @@ class AnimateDiffTransformer3D(nn.Module):
         gather = dist.gather_gn_partials if dist is not None else None
         hn = ops.group_norm(x.t, B, Fl * hw, self.groups, 1e-6, self.norm._g, self.norm._b, gather=gather,
                             two_pass=False)
-        h = ops.gemm(hn, self.proj_in._w, bias=self.proj_in._b)
         blk = self.transformer_blocks[0]
-        if dist is None:
-            h = blk.run_temporal(h, B, Fl, hw)
+        if dist is None:  # norm1 (+ PE by frame) fused into proj_in's epilogue
+            h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b, pe=blk.pos_embed._pe,
+                               pe_div=hw, pe_period=Fl)
+            h = blk.run_temporal(h, B, Fl, hw, n=n)
         else:
+            h = ops.gemm(hn, self.proj_in._w, bias=self.proj_in._b)
             if dist.window == "kv-gather":
                 h = blk.run_temporal_gathered(h, B, Fl, hw, dist)
             else:

@@ -80,6 +80,30 @@ def gemm(a, w, *, a1=None, bias=None, rowbias=None, rb_div=1, res=None, act=ACT_
     return out
 
 
+def gemm_ln(a, w, gamma, beta, *, eps=1e-5, pe=None, pe_div=1, pe_period=1, bias=None, res=None, out=None,
+            ln_out=None):
+    """(out, ln_out): out = a @ w^T (+ bias) (+ res) in bf16 and ln_out = LayerNorm(out)
+    (+ pe[(m / pe_div) % pe_period]) — the GEMM producing a transformer block's residual
+    stream with the next norm fused into its epilogue where one tile owns whole rows."""
+    _dev(a, w, gamma, beta, pe, bias, res, out, ln_out)
+    M = a.shape[0]
+    N, K = w.shape
+    if a.shape[1] != K:
+        raise ValueError(f"A has {a.shape[1]} columns, W has K={K}")
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=BF16)
+    if ln_out is None:
+        ln_out = torch.empty(M, N, device=a.device, dtype=BF16)
+    d = GemmDesc(a0=_p(a), lda0=_rows(a), k0=K, a1=None, lda1=0, a_mode=A_DENSE,
+                 w=_p(w), ldw=_rows(w), M=M, N=N, K=K, bias=_p(bias), rowbias=None, ld_rb=0, rb_div=1,
+                 res=_p(res), ld_res=_rows(res) if res is not None else 0, act=ACT_NONE,
+                 out=_p(out), ldc=_rows(out), out_f32=0,
+                 ln_gamma=_p(gamma), ln_beta=_p(beta), ln_eps=eps, ln_pe=_p(pe), ln_pe_div=pe_div,
+                 ln_pe_period=pe_period, ln_out=_p(ln_out), ld_ln=_rows(ln_out))
+    _run_gemm(d, a.device, "vd_gemm(ln)")
+    return out, ln_out
+
+
 def conv3x3(x, n_img, h_in, w_in, w, *, x1=None, stride=1, upsample=False, bias=None,
             rowbias=None, rb_div=1, res=None, act=ACT_NONE, out=None, out_f32=False):
     """3x3 pad-1 conv over NHWC rows x (+ channel-concat x1); w packed [Cout][3][3][Cin]."""
