@@ -97,11 +97,14 @@ for name, n, hw, ci, co in convs:
     lib().vd_gemm_select_path(0)
 
 for name, n_img, S, d, skv in [("attn L1 self", 32, 4096, 40, 4096), ("attn L2 self", 32, 1024, 80, 1024),
-                               ("attn L3 self", 32, 256, 160, 256), ("attn L1 cross", 32, 4096, 40, 77)]:
+                               ("attn L3 self", 32, 256, 160, 256), ("attn L1 cross", 32, 4096, 40, 77),
+                               ("attn L1 model", 32, 4096, 40, 4096)]:
     if flt not in name:
         continue
     C = 8 * d
     qkv = rnd(n_img * S, 3 * C, std=1.5)
+    if "model" in name:  # bench.py's roofline inputs: softmax scale d^-1/2 log2 e folded into q
+        qkv[:, :C] = (qkv[:, :C].float() * (d ** -0.5 * math.log2(math.e))).to(torch.bfloat16)
     kv = rnd(2 * skv, 2 * C, std=1.5)
     out = torch.empty(n_img * S, C, device=dev, dtype=torch.bfloat16)
     if skv == S:
