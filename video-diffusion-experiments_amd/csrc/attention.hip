@@ -1405,35 +1405,70 @@ __global__ __launch_bounds__(NT) void temporal_mfma_kernel(
   // head slices share 128-byte lines of the Q/K/V/O rows) get adjacent logical ids, which
   // xcd_remap keeps on one XCD, so a shared line is fetched into one L2, not two
   const int64_t lblk = xcd_remap(blockIdx.x, gridDim.x);
-  for (int64_t item = lblk * 4 + wave; item < nitems; item += stride) {
+  // Software-pipelined (round 2): the K/Q fragments and V chunks of the wave's NEXT item are
+  // loaded into registers while the current item computes, so a wave keeps one item of loads
+  // in flight behind its MFMAs, softmax and stores (the kernel is memory-latency bound: 3.3
+  // TB/s at L1 with one item's loads outstanding at a time).
+  constexpr int VN = (16 * C::DCH + 63) / 64;  // V chunks per lane (frames <= 16)
+  const bool fok = fr < frames, qok = fr < qframes;
+  uint4 kn[C::KSTEPS], qn[C::KSTEPS], vn[VN];
+  // (a macro, not a lambda: a lambda capturing the register arrays by reference left them on
+  // the scratch stack)
+#define TM_LOAD_ITEM(IT)                                                                              \
+  {                                                                                                   \
+    const int h_ = (int)((IT) % heads);                                                              \
+    const int64_t bp_ = (IT) / heads;                                                                 \
+    const int64_t p_ = bp_ % positions, b_ = bp_ / positions;                                         \
+    const int64_t row0_ = b_ * frames * positions + p_;                                               \
+    const int64_t rf_ = (row0_ + (fok ? fr : 0) * positions) * ldkv + (int64_t)h_ * D;                \
+    const int64_t rq_ = ((b_ * qframes * positions + p_) + (qok ? fr : 0) * positions) * ldq + (int64_t)h_ * D; \
+    _Pragma("unroll") for (int ks = 0; ks < C::KSTEPS; ++ks) {                                        \
+      const int dd = ks * 32 + 8 * fq;                                                                \
+      kn[ks] = make_uint4(0, 0, 0, 0);                                                                \
+      qn[ks] = make_uint4(0, 0, 0, 0);                                                                \
+      if (dd < D) {                                                                                   \
+        if (fok) kn[ks] = *(const uint4*)(k + rf_ + dd);                                              \
+        if (qok) qn[ks] = *(const uint4*)(q + rq_ + dd);                                              \
+      }                                                                                               \
+    }                                                                                                 \
+    _Pragma("unroll") for (int r = 0; r < VN; ++r) {                                                  \
+      const int idx = lane + 64 * r;                                                                  \
+      const int f = idx / C::DCH, cc = idx - f * C::DCH;                                              \
+      vn[r] = make_uint4(0, 0, 0, 0);                                                                 \
+      if (idx < frames * C::DCH)                                                                      \
+        vn[r] = *(const uint4*)(v + (row0_ + (int64_t)f * positions) * ldkv + (int64_t)h_ * D + cc * 8); \
+    }                                                                                                 \
+  }
+  int64_t item = lblk * 4 + wave;
+  if (item < nitems) TM_LOAD_ITEM(item)
+  for (; item < nitems; item += stride) {
+    uint4 kc[C::KSTEPS], qc[C::KSTEPS], vc[VN];
+#pragma unroll
+    for (int ks = 0; ks < C::KSTEPS; ++ks) {
+      kc[ks] = kn[ks];
+      qc[ks] = qn[ks];
+    }
+#pragma unroll
+    for (int r = 0; r < VN; ++r) vc[r] = vn[r];
     const int h = (int)(item % heads);
     const int64_t bp = item / heads;
     const int64_t p = bp % positions, b = bp / positions;
-    const int64_t row0 = b * frames * positions + p;   // key row of frame 0; frame f at + f * positions
     const int64_t qrow0 = b * qframes * positions + p;  // query / output row of frame 0
-    const bool fok = fr < frames, qok = fr < qframes;
-    const int64_t rf = (row0 + (fok ? fr : 0) * positions) * ldkv + (int64_t)h * D;
-    const int64_t rq = (qrow0 + (qok ? fr : 0) * positions) * ldq + (int64_t)h * D;
-    // ---- V rows -> LDS (d < D only)
+    if (item + stride < nitems) TM_LOAD_ITEM(item + stride)
+    // ---- V chunks -> LDS image (d < D only)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous item's tr reads done
-    for (int idx = lane; idx < frames * C::DCH; idx += 64) {
+#pragma unroll
+    for (int r = 0; r < VN; ++r) {
+      const int idx = lane + 64 * r;
       const int f = idx / C::DCH, cc = idx - f * C::DCH;
-      *(uint4*)(vl + f * C::VS + cc * 8) =
-          *(const uint4*)(v + (row0 + (int64_t)f * positions) * ldkv + (int64_t)h * D + cc * 8);
+      if (idx < frames * C::DCH) *(uint4*)(vl + f * C::VS + cc * 8) = vc[r];
     }
     // ---- S^T = K . Q^T
     f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < C::KSTEPS; ++ks) {
-      const int dd = ks * 32 + 8 * fq;
-      uint4 kq = make_uint4(0, 0, 0, 0), qq = make_uint4(0, 0, 0, 0);
-      if (dd < D) {
-        if (fok) kq = *(const uint4*)(k + rf + dd);
-        if (qok) qq = *(const uint4*)(q + rq + dd);
-      }
-      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kq), __builtin_bit_cast(bf16x8, qq), s,
-                                                  0, 0, 0);
-    }
+    for (int ks = 0; ks < C::KSTEPS; ++ks)
+      s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kc[ks]), __builtin_bit_cast(bf16x8, qc[ks]),
+                                                  s, 0, 0, 0);
     // ---- softmax over keys 4*fq + j of query fr (log2 units)
     float mx = -INFINITY;
 #pragma unroll
@@ -1450,7 +1485,7 @@ __global__ __launch_bounds__(NT) void temporal_mfma_kernel(
       pf[j] = (__bf16)__builtin_amdgcn_exp2f(s[j] - mx);
       pf[4 + j] = (__bf16)0.0f;
     }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // V image written
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // V image written (the prefetch stays in flight)
     __builtin_amdgcn_wave_barrier();
     // ---- O^T = V^T . P^T, one 16-row block of d at a time
     f32x4 ot[C::DB];
@@ -1474,6 +1509,7 @@ __global__ __launch_bounds__(NT) void temporal_mfma_kernel(
       }
     }
   }
+#undef TM_LOAD_ITEM
 }
 
 // 17..32 frames (the DiT's 32-frame temporal blocks): the 16-frame kernel's scheme on two
