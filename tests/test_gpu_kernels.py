@@ -563,13 +563,18 @@ def sdpa_ref(q, k, v, batch, heads, sq, skv, d, kv_div=1, scale=None):
     return (w @ vb).transpose(1, 2).reshape(batch * sq, heads * d)
 
 
-@pytest.fixture(params=["flash32", "v1"])
+@pytest.fixture(params=["flash32", "v1", "flash32-qb1"])
 def attn_path(request, cuda):
-    """d = 40 runs on the 32x32x16 kernel by default; "v1" forces the 16x16x32 one."""
+    """d = 40 runs on the 32x32x16 kernel by default; "v1" forces the 16x16x32 one;
+    "flash32-qb1" the 32x32x16 kernel with one 32-query block per wave (3 waves per SIMD)."""
     from vdiff._lib import lib
-    lib().vd_attention_force_v1(int(request.param == "v1"))
+    if request.param == "flash32-qb1":
+        lib().vd_attention_select(6)
+    else:
+        lib().vd_attention_force_v1(int(request.param == "v1"))
     yield request.param
     lib().vd_attention_force_v1(0)
+    lib().vd_attention_select(0)
 
 
 @pytest.mark.parametrize("d", [32, 40, 64, 80, 128, 160])

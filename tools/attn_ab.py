@@ -15,7 +15,7 @@ import torch  # noqa: E402
 from vdiff import ops  # noqa: E402
 from vdiff._lib import lib  # noqa: E402
 
-rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+rounds = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 5
 n_img, S, heads, d = 32, 4096, 8, 40
 C = heads * d
 g = torch.Generator(device="cuda").manual_seed(7)
@@ -23,15 +23,18 @@ qkv = (torch.randn(n_img * S, 3 * C, device="cuda", generator=g) * 1.5).to(torch
 q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
 scale = 1.0 / math.log2(math.e)
 flop = 4.0 * S * S * d * heads * n_img
-outs, res = {}, {1: [], 2: [], 3: [], 4: [], 5: []}
+SELS = (1, 2, 3, 4, 5, 6)
+outs, res = {}, {sel: [] for sel in SELS}
 names = {1: "flash_attn 16x16x32", 2: "flash32 (4 waves)", 3: "flash32pp (pipelined stagger)",
-         4: "flash32 interleaved", 5: "flash32, 1 WG per CU"}
-for sel in (1, 2, 3, 4, 5):
+         4: "flash32 interleaved", 5: "flash32, 1 WG per CU", 6: "flash32, 1 q-block/wave (3/SIMD)"}
+if "--model-scale" in sys.argv:  # bench.py's roofline inputs: softmax scale folded into q
+    qkv[:, :C] = (qkv[:, :C].float() * (d ** -0.5 * math.log2(math.e))).to(torch.bfloat16)
+for sel in SELS:
     lib().vd_attention_select(sel)
     outs[sel] = ops.attention(q, k, v, n_img, heads, S, S, d, scale=scale)
 torch.cuda.synchronize()
 for _ in range(rounds):
-    for sel in (1, 2, 3, 4, 5):
+    for sel in SELS:
         lib().vd_attention_select(sel)
         out = torch.empty_like(outs[sel])
         for _ in range(2):
@@ -44,7 +47,7 @@ for _ in range(rounds):
         e1.synchronize()
         res[sel].append(e0.elapsed_time(e1) / 10)
 lib().vd_attention_select(0)
-for sel in (1, 2, 3, 4, 5):
+for sel in SELS:
     ms = sorted(res[sel])
     print(f"{names[sel]:30s} median {ms[len(ms) // 2] * 1e3:7.1f} us  min {ms[0] * 1e3:7.1f} us  "
           f"{flop / ms[len(ms) // 2] / 1e9:7.1f} TF/s  ({flop / ms[len(ms) // 2] / 1e9 / 2500:.3f} of peak)")
@@ -55,5 +58,6 @@ for sel in (2, 4):
     print(f"select {sel}: rel-L2 vs fp32 softmax attention (2 images) {e.item():.3e}")
 print("interleaved vs flash32: max|diff| =", (outs[4].float() - outs[2].float()).abs().max().item(),
       " mean|diff| =", (outs[4].float() - outs[2].float()).abs().mean().item())
+print("flash32 qb1 == flash32 bitwise:", torch.equal(outs[2], outs[6]))
 print("flash32pp == flash32 bitwise:", torch.equal(outs[2], outs[3]),
       " max|pp - 16x16| =", (outs[3].float() - outs[1].float()).abs().max().item())

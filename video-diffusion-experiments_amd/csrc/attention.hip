@@ -399,16 +399,15 @@ __device__ __forceinline__ float partner32(float x) {
 // >= the running max (l >= 2^(max - mu)), so nothing underflows that matters;
 // a row sum >= 2^100 (or non-finite) means a score jumped past the fp32/bf16
 // range and the pass reports `bad` so the block reruns EXACT.
-template <int D, bool UNITC, bool EXACT, bool IL = false>
+template <int D, bool UNITC, bool EXACT, bool IL = false, int QB = 2>
 __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, const bf16_t* vb_ptr, int ldk32,
                                          int ldv32, int64_t skv, const int (&krow)[F32Cfg<D>::LREG],
                                          const uint32_t (&kcol)[F32Cfg<D>::LREG],
                                          const uint32_t (&ldsk)[F32Cfg<D>::LREG],
                                          const uint32_t (&ldsv)[F32Cfg<D>::LREG],
-                                         bf16x8 (&qf)[2][F32Cfg<D>::KSTEPS], f32x16 (&oacc)[F32Cfg<D>::NDB][2],
+                                         bf16x8 (&qf)[QB][F32Cfg<D>::KSTEPS], f32x16 (&oacc)[F32Cfg<D>::NDB][QB],
                                          int r32, int hh, int vtr, float c) {
   using C = F32Cfg<D>;
-  constexpr int QB = 2;
   constexpr float RESCALE = 4294967296.0f;        // 2^32
   constexpr float BAD = 1.2676506002282294e30f;   // 2^100
 #pragma unroll
@@ -751,13 +750,14 @@ __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, cons
   return bad;
 }
 
-template <int D, bool UNITC, bool IL = false>
-__global__ __launch_bounds__(NT, 2) void flash32_kernel(
+// QB = 32-query blocks per wave: 2 (default: 256 VGPRs, two waves per SIMD) or 1 (half the
+// registers, three waves per SIMD — round 2's occupancy variant, vd_attention_select(6)).
+template <int D, bool UNITC, bool IL = false, int QB = 2>
+__global__ __launch_bounds__(NT, QB == 1 ? 3 : 2) void flash32_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
     int64_t sq, int64_t skv, int64_t kv_div, float c, int out_f32 = 0) {
   using C = F32Cfg<D>;
-  constexpr int QB = 2;  // 32-query blocks per wave
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * C::STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -822,13 +822,13 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
   // V^T tr-read lane offset inside a [32 d] image row block (elements)
   const int vtr = ((4 * hh + (i16 >> 2)) * 32) + 16 * (g16 & 1) + 4 * (i16 & 3);
   f32x16 oacc[C::NDB][QB];
-  const bool bad = f32_loop<D, UNITC, false, IL>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv,
+  const bool bad = f32_loop<D, UNITC, false, IL, QB>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv,
                                                  qf, oacc, r32, hh, vtr, c);
   if (__syncthreads_or(bad)) {  // a score jumped > ~100 (log2) past mu somewhere: exact pass
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb)
       if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)0.0f;
-    f32_loop<D, UNITC, true>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv, qf, oacc, r32, hh,
+    f32_loop<D, UNITC, true, false, QB>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv, qf, oacc, r32, hh,
                              vtr, c);
   }
 
@@ -1235,6 +1235,18 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
       else
         hipLaunchKernelGGL((flash32pp_kernel<D, false>), grid, dim3(2 * NT), 0, s, (const bf16_t*)q, ldq,
                            (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
+      return vd_launch_status();
+    }
+    if (g_flash32 == 5 && ((uintptr_t)o & 15) == 0 && ldo % (out_f32 ? 4 : 8) == 0) {  // QB = 1, 4 waves/SIMD
+      const int64_t nblk = (sq + 127) / 128 * heads * batch;
+      if (nblk > 0x7fffffff) return VD_EINVAL;
+      const dim3 grid((unsigned)nblk);
+      if (c == 1.0f)
+        hipLaunchKernelGGL((flash32_kernel<D, true, false, 1>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+      else
+        hipLaunchKernelGGL((flash32_kernel<D, false, false, 1>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
       return vd_launch_status();
     }
     if (g_flash32 && ((uintptr_t)o & 15) == 0 && ldo % (out_f32 ? 4 : 8) == 0) {
@@ -1728,10 +1740,11 @@ extern "C" int vd_attention_force_v1(int32_t on) {
 // Test/benchmark hook: the d = 40 kernel — 0 = automatic, 1 = flash_attn (16x16x32),
 // 2 = flash32 (4-wave 32x32x16), 3 = flash32pp (8-wave pipeline), 4 = flash32 with the
 // intra-wave interleaved steady state (unit c only), 5 = flash32 held to one workgroup per
-// CU (96 KiB of dynamic LDS: one wave per SIMD — the occupancy probe of DESIGN.md §5).
+// CU (96 KiB of dynamic LDS: one wave per SIMD — the occupancy probe of DESIGN.md §5), 6 =
+// flash32 with one 32-query block per wave (128 VGPRs, four waves per SIMD).
 extern "C" int vd_attention_select(int32_t kernel) {
-  if (kernel < 0 || kernel > 5) return VD_EINVAL;
-  g_flash32 = kernel == 1 ? 0 : (kernel == 3 ? 2 : (kernel == 4 ? 3 : (kernel == 5 ? 4 : 1)));
+  if (kernel < 0 || kernel > 6) return VD_EINVAL;
+  g_flash32 = kernel == 1 ? 0 : (kernel == 3 ? 2 : (kernel == 4 ? 3 : (kernel == 5 ? 4 : (kernel == 6 ? 5 : 1))));
   return VD_OK;
 }
 
