@@ -42,6 +42,7 @@ METRIC = "denoising steps/sec (whole node) at 16-frame 512×512 bf16; 1/2/4/8-GP
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 STEP_TFLOP = {"full": 35.496, "tiny": 0.234}   # BASELINE.md §2 / SURVEY App. B, CFG batch, F=16 / F=4
+WARM_ATTN = 10                 # untimed launches before each roofline timing (tools/prof_summary.py skips them)
 
 
 def log(*a):
@@ -70,7 +71,7 @@ def time_attention(n_img, reps, stream, stress=False):
     out = torch.empty(n_img * S, C, device="cuda", dtype=torch.bfloat16)
     q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
     scale = 1.0 / math.log2(math.e)   # the model's call: softmax scale folded into to_q (Attention.prepare)
-    for _ in range(3):
+    for _ in range(WARM_ATTN):  # ~10 ms of launches: the clock settles after the step loops
         ops.attention(q, k, v, n_img, heads, S, S, d, out=out, scale=scale)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)

@@ -39,15 +39,16 @@ for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:40]:
           f"{k[0]} grid={k[1]} wg={k[2]}")
 
 # bench.py's roofline kernel: after the last step, time_attention() launches the L1
-# self-attention kernel (3 warm-up + attn_reps timed) on its own, first on model-scale inputs
+# self-attention kernel (10 warm-up + attn_reps timed) on its own, first on model-scale inputs
 # (the bench line's roofline.avg_launch_ms), then on the stress inputs (roofline.stress);
 # those launches close the trace and their averages must agree with the bench line.
 after = [r for r in rows if int(r["Start_Timestamp"]) > t1 and "flash32_kernel" in r["Kernel_Name"]]
 halves = [after[:len(after) // 2], after[len(after) // 2:]] if len(after) >= 8 else [after]
+WARM = 10  # bench.py WARM_ATTN
 for tag, part in zip(("model-scale inputs", "stress inputs"), halves):
-    if len(part) <= 3:
+    if len(part) <= WARM:
         continue
-    timed = part[3:]
+    timed = part[WARM:]
     d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed]
     print(f"roofline kernel (bench time_attention, {tag}): {len(d)} timed launches of "
           f"{timed[0]['Kernel_Name'].replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0][:60]} "
