@@ -215,6 +215,17 @@ int vd_temporal_attention_kv(const void* q, int64_t ldq, const void* k, const vo
                              void* o, int64_t ldo, int64_t batch, int32_t qframes, int32_t kframes,
                              int64_t positions, int32_t heads, int32_t d, float scale,
                              vd_stream_t stream);
+/* The motion module's temporal self-attention WITH its Q/K/V projection (round 2): x = the
+ * normed rows (b, f, p) [row stride ldx] of one BasicTransformerBlock attention
+ * (AnimateDiffTransformer3D, a8/a9), wqkv = the fused [3C][C] to_q|to_k|to_v weight (the
+ * softmax scale folded into to_q as vdiff's Attention.prepare does, or passed as `scale`),
+ * o = the attention output rows [row stride ldo], before to_out.  Equal bit for bit to
+ * vd_gemm(x, wqkv) followed by vd_temporal_attention; the [rows][3C] projection never
+ * reaches HBM.  Implemented for the level-1 shape (frames 16, 8 heads, d 40; else
+ * VD_EUNSUPPORTED — callers run the two-launch path). */
+int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* wqkv, int64_t ldw, void* o, int64_t ldo,
+                            int64_t batch, int32_t frames, int64_t positions, int32_t heads, int32_t d,
+                            float scale, vd_stream_t stream);
 /* vd_temporal_attention for the DiT's temporal blocks (d = 64, 17..32 frames) with the 1-D
  * temporal RoPE (vd_rope_qk mode 1, angle by frame) applied to q/k inside the kernel as they
  * are loaded; q and k are read un-rotated and left unchanged.  Returns VD_EUNSUPPORTED while

@@ -773,6 +773,33 @@ def test_temporal_attention_kv(cuda, frames, qf, f0, d):
     close_bf16(got, want.reshape(batch, pos, qf, C).permute(0, 2, 1, 3).reshape(-1, C))
 
 
+@pytest.mark.parametrize("batch,positions,unit", [(2, 4096, True), (1, 100, False), (2, 13, True)])
+def test_motion_qkv_attention(cuda, batch, positions, unit):
+    """vd_motion_qkv_attention (the level-1 motion module's Q/K/V projection fused into its
+    temporal attention) equals vd_gemm + vd_temporal_attention bit for bit — ragged position
+    counts (the last workgroup's idle waves), both softmax-scale forms — and fp64 SDPA of the
+    bf16 projection to bf16 rounding."""
+    C, d, heads, F = 320, 40, 8, 16
+    x = rnd(batch * F * positions, C)
+    w = rnd(3 * C, C, std=C ** -0.5 * 2.0)
+    sc = 1.0 / math.log2(math.e) if unit else None
+    got = ops.motion_qkv_attention(x, w, batch, F, positions, heads, d, scale=sc)
+    assert got is not None
+    qkv = ops.gemm(x, w)
+    want = ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch, F, positions, heads, d, scale=sc)
+    assert torch.equal(got, want)
+    q, k, v = qkv[:, :C].double(), qkv[:, C:2 * C].double(), qkv[:, 2 * C:].double()
+    if unit:
+        q = q * (sc * math.sqrt(d))   # sdpa_ref applies d^-0.5
+
+    def tok(t):  # rows (b, f, p) -> (b*p, f, C)
+        return t.reshape(batch, F, positions, C).permute(0, 2, 1, 3).reshape(batch * positions, F, C)
+
+    ref = sdpa_ref(tok(q), tok(k), tok(v), batch * positions, heads, F, F, d)
+    close_bf16(got, ref.reshape(batch, positions, F, C).permute(0, 2, 1, 3).reshape(-1, C))
+    assert ops.motion_qkv_attention(x[:, :320], w[:, :320], batch, 8, positions * 2, heads, d) is None  # 8 frames
+
+
 # ---------------------------------------------------------------- step glue
 def test_timestep_embed(cuda):
     from oracle.unet_ref import timestep_embedding

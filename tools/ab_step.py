@@ -2,7 +2,8 @@
 variance is ~3 %): python tools/ab_step.py MODE [frames] — alternates two captured-graph loops:
   gn   GroupNorm policy (two-launch image norms vs partial/finalize/apply everywhere)
   ln   LayerNorm fused into the residual GEMM's epilogue (ops.gemm_ln) vs GEMM + vd_layernorm
-  v3p  persistent v3 GEMM vs one unit per workgroup (vd_gemm_select_path 0 vs 11)"""
+  v3p  persistent v3 GEMM vs one unit per workgroup (vd_gemm_select_path 0 vs 11)
+  mq   motion-module Q/K/V projection fused into the temporal attention (L1) vs GEMM + attention"""
 import sys
 import time
 from pathlib import Path
@@ -51,6 +52,15 @@ elif mode == "v3p":
         lib().vd_gemm_select_path(path)  # the plan is fixed at capture
         loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
     lib().vd_gemm_select_path(0)
+elif mode == "mq":
+    from vdiff.models.blocks import BasicTransformerBlock
+    blocks = [m for m in unet.modules() if isinstance(m, BasicTransformerBlock)]
+    for name, on in (("qkv-attn-fused", True), ("qkv-gemm+attn", False)):
+        for m in blocks:
+            m.fuse_qkv_attention = on
+        loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
+    for m in blocks:
+        m.fuse_qkv_attention = True
 else:
     sys.exit(f"unknown mode {mode}")
 res = {k: [] for k in loops}

@@ -116,6 +116,7 @@ class BasicTransformerBlock(nn.Module):
         self.ff = FeedForward(dim)
         self.pos_embed = (SinusoidalPositionalEmbedding(dim, num_positional_embeddings)
                           if positional_embeddings == "sinusoidal" else None)
+        self.fuse_qkv_attention = True  # run_temporal: ops.motion_qkv_attention where it applies
 
     def _nrm(self, i):
         m = getattr(self, f"norm{i}")
@@ -152,9 +153,14 @@ class BasicTransformerBlock(nn.Module):
         if n is None:
             n = ops.layer_norm(h, *self._nrm(1), pe=pe, pe_div=positions, pe_period=frames)
         for attn, i in ((self.attn1, 1), (self.attn2, 2)):
-            qkv = ops.gemm(n, attn._wqkv)
-            a = ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch, frames,
-                                       positions, self.heads, d, scale=attn.attn_scale)
+            # Q/K/V projection fused into the attention where the kernel takes the shape
+            # (level 1: 16 frames, d 40), else the QKV GEMM + the attention kernel
+            a = (ops.motion_qkv_attention(n, attn._wqkv, batch, frames, positions, self.heads, d,
+                                          scale=attn.attn_scale) if self.fuse_qkv_attention else None)
+            if a is None:
+                qkv = ops.gemm(n, attn._wqkv)
+                a = ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch, frames,
+                                           positions, self.heads, d, scale=attn.attn_scale)
             # norm2 (+ PE) after attn1, norm3 after attn2
             h, n = ops.gemm_ln(a, attn._wo, *self._nrm(i + 1), bias=attn._bo, res=h,
                                pe=pe if i == 1 else None, pe_div=positions, pe_period=frames)

@@ -293,6 +293,23 @@ def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, 
     return out
 
 
+def motion_qkv_attention(x, wqkv, batch, frames, positions, heads, d, scale=None, out=None):
+    """Temporal attention over frames with the fused Q/K/V projection folded in
+    (vd_motion_qkv_attention): x = normed rows (b, f, p), wqkv = [3C][C].  Returns None where
+    the fused kernel does not take the shape (the caller runs gemm + temporal_attention)."""
+    _dev(x, wqkv, out)
+    C = heads * d
+    if out is None:
+        out = torch.empty(x.shape[0], C, device=x.device, dtype=BF16)
+    scale = d ** -0.5 if scale is None else scale
+    rc = lib().vd_motion_qkv_attention(_p(x), _rows(x), _p(wqkv), _rows(wqkv), _p(out), _rows(out), batch, frames,
+                                       positions, heads, d, scale, _stream())
+    if rc == VD_EUNSUPPORTED:
+        return None
+    check(rc, "vd_motion_qkv_attention")
+    return out
+
+
 def temporal_attention_kv(q, k, v, batch, qframes, kframes, positions, heads, d, scale=None, out=None):
     """A rank's own `qframes` query frames (rows (b, qframes, p) of q) against `kframes` key
     frames (rows (b, kframes, p) of k/v, e.g. all-gathered from every frame shard)."""
