@@ -221,8 +221,9 @@ int vd_temporal_attention_kv(const void* q, int64_t ldq, const void* k, const vo
  * softmax scale folded into to_q as vdiff's Attention.prepare does, or passed as `scale`),
  * o = the attention output rows [row stride ldo], before to_out.  Equal bit for bit to
  * vd_gemm(x, wqkv) followed by vd_temporal_attention; the [rows][3C] projection never
- * reaches HBM.  Implemented for the level-1 shape (frames 16, 8 heads, d 40; else
- * VD_EUNSUPPORTED — callers run the two-launch path). */
+ * reaches HBM.  Implemented for the level-1 shape (frames 16, 8 heads, d 40) with at least
+ * two workgroups (8 positions of one video each) per CU; else VD_EUNSUPPORTED — callers run
+ * the two-launch path. */
 int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* wqkv, int64_t ldw, void* o, int64_t ldo,
                             int64_t batch, int32_t frames, int64_t positions, int32_t heads, int32_t d,
                             float scale, vd_stream_t stream);

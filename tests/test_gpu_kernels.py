@@ -773,7 +773,7 @@ def test_temporal_attention_kv(cuda, frames, qf, f0, d):
     close_bf16(got, want.reshape(batch, pos, qf, C).permute(0, 2, 1, 3).reshape(-1, C))
 
 
-@pytest.mark.parametrize("batch,positions,unit", [(2, 4096, True), (1, 100, False), (2, 13, True)])
+@pytest.mark.parametrize("batch,positions,unit", [(2, 4096, True), (1, 4100, False), (3, 1373, True)])
 def test_motion_qkv_attention(cuda, batch, positions, unit):
     """vd_motion_qkv_attention (the level-1 motion module's Q/K/V projection fused into its
     temporal attention) equals vd_gemm + vd_temporal_attention bit for bit — ragged position
@@ -798,6 +798,7 @@ def test_motion_qkv_attention(cuda, batch, positions, unit):
     ref = sdpa_ref(tok(q), tok(k), tok(v), batch * positions, heads, F, F, d)
     close_bf16(got, ref.reshape(batch, positions, F, C).permute(0, 2, 1, 3).reshape(-1, C))
     assert ops.motion_qkv_attention(x[:, :320], w[:, :320], batch, 8, positions * 2, heads, d) is None  # 8 frames
+    assert ops.motion_qkv_attention(x[:16 * 64], w, 1, F, 64, heads, d) is None  # 8 workgroups: unfused path
 
 
 # ---------------------------------------------------------------- step glue

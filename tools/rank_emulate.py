@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--window", default="a2a", choices=["a2a", "kv-gather"])
     ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--mq", default="on", choices=["on", "off", "both"],
+                    help="motion-module Q/K/V projection fused into the temporal attention (A/B with both)")
     args = ap.parse_args()
     unet = materialize_synthetic("full", device="cuda", seed=0)
     fl = args.frames // args.world
@@ -70,7 +72,12 @@ def main():
     s.set_timesteps(50)
     ts = s.timesteps.repeat(2)
     res = {}
-    for c in args.chunks:
+    from vdiff.models.blocks import BasicTransformerBlock
+    blocks = [m for m in unet.modules() if isinstance(m, BasicTransformerBlock)]
+    runs = [(c, mq) for c in args.chunks for mq in ({"on": [True], "off": [False], "both": [True, False]}[args.mq])]
+    for c, mq in runs:
+        for m in blocks:
+            m.fuse_qkv_attention = mq
         unet.dist = EmulatedShard(args.world, c, args.comm, args.window) if args.world > 1 else None
         unet.prepare()
         loop = DenoiseLoop(unet, s, lat, ehs, 7.5, timesteps=ts, use_graph=True).prime()
@@ -81,9 +88,9 @@ def main():
         loop.run(args.steps)
         torch.cuda.synchronize()
         ms = 1e3 * (time.perf_counter() - t0) / args.steps
-        res[c] = round(ms, 3)
-        print(f"world {args.world} frames/rank {fl} window {args.window} chunks {c} comm {args.comm}: {ms:.3f} ms/step",
-              flush=True)
+        res[f"{c}{'' if mq else ' (mq off)'}"] = round(ms, 3)
+        print(f"world {args.world} frames/rank {fl} window {args.window} chunks {c} comm {args.comm}"
+              f"{'' if mq else ' qkv-attn unfused'}: {ms:.3f} ms/step", flush=True)
         del loop
     print(json.dumps({"world": args.world, "frames_local": fl, "window": args.window, "comm": args.comm,
                       "ms_per_step": res}))

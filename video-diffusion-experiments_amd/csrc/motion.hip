@@ -248,6 +248,14 @@ extern "C" int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* w
   VD_CHECK_ARG(ldx >= Cf::C && ldw >= Cf::C && ldo >= Cf::C);
   const int64_t nwg = batch * ((positions + Cf::P - 1) / Cf::P);
   VD_CHECK_ARG(nwg < 0x7fffffff && batch * MF * positions < 0x7fffffff);
+  // one workgroup per CU (156 KiB of LDS): below two rounds of the chip the unfused GEMM +
+  // attention is faster (a 2-frame rank of the 8-way run, 128 workgroups: 13.92 vs 13.66
+  // ms/step, tools/rank_emulate.py --mq both; the full 16-frame step, 1024: -0.31 ms/step)
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  if (nwg < 2 * (int64_t)cus) return VD_EUNSUPPORTED;
   static bool attr_set = false;
   if (!attr_set) {  // > 64 KiB of dynamic LDS
     if (hipFuncSetAttribute((const void*)motion_qkv_attn_kernel<40>, hipFuncAttributeMaxDynamicSharedMemorySize,
