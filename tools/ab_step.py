@@ -3,7 +3,9 @@ variance is ~3 %): python tools/ab_step.py MODE [frames] — alternates two capt
   gn   GroupNorm policy (two-launch image norms vs partial/finalize/apply everywhere)
   ln   LayerNorm fused into the residual GEMM's epilogue (ops.gemm_ln) vs GEMM + vd_layernorm
   v3p  persistent v3 GEMM vs one unit per workgroup (vd_gemm_select_path 0 vs 11)
-  mq   motion-module Q/K/V projection fused into the temporal attention (L1) vs GEMM + attention"""
+  mq   motion-module Q/K/V projection fused into the temporal attention (L1) vs GEMM + attention
+  pf   v2/v6 GEMM fragment-read order: the default vs round 1's, k-step-pipelined and all-ahead
+       (vd_gemm_select_path 0 / 12 / 13 / 14)"""
 import sys
 import time
 from pathlib import Path
@@ -50,6 +52,12 @@ elif mode == "v3p":
     from vdiff._lib import lib
     for name, path in (("v3-persistent", 0), ("v3-per-tile", 11)):
         lib().vd_gemm_select_path(path)  # the plan is fixed at capture
+        loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
+    lib().vd_gemm_select_path(0)
+elif mode == "pf":
+    from vdiff._lib import lib
+    for name, path in (("frag-default", 0), ("frag-r1-order", 12), ("frag-pipelined", 13), ("frag-all-ahead", 14)):
+        lib().vd_gemm_select_path(path)  # the launch choice is fixed at capture
         loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
     lib().vd_gemm_select_path(0)
 elif mode == "mq":

@@ -372,6 +372,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
 // num_records returns 0).  Per-tile address work: one integer add per load.
 constexpr int G2_BM = 256, G2_NT = 512, G2_STAGES = 3;
 int g_num_cus = 256;  // MI355X; refreshed from the device on first use
+// v2 fragment-read order (A/B: vd_gemm_select_path 12/13/14 force 0/2/1); -1 = the default, 2:
+// k-step 0's reads ahead, k-step 1's interleaved with k-step 0's MFMAs (tools/ab_step.py pf:
+// 52.79 vs 53.50 ms/step for round 1's order, 53.11 all-ahead; profiles/r02f_fragment_order.txt)
+int g_g2_pf = -1;
+int g_g2_old = 0;     // 1: v6 with the round-1 fragment-read order (vd_gemm_select_path(12))
 constexpr uint32_t G2_OOB = 0x80000000u;
 
 template <int BN>
@@ -402,7 +407,12 @@ __device__ __forceinline__ void wait_vm() {
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
-template <int BN, int MODE>
+// PF (fragment-read order, round 2): without a pin hipcc sinks each X fragment read to its 4
+// MFMAs behind an lgkmcnt(0) — 8 exposed LDS latencies per K-tile (PF = 0, round 1's order).
+// PF = 1 issues all 18 reads of the K-tile right after the barrier (sched_barrier), PF = 2 (the
+// default) issues k-step 0's 9 reads, then interleaves k-step 1's reads one per two of k-step
+// 0's MFMAs (sched_group_barrier), so the MFMA chain waits on counted lgkmcnt only.
+template <int BN, int MODE, int PF = 1>
 __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                          uint32_t a1_bytes, uint32_t w_bytes,
                                                          int split) {
@@ -576,20 +586,48 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's DMA for `it` landed; stage (it-1)%3 fully read
     const char* sbase = smem + stage * C::STAGE;
+    if constexpr (PF != 0) {
+      bf16x8 wf[BK / 32][C::NB], xf[BK / 32][C::MB];
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 wf[C::NB], xf[C::MB];
-      const char* wp = sbase + wlane[ks];
-      const char* xp = sbase + xlane[ks];
+      for (int ks = 0; ks < BK / 32; ++ks) {
 #pragma unroll
-      for (int a = 0; a < C::NB; ++a) wf[a] = *(const bf16x8*)(wp + a * 16 * BK * 2);
+        for (int b = 0; b < C::MB; ++b) xf[ks][b] = *(const bf16x8*)(sbase + xlane[ks] + b * 16 * BK * 2);
 #pragma unroll
-      for (int b = 0; b < C::MB; ++b) xf[b] = *(const bf16x8*)(xp + b * 16 * BK * 2);
+        for (int a = 0; a < C::NB; ++a) wf[ks][a] = *(const bf16x8*)(sbase + wlane[ks] + a * 16 * BK * 2);
+        if (PF == 1 || ks == 0) __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
-      for (int a = 0; a < C::NB; ++a)
+      for (int ks = 0; ks < BK / 32; ++ks)
 #pragma unroll
-        for (int b = 0; b < C::MB; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][b], 0, 0, 0);
+        for (int a = 0; a < C::NB; ++a)
+#pragma unroll
+          for (int b = 0; b < C::MB; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][a], xf[ks][b], acc[a][b], 0, 0, 0);
+      if constexpr (PF == 2) {  // k-step 1's reads one per two of k-step 0's MFMAs
+        constexpr int NR = C::MB + C::NB, NM = 2 * C::MB * C::NB;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8 wf[C::NB], xf[C::MB];
+        const char* wp = sbase + wlane[ks];
+        const char* xp = sbase + xlane[ks];
+#pragma unroll
+        for (int a = 0; a < C::NB; ++a) wf[a] = *(const bf16x8*)(wp + a * 16 * BK * 2);
+#pragma unroll
+        for (int b = 0; b < C::MB; ++b) xf[b] = *(const bf16x8*)(xp + b * 16 * BK * 2);
+#pragma unroll
+        for (int a = 0; a < C::NB; ++a)
+#pragma unroll
+          for (int b = 0; b < C::MB; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][b], 0, 0, 0);
+      }
     }
     if (++ckt == ckt1) {  // unit finished: epilogue (its memory ops precede the next DMA)
       const int tile = cu / split, sp = cu % split;
@@ -1420,7 +1458,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
 constexpr int G6_BM = 64, G6_BN = 64, G6_NT = 256;
 constexpr int G6_A = G6_BM * BK * 2, G6_W = G6_BN * BK * 2, G6_STAGE = G6_A + G6_W;  // 8 + 8 KiB
 
-template <int MODE, int G6_S>
+template <int MODE, int G6_S, bool PF = true>  // PF: as gemm2's (all fragment reads ahead of the MFMAs)
 __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void gemm6_kernel(
     const vd_gemm_desc d, uint32_t a0_bytes, uint32_t a1_bytes, uint32_t w_bytes, int split) {
   constexpr int MB = 2, NB = 2;
@@ -1536,18 +1574,38 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
     __builtin_amdgcn_s_barrier();
     if (it + G6_S - 1 < nk) issue(stage == 0 ? G6_S - 1 : stage - 1);
     const char* sb = smem + stage * G6_STAGE;
+    if constexpr (PF) {
+      bf16x8 wf[BK / 32][NB], xf[BK / 32][MB];
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 wf[NB], xf[MB];
+      for (int ks = 0; ks < BK / 32; ++ks) {
 #pragma unroll
-      for (int a = 0; a < NB; ++a) wf[a] = *(const bf16x8*)(sb + G6_A + 2 * lds_off(wn * 32 + a * 16 + fr, ks * 4 + fq));
+        for (int b = 0; b < MB; ++b) xf[ks][b] = *(const bf16x8*)(sb + 2 * lds_off(wm * 32 + b * 16 + fr, ks * 4 + fq));
 #pragma unroll
-      for (int b = 0; b < MB; ++b) xf[b] = *(const bf16x8*)(sb + 2 * lds_off(wm * 32 + b * 16 + fr, ks * 4 + fq));
+        for (int a = 0; a < NB; ++a)
+          wf[ks][a] = *(const bf16x8*)(sb + G6_A + 2 * lds_off(wn * 32 + a * 16 + fr, ks * 4 + fq));
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int a = 0; a < NB; ++a)
+      for (int ks = 0; ks < BK / 32; ++ks)
 #pragma unroll
-        for (int b = 0; b < MB; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][b], 0, 0, 0);
+        for (int a = 0; a < NB; ++a)
+#pragma unroll
+          for (int b = 0; b < MB; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][a], xf[ks][b], acc[a][b], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8 wf[NB], xf[MB];
+#pragma unroll
+        for (int a = 0; a < NB; ++a) wf[a] = *(const bf16x8*)(sb + G6_A + 2 * lds_off(wn * 32 + a * 16 + fr, ks * 4 + fq));
+#pragma unroll
+        for (int b = 0; b < MB; ++b) xf[b] = *(const bf16x8*)(sb + 2 * lds_off(wm * 32 + b * 16 + fr, ks * 4 + fq));
+#pragma unroll
+        for (int a = 0; a < NB; ++a)
+#pragma unroll
+          for (int b = 0; b < MB; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][b], 0, 0, 0);
+      }
     }
     stage = stage == G6_S - 1 ? 0 : stage + 1;
   }
@@ -1706,12 +1764,19 @@ int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   // persistent: one workgroup per CU, ceil(units / grid) rounds, balanced grid
   const int64_t rounds = (units + g_num_cus - 1) / g_num_cus;
   const int64_t grid = (units + rounds - 1) / rounds;
-  if (d.a_mode == VD_A_CONV3X3)
-    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb,
-                       split);
-  else
-    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb,
-                       split);
+  const int pf = g_g2_pf >= 0 ? g_g2_pf : 2;
+#define G2_LAUNCH(MODE_, PF_) \
+  hipLaunchKernelGGL((gemm2_kernel<BN, MODE_, PF_>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split)
+  if (d.a_mode == VD_A_CONV3X3) {
+    if (pf == 0) G2_LAUNCH(VD_A_CONV3X3, 0);
+    else if (pf == 1) G2_LAUNCH(VD_A_CONV3X3, 1);
+    else G2_LAUNCH(VD_A_CONV3X3, 2);
+  } else {
+    if (pf == 0) G2_LAUNCH(VD_A_DENSE, 0);
+    else if (pf == 1) G2_LAUNCH(VD_A_DENSE, 1);
+    else G2_LAUNCH(VD_A_DENSE, 2);
+  }
+#undef G2_LAUNCH
   int rc = vd_launch_status();
   if (rc != VD_OK || split == 1) return rc;
   const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
@@ -1765,10 +1830,14 @@ int launch6(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   }
   const int64_t wgs = tiles * split;
   const dim3 grid((unsigned)wgs);
-#define G6_LAUNCH(S)                                                                                    \
-  if (d.a_mode == VD_A_CONV3X3)                                                                         \
-    hipLaunchKernelGGL((gemm6_kernel<VD_A_CONV3X3, S>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split); \
-  else                                                                                                  \
+#define G6_LAUNCH(S)                                                                                           \
+  if (d.a_mode == VD_A_CONV3X3 && g_g2_old)                                                                    \
+    hipLaunchKernelGGL((gemm6_kernel<VD_A_CONV3X3, S, false>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split); \
+  else if (d.a_mode == VD_A_CONV3X3)                                                                           \
+    hipLaunchKernelGGL((gemm6_kernel<VD_A_CONV3X3, S>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split);        \
+  else if (g_g2_old)                                                                                           \
+    hipLaunchKernelGGL((gemm6_kernel<VD_A_DENSE, S, false>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split);   \
+  else                                                                                                         \
     hipLaunchKernelGGL((gemm6_kernel<VD_A_DENSE, S>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split);
   if (wgs <= g_num_cus) {
     G6_LAUNCH(6)
@@ -1984,7 +2053,10 @@ extern "C" int vd_gemm_force_v1(int32_t on) {
   return VD_OK;
 }
 extern "C" int vd_gemm_select_path(int32_t path) {
-  if (path < 0 || path > 11 || path == 4) return VD_EINVAL;
+  if (path < 0 || path > 14 || path == 4) return VD_EINVAL;
+  g_g2_old = path == 12;
+  g_g2_pf = path == 12 ? 0 : path == 13 ? 2 : path == 14 ? 1 : -1;
+  if (path >= 12) path = 0;  // auto plan; v2 / v6 fragment-read order forced (A/B)
   g_split_cap = path == 9 ? 8 : 32;
   g_path = path == 9 ? 0 : path;
   return VD_OK;
