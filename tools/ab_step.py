@@ -5,7 +5,8 @@ variance is ~3 %): python tools/ab_step.py MODE [frames] — alternates two capt
   v3p  persistent v3 GEMM vs one unit per workgroup (vd_gemm_select_path 0 vs 11)
   mq   motion-module Q/K/V projection fused into the temporal attention (L1) vs GEMM + attention
   pf   v2/v6 GEMM fragment-read order: the default vs round 1's, k-step-pipelined and all-ahead
-       (vd_gemm_select_path 0 / 12 / 13 / 14)"""
+       (vd_gemm_select_path 0 / 12 / 13 / 14)
+  v3e  v3 GEMM with the LDS-bias load-free epilogue vs gemm_epilogue (vd_gemm_select_path 0 vs 15)"""
 import sys
 import time
 from pathlib import Path
@@ -58,6 +59,12 @@ elif mode == "pf":
     from vdiff._lib import lib
     for name, path in (("frag-default", 0), ("frag-r1-order", 12), ("frag-pipelined", 13), ("frag-all-ahead", 14)):
         lib().vd_gemm_select_path(path)  # the launch choice is fixed at capture
+        loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
+    lib().vd_gemm_select_path(0)
+elif mode == "v3e":
+    from vdiff._lib import lib
+    for name, path in (("v3-lds-bias", 0), ("v3-gemm-epi", 15)):
+        lib().vd_gemm_select_path(path)
         loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
     lib().vd_gemm_select_path(0)
 elif mode == "mq":

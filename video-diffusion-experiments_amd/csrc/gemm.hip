@@ -659,6 +659,108 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
   }
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// Load-free epilogue (v5, split == 1, bf16 out, no residual / row bias): the bias
+// comes from the unit's LDS slot (DMA'd with its first k-step) and every store is
+// an UNCONDITIONAL buffer store whose out-of-range lanes carry an offset past the
+// resource's num_records (dropped by the hardware).  So the epilogue issues no
+// vector-memory load — nothing makes the wave wait for the k-steps still in flight
+// — and a compile-time number of stores, which the k-loop's counted vmcnt then
+// leaves outstanding instead of draining.  Returns that number.
+template <int MB, int NB>
+__device__ __forceinline__ int epi_fast(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], int mbase, int nbase, int lane,
+                                        const float* bsl, int n0, __amdgpu_buffer_rsrc_t ro) {
+  static_assert(NB % 2 == 0, "epi_fast: whole 16-column pairs");
+  const int M = (int)d.M, N = (int)d.N, ldc = (int)d.ldc;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int wcol = 16 * (fq & 1) + 8 * (fq >> 1);
+  int nst = 0;
+  if (d.act == VD_ACT_GEGLU) {
+    // pairs (a, a+1) = (hidden, gate) blocks -> 16 output columns; pair-pairs swapped
+    // by permlane16 into 8 consecutive columns per lane (16-B stores), a lone last
+    // pair stores 4 columns (8 B)
+    constexpr int NP = NB / 2;
+#pragma unroll
+    for (int pp = 0; pp + 1 < NP; pp += 2) {
+      const int a = 2 * pp;
+      const int c0 = nbase - n0 + a * 16 + 4 * fq;  // column of acc[a][.][0] inside the tile
+      const float4 th0 = *(const float4*)(bsl + c0), tg0 = *(const float4*)(bsl + c0 + 16);
+      const float4 th1 = *(const float4*)(bsl + c0 + 32), tg1 = *(const float4*)(bsl + c0 + 48);
+      const float bh0[4] = {th0.x, th0.y, th0.z, th0.w}, bg0[4] = {tg0.x, tg0.y, tg0.z, tg0.w};
+      const float bh1[4] = {th1.x, th1.y, th1.z, th1.w}, bg1[4] = {tg1.x, tg1.y, tg1.z, tg1.w};
+      const int nout = nbase / 2 + pp * 16 + wcol;
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        const int m = mbase + b * 16 + fr;
+        uint32_t x[2], y[2];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const float o0 = (acc[a][b][2 * h2] + bh0[2 * h2]) * gelu_erf(acc[a + 1][b][2 * h2] + bg0[2 * h2]);
+          const float o1 = (acc[a][b][2 * h2 + 1] + bh0[2 * h2 + 1]) * gelu_erf(acc[a + 1][b][2 * h2 + 1] + bg0[2 * h2 + 1]);
+          const float p0 = (acc[a + 2][b][2 * h2] + bh1[2 * h2]) * gelu_erf(acc[a + 3][b][2 * h2] + bg1[2 * h2]);
+          const float p1 = (acc[a + 2][b][2 * h2 + 1] + bh1[2 * h2 + 1]) * gelu_erf(acc[a + 3][b][2 * h2 + 1] + bg1[2 * h2 + 1]);
+          auto r = __builtin_amdgcn_permlane16_swap(pack2(o0, o1), pack2(p0, p1), false, false);
+          x[h2] = r[0];
+          y[h2] = r[1];
+        }
+        const bool ok = m < M && 2 * nout < N;
+        const uint32_t off = ok ? (uint32_t)(m * ldc + nout) * 2u : G2_OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{x[0], x[1], y[0], y[1]}, ro, off, 0, 0);
+        ++nst;
+      }
+    }
+    if constexpr (NP % 2 == 1) {
+      const int a = NB - 2;
+      const int c0 = nbase - n0 + a * 16 + 4 * fq;
+      const float4 th = *(const float4*)(bsl + c0), tg = *(const float4*)(bsl + c0 + 16);
+      const float bh[4] = {th.x, th.y, th.z, th.w}, bg[4] = {tg.x, tg.y, tg.z, tg.w};
+      const int nout = nbase / 2 + (a / 2) * 16 + 4 * fq;
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        const int m = mbase + b * 16 + fr;
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (acc[a][b][j] + bh[j]) * gelu_erf(acc[a + 1][b][j] + bg[j]);
+        const bool ok = m < M && 2 * nout < N;
+        const uint32_t off = ok ? (uint32_t)(m * ldc + nout) * 2u : G2_OOB;
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])}, ro, off, 0, 0);
+        ++nst;
+      }
+    }
+    return nst;
+  }
+#pragma unroll
+  for (int a = 0; a < NB; a += 2) {
+    const int n = nbase + a * 16 + wcol;  // first of this lane's 8 columns after the swap
+    const float4 t0 = *(const float4*)(bsl + (n - n0)), t1 = *(const float4*)(bsl + (n - n0) + 4);
+    const float bv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      const int m = mbase + b * 16 + fr;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[a][b][j]), __float_as_uint(acc[a + 1][b][j]),
+                                                  false, false);
+        o[j] = __uint_as_float(r[0]) + bv[j];
+        o[4 + j] = __uint_as_float(r[1]) + bv[4 + j];
+      }
+      if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = act_pw(d.act, o[j]);
+      }
+      const uint4 pk = pack8(o);
+      const bool ok = m < M && n < N;
+      const uint32_t off = ok ? (uint32_t)(m * ldc + n) * 2u : G2_OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{pk.x, pk.y, pk.z, pk.w}, ro, off, 0, 0);
+      ++nst;
+    }
+  }
+  return nst;
+}
+
 // ============================================================================ v3
 // 256x256 tile, 8 waves as 2(M) x 4(N) (128 x 64 per wave: 0.375 LDS fragment
 // reads per MFMA vs 0.45 for v2's 64 x 80), after the 8-phase template of
@@ -693,6 +795,13 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
 constexpr int G3_BM = 256, G3_BN = 256, G3_NT = 512;
 constexpr int G3_A_BYTES = G3_BM * BK * 2;     // 32 KiB
 constexpr int G3_STAGE = 2 * G3_A_BYTES;       // A + W: 64 KiB
+// Load-free epilogue (round 2): for plain bf16 outputs (no residual / row bias, unsplit) with
+// N <= G3_BIAS_N the whole bias vector is copied into LDS once, before the first DMA, and the
+// epilogue is v5's epi_fast (bias from LDS, unconditional buffer stores).  gemm_epilogue's
+// global bias loads made hipcc wait vmcnt(0) at every unit boundary — draining the next
+// unit's two K-tiles of DMA under the epilogue (20 units per CU at the L1 GEGLU).
+constexpr int G3_BIAS_N = 5120;
+int g_g3_fast = 1;  // 0: gemm_epilogue everywhere (vd_gemm_select_path(15), A/B only)
 
 struct G3Cursor {  // a position (unit, local K-tile) in the workgroup's flat K-tile stream
   int u, t, kt0, nk, m0, n0;
@@ -700,9 +809,10 @@ struct G3Cursor {  // a position (unit, local K-tile) in the workgroup's flat K-
 
 template <int MODE>
 __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
-                                                         uint32_t a1_bytes, uint32_t w_bytes, int split) {
+                                                         uint32_t a1_bytes, uint32_t w_bytes, int split,
+                                                         int fast) {
   static_assert(MODE == VD_A_DENSE, "gemm3: dense A only");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * G3_STAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * G3_STAGE + G3_BIAS_N * 4];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 2, wc = wid & 3;
@@ -741,6 +851,14 @@ __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, u
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.a1 ? d.a1 : d.a0), 0, d.a1 ? a1_bytes : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, w_bytes, 0x00020000);
   const uint32_t lda0b = (uint32_t)d.lda0 * 2, lda1b = (uint32_t)d.lda1 * 2, ldwb = (uint32_t)d.ldw * 2;
+  float* const bias_lds = (float*)(smem + 2 * G3_STAGE);
+  const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(d.out, 0, (uint32_t)(M * d.ldc * 2), 0x00020000);
+  if (fast) {  // the bias (or zeros) into LDS before any DMA is in flight; the prologue's
+               // lgkmcnt(0) + s_barrier publish it
+    for (int i = 4 * tid; i < N; i += 4 * G3_NT)
+      *(float4*)(bias_lds + i) = d.bias ? *(const float4*)(d.bias + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 
   // DMA slots (wave-uniform LDS offsets; per-lane source rows from the cursor's tile): X part
   // q, slot j covers A rows 128*wr + 64*q + 8*(2*wc + j) + 0..7; W part q, slot j covers W
@@ -857,7 +975,9 @@ __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, u
     if (c0.t + 1 == c0.nk) {  // unit finished
       if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
       const int mbase = c0.m0 + 128 * wr, nbase = c0.n0 + 64 * wc;
-      if (split == 1) {
+      if (fast) {
+        epi_fast<8, 4>(d, acc, mbase, nbase, lane, bias_lds + c0.n0, c0.n0, rout);
+      } else if (split == 1) {
         gemm_epilogue<8, 4>(d, acc, mbase, nbase, lane);
       } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
         float* slab = (float*)d.ws + (int64_t)(c0.u % split) * d.M * d.N;
@@ -944,108 +1064,6 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
     default: s_wait_vm<63>(); break;
   }
 #undef VM4
-}
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-// Load-free epilogue (v5, split == 1, bf16 out, no residual / row bias): the bias
-// comes from the unit's LDS slot (DMA'd with its first k-step) and every store is
-// an UNCONDITIONAL buffer store whose out-of-range lanes carry an offset past the
-// resource's num_records (dropped by the hardware).  So the epilogue issues no
-// vector-memory load — nothing makes the wave wait for the k-steps still in flight
-// — and a compile-time number of stores, which the k-loop's counted vmcnt then
-// leaves outstanding instead of draining.  Returns that number.
-template <int MB, int NB>
-__device__ __forceinline__ int epi_fast(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], int mbase, int nbase, int lane,
-                                        const float* bsl, int n0, __amdgpu_buffer_rsrc_t ro) {
-  static_assert(NB % 2 == 0, "epi_fast: whole 16-column pairs");
-  const int M = (int)d.M, N = (int)d.N, ldc = (int)d.ldc;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int wcol = 16 * (fq & 1) + 8 * (fq >> 1);
-  int nst = 0;
-  if (d.act == VD_ACT_GEGLU) {
-    // pairs (a, a+1) = (hidden, gate) blocks -> 16 output columns; pair-pairs swapped
-    // by permlane16 into 8 consecutive columns per lane (16-B stores), a lone last
-    // pair stores 4 columns (8 B)
-    constexpr int NP = NB / 2;
-#pragma unroll
-    for (int pp = 0; pp + 1 < NP; pp += 2) {
-      const int a = 2 * pp;
-      const int c0 = nbase - n0 + a * 16 + 4 * fq;  // column of acc[a][.][0] inside the tile
-      const float4 th0 = *(const float4*)(bsl + c0), tg0 = *(const float4*)(bsl + c0 + 16);
-      const float4 th1 = *(const float4*)(bsl + c0 + 32), tg1 = *(const float4*)(bsl + c0 + 48);
-      const float bh0[4] = {th0.x, th0.y, th0.z, th0.w}, bg0[4] = {tg0.x, tg0.y, tg0.z, tg0.w};
-      const float bh1[4] = {th1.x, th1.y, th1.z, th1.w}, bg1[4] = {tg1.x, tg1.y, tg1.z, tg1.w};
-      const int nout = nbase / 2 + pp * 16 + wcol;
-#pragma unroll
-      for (int b = 0; b < MB; ++b) {
-        const int m = mbase + b * 16 + fr;
-        uint32_t x[2], y[2];
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          const float o0 = (acc[a][b][2 * h2] + bh0[2 * h2]) * gelu_erf(acc[a + 1][b][2 * h2] + bg0[2 * h2]);
-          const float o1 = (acc[a][b][2 * h2 + 1] + bh0[2 * h2 + 1]) * gelu_erf(acc[a + 1][b][2 * h2 + 1] + bg0[2 * h2 + 1]);
-          const float p0 = (acc[a + 2][b][2 * h2] + bh1[2 * h2]) * gelu_erf(acc[a + 3][b][2 * h2] + bg1[2 * h2]);
-          const float p1 = (acc[a + 2][b][2 * h2 + 1] + bh1[2 * h2 + 1]) * gelu_erf(acc[a + 3][b][2 * h2 + 1] + bg1[2 * h2 + 1]);
-          auto r = __builtin_amdgcn_permlane16_swap(pack2(o0, o1), pack2(p0, p1), false, false);
-          x[h2] = r[0];
-          y[h2] = r[1];
-        }
-        const bool ok = m < M && 2 * nout < N;
-        const uint32_t off = ok ? (uint32_t)(m * ldc + nout) * 2u : G2_OOB;
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{x[0], x[1], y[0], y[1]}, ro, off, 0, 0);
-        ++nst;
-      }
-    }
-    if constexpr (NP % 2 == 1) {
-      const int a = NB - 2;
-      const int c0 = nbase - n0 + a * 16 + 4 * fq;
-      const float4 th = *(const float4*)(bsl + c0), tg = *(const float4*)(bsl + c0 + 16);
-      const float bh[4] = {th.x, th.y, th.z, th.w}, bg[4] = {tg.x, tg.y, tg.z, tg.w};
-      const int nout = nbase / 2 + (a / 2) * 16 + 4 * fq;
-#pragma unroll
-      for (int b = 0; b < MB; ++b) {
-        const int m = mbase + b * 16 + fr;
-        float o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = (acc[a][b][j] + bh[j]) * gelu_erf(acc[a + 1][b][j] + bg[j]);
-        const bool ok = m < M && 2 * nout < N;
-        const uint32_t off = ok ? (uint32_t)(m * ldc + nout) * 2u : G2_OOB;
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])}, ro, off, 0, 0);
-        ++nst;
-      }
-    }
-    return nst;
-  }
-#pragma unroll
-  for (int a = 0; a < NB; a += 2) {
-    const int n = nbase + a * 16 + wcol;  // first of this lane's 8 columns after the swap
-    const float4 t0 = *(const float4*)(bsl + (n - n0)), t1 = *(const float4*)(bsl + (n - n0) + 4);
-    const float bv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
-#pragma unroll
-    for (int b = 0; b < MB; ++b) {
-      const int m = mbase + b * 16 + fr;
-      float o[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[a][b][j]), __float_as_uint(acc[a + 1][b][j]),
-                                                  false, false);
-        o[j] = __uint_as_float(r[0]) + bv[j];
-        o[4 + j] = __uint_as_float(r[1]) + bv[4 + j];
-      }
-      if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = act_pw(d.act, o[j]);
-      }
-      const uint4 pk = pack8(o);
-      const bool ok = m < M && n < N;
-      const uint32_t off = ok ? (uint32_t)(m * ldc + n) * 2u : G2_OOB;
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{pk.x, pk.y, pk.z, pk.w}, ro, off, 0, 0);
-      ++nst;
-    }
-  }
-  return nst;
 }
 
 // Epilogue with the next LayerNorm fused (vd_gemm_desc.ln_out; v5 with N == BN == 320, so
@@ -1857,7 +1875,11 @@ int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   // persistent: one workgroup per CU, ceil(units / CUs) units each, balanced grid
   const int64_t rounds = persistent ? (units + g_num_cus - 1) / g_num_cus : 1;
   const int64_t grid = (units + rounds - 1) / rounds;
-  hipLaunchKernelGGL((gemm3_kernel<VD_A_DENSE>), dim3((unsigned)grid), dim3(G3_NT), 0, s, d, a0b, a1b, wb, split);
+  const int fast = g_g3_fast && split == 1 && !d.res && !d.rowbias && !d.out_f32 && d.N % 8 == 0 &&
+                   d.N <= G3_BIAS_N && d.ldc % 8 == 0 && ((uintptr_t)d.out & 15) == 0 &&
+                   d.M * d.ldc * 2 < (int64_t)G2_OOB;
+  hipLaunchKernelGGL((gemm3_kernel<VD_A_DENSE>), dim3((unsigned)grid), dim3(G3_NT), 0, s, d, a0b, a1b, wb, split,
+                     fast);
   int rc = vd_launch_status();
   if (rc != VD_OK || split == 1) return rc;
   const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
@@ -2053,7 +2075,9 @@ extern "C" int vd_gemm_force_v1(int32_t on) {
   return VD_OK;
 }
 extern "C" int vd_gemm_select_path(int32_t path) {
-  if (path < 0 || path > 14 || path == 4) return VD_EINVAL;
+  if (path < 0 || path > 15 || path == 4) return VD_EINVAL;
+  g_g3_fast = path != 15;
+  if (path == 15) path = 0;  // auto plan, v3 with gemm_epilogue (A/B)
   g_g2_old = path == 12;
   g_g2_pf = path == 12 ? 0 : path == 13 ? 2 : path == 14 ? 1 : -1;
   if (path >= 12) path = 0;  // auto plan; v2 / v6 fragment-read order forced (A/B)
