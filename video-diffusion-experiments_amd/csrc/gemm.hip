@@ -2037,7 +2037,12 @@ Plan plan(const vd_gemm_desc& d) {
   // persistent v3 (round 2) also wins at 1/8 padding with short K: L2 qkv N 1920 -> 2048,
   // K 640: 98 vs 109 us on v2 (profiles/r02_gemm3_persistent.txt)
   const bool v3pad = (p256 - d.N) * 8 <= d.N;
-  const bool v3auto = v3ok && d.N >= 768 && v3pad && ((d.M + G3_BM - 1) / G3_BM) * (p256 / 256) >= 256;
+  const int64_t tiles3 = ((d.M + G3_BM - 1) / G3_BM) * (p256 / 256);
+  // GEGLU on v3 only from 3 tiles per CU: after the v2 fragment-order fix (round 2) v2's 256 x 128
+  // tiles win the 320-640-tile GEGLUs (4 images L1 46 vs 51 us, L2 41 vs 52; 32 images L4 66 vs
+  // 81 us; tools/plan_sweep.py, profiles/r02f_plan_sweep.txt)
+  const bool v3auto = v3ok && d.N >= 768 && v3pad && tiles3 >= 256 &&
+                      (d.act != VD_ACT_GEGLU || tiles3 >= 3 * g_num_cus);
   if (g_path == 3 || g_path == 10 ? v3ok : v3auto) {
     p.ver = 3;
     p.bn = 256;
