@@ -2,7 +2,7 @@
 v2 / v3 / v5 / v6 and the automatic plan, interleaved over rounds in one process (min of the
 rounds reported; a warm-up pass first so no case pays the clock ramp).
 
-python tools/plan_sweep.py [images ...]   (default 32 4)"""
+python tools/plan_sweep.py [images ...]   (default 32 4; SWEEP=dense / conv / dense,conv)"""
 import sys
 from pathlib import Path
 
@@ -31,7 +31,17 @@ def run(imgs):
                   (f"L{lvl+1} ff2+res  M={M} N={C} K={4*C}", M, C, 4 * C, True, False),
                   (f"L{lvl+1} geglu    M={M} N={8*C} K={C}", M, 8 * C, C, False, True)]
     fns = []
+    for name, hw, ci, co in [("L1 conv 320->320", 64, 320, 320), ("L1 conv 640->320", 64, 640, 320),
+                             ("L2 conv 640->640", 32, 640, 640), ("L2 conv 1280->640", 32, 1280, 640),
+                             ("L3 conv 1280->1280", 16, 1280, 1280), ("L3 conv 2560->1280", 16, 2560, 1280),
+                             ("L4 conv 1280->1280", 8, 1280, 1280), ("L4 conv 2560->1280", 8, 2560, 1280)]:
+        if CONV:
+            x, w = rnd(imgs * hw * hw, ci), rnd(co, 9 * ci, std=(9 * ci) ** -0.5)
+            out = torch.empty(imgs * hw * hw, co, device="cuda", dtype=torch.bfloat16)
+            fns.append((f"{name} M={imgs*hw*hw}", lambda x=x, w=w, out=out, hw=hw: ops.conv3x3(x, imgs, hw, hw, w, out=out)))
     for name, M, N, K, res, geglu in cases:
+        if not DENSE:
+            continue
         a, w = rnd(M, K), rnd(N, K, std=K ** -0.5)
         b = torch.zeros(N, device="cuda")
         r = rnd(M, N) if res else None
@@ -63,5 +73,8 @@ def run(imgs):
         print(f"[{imgs:2d} img] {name:36s} {row}", flush=True)
 
 
+import os  # noqa: E402
+CONV = os.environ.get("SWEEP", "dense,conv").find("conv") >= 0
+DENSE = os.environ.get("SWEEP", "dense,conv").find("dense") >= 0
 for imgs in [int(x) for x in sys.argv[1:]] or [32, 4]:
     run(imgs)
