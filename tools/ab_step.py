@@ -6,7 +6,8 @@ variance is ~3 %): python tools/ab_step.py MODE [frames] — alternates two capt
   mq   motion-module Q/K/V projection fused into the temporal attention (L1) vs GEMM + attention
   pf   v2/v6 GEMM fragment-read order: the default vs round 1's, k-step-pipelined and all-ahead
        (vd_gemm_select_path 0 / 12 / 13 / 14)
-  v3e  v3 GEMM with the LDS-bias load-free epilogue vs gemm_epilogue (vd_gemm_select_path 0 vs 15)"""
+  v3e  v3 GEMM with the LDS-bias load-free epilogue vs gemm_epilogue (vd_gemm_select_path 0 vs 15)
+  roll v5 GEMM with the rolling W-fragment window vs round 1's halves (vd_gemm_select_path 0 vs 16)"""
 import sys
 import time
 from pathlib import Path
@@ -64,6 +65,12 @@ elif mode == "pf":
 elif mode == "v3e":
     from vdiff._lib import lib
     for name, path in (("v3-lds-bias", 0), ("v3-gemm-epi", 15)):
+        lib().vd_gemm_select_path(path)
+        loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
+    lib().vd_gemm_select_path(0)
+elif mode == "roll":
+    from vdiff._lib import lib
+    for name, path in (("v5-rolling-w", 0), ("v5-w-halves", 16)):
         lib().vd_gemm_select_path(path)
         loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
     lib().vd_gemm_select_path(0)

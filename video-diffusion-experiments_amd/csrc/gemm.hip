@@ -376,6 +376,7 @@ int g_num_cus = 256;  // MI355X; refreshed from the device on first use
 // k-step 0's reads ahead, k-step 1's interleaved with k-step 0's MFMAs (tools/ab_step.py pf:
 // 52.79 vs 53.50 ms/step for round 1's order, 53.11 all-ahead; profiles/r02f_fragment_order.txt)
 int g_g2_pf = -1;
+int g_g4_roll = 1;  // v5 W-fragment rolling window (0: round 1's halves, vd_gemm_select_path(16), A/B)
 int g_g2_old = 0;     // 1: v6 with the round-1 fragment-read order (vd_gemm_select_path(12))
 constexpr uint32_t G2_OOB = 0x80000000u;
 
@@ -1194,7 +1195,7 @@ __device__ __forceinline__ void epi_ln(const vd_gemm_desc& d, f32x4 (&acc)[NB][M
   }
 }
 
-template <int BN, int WM, int WN, int STAGES, int MODE, bool LN = false>
+template <int BN, int WM, int WN, int STAGES, int MODE, bool LN = false, bool ROLL = true>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_waves_per_eu(2))) void gemm4_kernel(
     const vd_gemm_desc d, uint32_t a0_bytes, uint32_t a1_bytes, uint32_t w_bytes, int split) {
   using C = G4<BN, WM, WN, STAGES>;
@@ -1392,6 +1393,30 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
 #pragma unroll
           for (int a = 0; a < C::NB; ++a)
             acc[a][4 * h + b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][4 * h + b], 0, 0, 0);
+      }
+    } else if constexpr (ROLL) {
+      // X once; W fragments two ahead in a rolling window (round 2): each W read issues under the
+      // MFMAs of the fragment two before it, pinned by sched_group_barrier — the halves below let
+      // hipcc wait lgkmcnt on every pair right before its MFMAs
+      bf16x8 xf[C::MB];
+#pragma unroll
+      for (int b = 0; b < C::MB; ++b) xf[b] = *(const bf16x8*)(sbase + xlane + b * 1024);
+      bf16x8 w0 = *(const bf16x8*)(sbase + wlane), w1 = *(const bf16x8*)(sbase + wlane + 1024);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int a = 0; a < C::NB; ++a) {
+        bf16x8 wn = w1;
+        if (a + 2 < C::NB) wn = *(const bf16x8*)(sbase + wlane + (a + 2) * 1024);
+#pragma unroll
+        for (int b = 0; b < C::MB; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, xf[b], acc[a][b], 0, 0, 0);
+        w0 = w1;
+        w1 = wn;
+      }
+#pragma unroll
+      for (int a = 0; a < C::NB; ++a) {
+        if (a + 2 < C::NB) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, C::MB, 0);
       }
     } else {
       // X once, W in two halves
@@ -1825,12 +1850,18 @@ int launch4(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   if (d.a_mode == VD_A_CONV3X3)
     hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_CONV3X3>), dim3((unsigned)grid), dim3(C::NT), 0,
                        s, d, a0b, a1b, wb, split);
-  else if (d.ln_out)  // plan() only lets a fusable descriptor keep ln_out
+  else if (d.ln_out && g_g4_roll)  // plan() only lets a fusable descriptor keep ln_out
     hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_DENSE, true>), dim3((unsigned)grid), dim3(C::NT), 0,
                        s, d, a0b, a1b, wb, split);
-  else
+  else if (d.ln_out)
+    hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_DENSE, true, false>), dim3((unsigned)grid),
+                       dim3(C::NT), 0, s, d, a0b, a1b, wb, split);
+  else if (g_g4_roll)
     hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_DENSE>), dim3((unsigned)grid), dim3(C::NT), 0, s,
                        d, a0b, a1b, wb, split);
+  else
+    hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_DENSE, false, false>), dim3((unsigned)grid),
+                       dim3(C::NT), 0, s, d, a0b, a1b, wb, split);
   int rc = vd_launch_status();
   if (rc != VD_OK || split == 1) return rc;
   const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
@@ -2080,7 +2111,9 @@ extern "C" int vd_gemm_force_v1(int32_t on) {
   return VD_OK;
 }
 extern "C" int vd_gemm_select_path(int32_t path) {
-  if (path < 0 || path > 15 || path == 4) return VD_EINVAL;
+  if (path < 0 || path > 16 || path == 4) return VD_EINVAL;
+  g_g4_roll = path != 16;
+  if (path == 16) path = 0;  // auto plan, v5 with round 1's fragment halves (A/B)
   g_g3_fast = path != 15;
   if (path == 15) path = 0;  // auto plan, v3 with gemm_epilogue (A/B)
   g_g2_old = path == 12;
