@@ -188,14 +188,26 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
     for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
       for (int qb = 0; qb < QBLK; ++qb) s[kb][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    {  // K fragments two ahead in a rolling window (round 2): hipcc otherwise read each one right
+       // before its QBLK MFMAs behind an lgkmcnt(0) — an exposed LDS latency per fragment
+      constexpr int NK = C::DQK / 32 * 4;  // fragment i = (dc, kb) = (i / 4, i % 4)
+      auto kfrag = [&](int i) { return *(const bf16x8*)(kl + ((i % 4) * 16 + fr) * C::KS + (i / 4) * 32 + 8 * fg); };
+      bf16x8 k0 = kfrag(0), k1 = kfrag(1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int dc = 0; dc < C::DQK / 32; ++dc) {
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) {
-        const bf16x8 kf = *(const bf16x8*)(kl + (kb * 16 + fr) * C::KS + dc * 32 + 8 * fg);
+      for (int i = 0; i < NK; ++i) {
+        bf16x8 kn = k1;
+        if (i + 2 < NK) kn = kfrag(i + 2);
 #pragma unroll
         for (int qb = 0; qb < QBLK; ++qb)
-          s[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qb][dc], s[kb][qb], 0, 0, 0);
+          s[i % 4][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[qb][i / 4], s[i % 4][qb], 0, 0, 0);
+        k0 = k1;
+        k1 = kn;
+      }
+#pragma unroll
+      for (int i = 0; i < NK; ++i) {
+        if (i + 2 < NK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, QBLK, 0);
       }
     }
     if (ragged && t == ntiles - 1) {  // only the last tile of a ragged key range is masked
@@ -255,19 +267,31 @@ __global__ __launch_bounds__(NT, 2) void flash_attn_kernel(
           for (int j = 0; j < 4; ++j) oacc[a][qb][j] *= alpha[qb];
     }
     // ---- O^T += V^T . P^T
+    {  // V^T fragments two ahead in a rolling window, as K above (fragment j = (a, st) = (j / 2, j % 2))
+      constexpr int NV = C::DV / 16 * 2;
+      auto vfrag = [&](int j) {
+        const bf16_t* p0 = vl + (32 * (j % 2) + 4 * fg + qq) * C::VS + (j / 2) * 16 + 4 * pp;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(p0));
+        const bf16x4 hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(p0 + 16 * C::VS));
+        return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      };
+      bf16x8 v0 = vfrag(0), v1 = vfrag(1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int a = 0; a < C::DV / 16; ++a) {
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16_t* p0 = vl + (32 * st + 4 * fg + qq) * C::VS + a * 16 + 4 * pp;
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (bf16x4 __attribute__((address_space(3)))*)(p0));
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (bf16x4 __attribute__((address_space(3)))*)(p0 + 16 * C::VS));
-        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      for (int j = 0; j < NV; ++j) {
+        bf16x8 vn = v1;
+        if (j + 2 < NV) vn = vfrag(j + 2);
 #pragma unroll
         for (int qb = 0; qb < QBLK; ++qb)
-          oacc[a][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[st][qb], oacc[a][qb], 0, 0, 0);
+          oacc[j / 2][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v0, pf[j % 2][qb], oacc[j / 2][qb], 0, 0, 0);
+        v0 = v1;
+        v1 = vn;
+      }
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        if (j + 2 < NV) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, QBLK, 0);
       }
     }
     if (t + 1 < ntiles) kv_store<C::LREG>(kvst, ks_lds[buf ^ 1], vs_lds[buf ^ 1], ldsk, ldsv);
