@@ -1657,37 +1657,44 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
     gemm_epilogue<MB, NB>(d, acc, mbase, nbase, lane);
     return;
   }
-  // ---- split K: slab, arrival counter, last arriver reduces
+  // ---- split K: slab, arrival counter, last arriver reduces.  Round 2: the hand-off is the
+  // guide's fence-free form (cdna_hip_programming.md Guideline 16, R1 / "sc1 slab stores"): every
+  // slab store is write-through (sc1), every storing wave drains it (vmcnt(0)) before the
+  // workgroup barrier, ONE lane adds to the tile's counter (relaxed, agent scope), and the last
+  // arriver reads every slab with sc1 loads (past this CU's L1), so neither side needs an
+  // agent-scope fence — the release fence of round 1 wrote back the XCD's whole L2 (~25 us).
   float* slabs = (float*)d.ws;
-  float* slab = slabs + (int64_t)sp * M * N;
+  const __amdgpu_buffer_rsrc_t rws =
+      __builtin_amdgcn_make_buffer_rsrc(d.ws, 0, (uint32_t)((int64_t)split * M * N * 4), 0x00020000);
 #pragma unroll
   for (int a = 0; a < NB; ++a) {
     const int64_t n = nbase + a * 16 + 4 * fq;
-    if (n >= N) continue;
 #pragma unroll
     for (int b = 0; b < MB; ++b) {
       const int64_t m = mbase + b * 16 + fr;
-      if (m < M) *(float4*)(slab + m * N + n) = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+      const uint32_t off = (n < N && m < M) ? (uint32_t)((((int64_t)sp * M + m) * N + n) * 4) : G2_OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u32x4{__float_as_uint(acc[a][b][0]), __float_as_uint(acc[a][b][1]), __float_as_uint(acc[a][b][2]),
+                __float_as_uint(acc[a][b][3])},
+          rws, off, 0, 16);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
   int* cnt = (int*)(slabs + (int64_t)split * M * N);
   int* last_flag = (int*)(smem + G6_S * G6_STAGE);
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int prev = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = prev == split - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      cnt[tile] = 0;  // ready for the next launch (the memset node zeroes it as well)
-    }
+    if (last) __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the memset node zeroes it too
     *last_flag = last;
   }
   __syncthreads();
   if (!*last_flag) return;
+  auto slab4 = [&](int s2, int64_t m, int64_t n) {  // sc1 load of 4 slab floats
+    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rws, (uint32_t)((((int64_t)s2 * M + m) * N + n) * 4), 0, 16);
+    return make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3]));
+  };
   // 64 x 64 outputs (GEGLU: 64 x 32), 4 consecutive columns per thread-step
   const bool geglu = d.act == VD_ACT_GEGLU;
   const int ncol = geglu ? G6_BN / 2 : G6_BN;
@@ -1702,8 +1709,8 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
       if (ng >= N) continue;
       float h[4] = {0, 0, 0, 0}, g[4] = {0, 0, 0, 0};
       for (int s2 = 0; s2 < split; ++s2) {
-        const float4 a4 = *(const float4*)(slabs + ((int64_t)s2 * M + m) * N + nh);
-        const float4 b4 = *(const float4*)(slabs + ((int64_t)s2 * M + m) * N + ng);
+        const float4 a4 = slab4(s2, m, nh);
+        const float4 b4 = slab4(s2, m, ng);
         h[0] += a4.x; h[1] += a4.y; h[2] += a4.z; h[3] += a4.w;
         g[0] += b4.x; g[1] += b4.y; g[2] += b4.z; g[3] += b4.w;
       }
@@ -1721,7 +1728,7 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
     if (o >= N) continue;
     float v[4] = {0, 0, 0, 0};
     for (int s2 = 0; s2 < split; ++s2) {
-      const float4 a4 = *(const float4*)(slabs + ((int64_t)s2 * M + m) * N + o);
+      const float4 a4 = slab4(s2, m, o);
       v[0] += a4.x; v[1] += a4.y; v[2] += a4.z; v[3] += a4.w;
     }
     if (d.bias) {
