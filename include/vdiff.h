@@ -117,7 +117,12 @@ int vd_gemm_force_v1(int32_t on);
  * 2 = v2 (256 x {128,160} persistent LDS-DMA), 3 = v3 (256 x 256 8-phase, dense A only;
  * shapes it cannot take fall back to the automatic choice), 5 = v5 (256 x 320, BK 32,
  * 4-stage ring, load-free epilogue), 6 = v6 (64 x 64, in-kernel split-K reduction), 7 = the
- * automatic choice without v6. */
+ * automatic choice without v6, 8 = v6 unsplit, 9 = automatic with split-K cap 8, 10 = v3 one
+ * unit per workgroup, 11 = automatic with that v3; A/B hooks of round-2 kernel changes, each the
+ * automatic plan with one change undone: 12 = v2 / v6 fragment reads in round 1's order,
+ * 13 / 14 = v2 fragment reads pipelined (the default) / all ahead, 15 = v3 with gemm_epilogue
+ * instead of the LDS-bias epilogue, 16 = v5 W fragments in halves instead of the rolling window.
+ * Every path computes the same arithmetic (the K order of each output is fixed). */
 int vd_gemm_select_path(int32_t path);
 
 /* ---------------------------------------------------------------- GroupNorm
