@@ -135,6 +135,14 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
         bv[0] = t0.x; bv[1] = t0.y; bv[2] = t0.z; bv[3] = t0.w;
         bv[4] = t1.x; bv[5] = t1.y; bv[6] = t1.z; bv[7] = t1.w;
       }
+      uint4 rsv[MB];  // residual rows loaded together ahead of the stores (as epi_ln, round 2)
+      if (d.res) {
+#pragma unroll
+        for (int b = 0; b < MB; ++b) {
+          VD_EPI_ROW(b)
+          rsv[b] = *(const uint4*)((const bf16_t*)d.res + (uint32_t)(mrow_ * (int)d.ld_res + nn));
+        }
+      }
 #pragma unroll
       for (int b = 0; b < MB; ++b) {
         VD_EPI_ROW(b)
@@ -159,7 +167,7 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
         }
         if (d.res) {
           float rf[8];
-          unpack8(*(const uint4*)((const bf16_t*)d.res + (uint32_t)(mrow_ * (int)d.ld_res + n)), rf);
+          unpack8(rsv[b], rf);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += rf[j];
         }
