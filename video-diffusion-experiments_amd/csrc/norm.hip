@@ -389,10 +389,13 @@ __global__ __launch_bounds__(NT) void layernorm_kernel(const bf16_t* x, int64_t 
 // C = 320 and has one 16-byte load per lane outstanding).  Row sums by xor shuffles inside
 // each LPR-lane group; lane l of a group holds chunks l, l + LPR, ... (coalesced rows).
 template <int LPR, int CH>
+// gamma / beta / pe are __restrict__ (read-only tables no store of this kernel touches), so
+// hipcc may issue the next chunk's loads ahead of this chunk's y store (round 2)
 __global__ __launch_bounds__(NT) void layernorm_rows_kernel(const bf16_t* x, int64_t ldx, int64_t rows,
-                                                            const float* gamma, const float* beta, float eps,
-                                                            const float* pe, int64_t pe_div, int64_t pe_period,
-                                                            bf16_t* y, int64_t ldy) {
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float eps,
+                                                            const float* __restrict__ pe, int64_t pe_div,
+                                                            int64_t pe_period, bf16_t* y, int64_t ldy) {
   constexpr int C = 8 * LPR * CH, RPW = 64 / LPR;
   const int lane = threadIdx.x & 63, sub = lane % LPR;
   const int64_t row = ((int64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6)) * RPW + lane / LPR;
@@ -401,6 +404,17 @@ __global__ __launch_bounds__(NT) void layernorm_rows_kernel(const bf16_t* x, int
   uint4 u[CH];
 #pragma unroll
   for (int q = 0; q < CH; ++q) u[q] = *(const uint4*)(x + rr * ldx + (sub + q * LPR) * 8);
+  // gamma / beta of every chunk issue right behind x (they do not depend on it), so their L2
+  // latency hides under the x loads and the two reductions (round 2)
+  float4 gv[CH][2], bvv[CH][2];
+#pragma unroll
+  for (int q = 0; q < CH; ++q) {
+    const int j = sub + q * LPR;
+    gv[q][0] = *(const float4*)(gamma + j * 8);
+    gv[q][1] = *(const float4*)(gamma + j * 8 + 4);
+    bvv[q][0] = *(const float4*)(beta + j * 8);
+    bvv[q][1] = *(const float4*)(beta + j * 8 + 4);
+  }
   float v[CH][8];
   float s = 0.f;
 #pragma unroll
@@ -428,8 +442,8 @@ __global__ __launch_bounds__(NT) void layernorm_rows_kernel(const bf16_t* x, int
 #pragma unroll
   for (int q = 0; q < CH; ++q) {
     const int j = sub + q * LPR;
-    const float4 g0 = *(const float4*)(gamma + j * 8), g1 = *(const float4*)(gamma + j * 8 + 4);
-    const float4 b0 = *(const float4*)(beta + j * 8), b1 = *(const float4*)(beta + j * 8 + 4);
+    const float4 g0 = gv[q][0], g1 = gv[q][1];
+    const float4 b0 = bvv[q][0], b1 = bvv[q][1];
     const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
     const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
     float o[8];
