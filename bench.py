@@ -91,28 +91,51 @@ def time_attention(n_img, reps, stream, stress=False):
             "algorithmic_bytes_per_launch": byts}
 
 
+ROOF_SOURCES = ("video-diffusion-experiments_amd/csrc/attention.hip", "video-diffusion-experiments_amd/csrc/common.h")
+
+
+def roof_src_hash() -> str:
+    """sha256[:16] of the roofline kernel's sources: the PMC summaries under profiles/ record the
+    hash of the tree they were measured on, and bench.py uses only a summary whose hash equals
+    the current tree's (tools/roofline_prof.sh writes them)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ROOF_SOURCES:
+        h.update(f.encode() + b"\0" + (ROOT / f).read_bytes() + b"\0")
+    return h.hexdigest()[:16]
+
+
+def _pmc_file(pattern):
+    """The committed PMC summary (profiles/<pattern>) measured on THIS tree's roofline kernel
+    sources (its kernel_src_hash), newest round first; (None, None) when there is none."""
+    want = roof_src_hash()
+    for f in sorted((ROOT / "profiles").glob(pattern), reverse=True):
+        try:
+            t = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        if t.get("kernel_src_hash") == want:
+            return t, f.name
+    return None, None
+
+
 def pmc_traffic(n_img):
-    """HBM bytes per launch of the roofline kernel from the newest committed PMC
-    summary (profiles/rNN_traffic.json, written by tools/traffic.sh from separate
-    FETCH_SIZE / WRITE_SIZE rocprofv3 passes over the same kernel at 32 images;
-    scaled linearly to this rank's image count).  None when absent."""
-    files = sorted((ROOT / "profiles").glob("r*_traffic.json"))
-    if not files:
+    """HBM bytes per launch of the roofline kernel from the committed PMC summary measured on
+    this tree (profiles/rNN_traffic.json: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over
+    `bench.py --roofline-only` at 32 images, corrected as MI355X_MICROARCH.md §HBM prescribes;
+    scaled linearly to this rank's image count).  None when no summary matches the sources."""
+    t, name = _pmc_file("r*_traffic.json")
+    if t is None or "flash32_kernel<40" not in (t.get("kernel") or ""):
         return None, None
-    t = json.loads(files[-1].read_text())
-    if "flash32_kernel<40" not in (t.get("kernel") or ""):
-        return None, None
-    return t["traffic_bytes_per_launch"] * n_img / 32.0, files[-1].name
+    return t["traffic_bytes_per_launch"] * n_img / 32.0, name
 
 
 def pmc_mfma_busy():
     """MFMA-busy share of the roofline kernel (SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x
-    GRBM_GUI_ACTIVE/8) from the newest committed profiles/rNN_mfma_busy.json (tools/mfma_busy.sh:
-    one PMC pass over a bench.py run).  Counts padded MFMA work, unlike `frac`."""
-    files = sorted((ROOT / "profiles").glob("r*_mfma_busy.json"))
-    if not files:
-        return None, None
-    return json.loads(files[-1].read_text()).get("mfma_busy_frac"), files[-1].name
+    GRBM_GUI_ACTIVE/8) from the committed profiles/rNN_mfma_busy.json measured on this tree.
+    Counts padded MFMA work, unlike `frac`."""
+    t, name = _pmc_file("r*_mfma_busy.json")
+    return (t.get("mfma_busy_frac"), name) if t else (None, None)
 
 
 def cpu_baseline(unet_gpu, cfg_name, frames_sample, frames_full):
@@ -154,6 +177,9 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--attn-reps", type=int, default=20)
     ap.add_argument("--no-nocfg", action="store_true", help="skip the B=1 (no-CFG) variant")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the roofline kernel's timing (the same time_attention call as the bench line; "
+                         "tools/roofline_prof.sh runs its PMC passes over this)")
     ap.add_argument("--overlap", type=int, default=1,
                     help="N>1: chunk each motion module's all-to-alls over positions and overlap them with "
                          "the transformer block on a second stream (vdiff.dist.FrameShard overlap_chunks)")
@@ -168,6 +194,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
+    if args.roofline_only:
+        imgs = 2 * (args.frames or 16)
+        roof = time_attention(imgs, args.attn_reps, torch.cuda.current_stream())
+        roof["kernel_src_hash"] = roof_src_hash()
+        print(json.dumps({"roofline": roof}), flush=True)
+        return
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
@@ -258,6 +290,7 @@ def main():
                       "(exp2 argument std ~3.2); `stress`: the scale not folded (std ~14)")
     roof["traffic"], roof["traffic_source"] = pmc_traffic(imgs)
     roof["mfma_busy"], roof["mfma_busy_source"] = pmc_mfma_busy()
+    roof["kernel_src_hash"] = roof_src_hash()
     step_tf = STEP_TFLOP[cfg_name] * (frames / (16 if cfg_name == "full" else 4)) / (ms * 1e-3) / world
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -45,6 +45,9 @@ int vd_version(void);  /* 3 */
 /* Content hash (16 hex digits) of the sources and compile flags the library was built from
  * (video-diffusion-experiments_amd/build_ext.py); the Python loader compares it with the tree. */
 const char* vd_build_hash(void);
+/* The --offload-arch the library's code objects were compiled for ("gfx950" unless the build
+ * set VDIFF_ARCH); not part of the content hash above. */
+const char* vd_build_arch(void);
 
 /* ---------------------------------------------------------------- GEMM / conv
  * out[m, n] = epi( sum_k A[m, k] * W[n, k] )          (bf16 MFMA, fp32 accumulate)

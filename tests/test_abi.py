@@ -31,6 +31,8 @@ def test_library_loads_and_exports_every_symbol():
     from vdiff._srchash import source_hash
     import build_ext
     assert h.vd_build_hash().decode() == source_hash(build_ext.HASH_FLAGS)  # a build of THIS tree
+    assert h.vd_build_arch().decode() == build_ext.ARCH
+    assert not any(f.startswith("--offload-arch") for f in build_ext.HASH_FLAGS)  # arch-independent hash
     assert h.vd_strerror(1000).decode().startswith("vdiff: invalid argument")
     out = subprocess.run(["nm", "-D", "--defined-only", str(L.LIB_PATH)], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (vd_\w+)", out))

@@ -720,6 +720,39 @@ def test_attention_fp32_out_north_star_tolerance(attn_path, d, sq, skv, batch, k
     assert torch.all(err <= 1e-4 + 1e-3 * want.abs()), err.max().item()
 
 
+@pytest.mark.parametrize("sq,skv,batch", [(4096, 4096, 2), (1000, 333, 2), (300, 77, 3)])
+def test_attention_d40_real_valued_north_star_tolerance(cuda, sq, skv, batch):
+    """The roofline kernel (flash32, d = 40, the model's unit scale) on REAL-valued inputs as the
+    model produces them (q, k, v ~ N(0, 1.5^2), softmax scale * log2 e folded into q), fp32
+    output, at the north star's rtol 1e-3 / atol 1e-4 against an fp64 reference that rounds P
+    to bf16 exactly where the kernel does: P = bf16(2^(s - mu)) with mu = bf16(max of the
+    row's scores over the first 64-key tile) (the fast pass's running offset; its 2^32 row-sum
+    rescale is not reached at this logit range, asserted below), O = (P V) / sum(P), the sum
+    taken over the same bf16 P.  Printed beside it: the distance to exact fp64 softmax, i.e.
+    what the bf16 P rounding itself costs."""
+    torch.manual_seed(sq + skv)
+    heads, d = 2, 40
+    C = heads * d
+    q = bf(torch.randn(batch * sq, C, device="cuda") * 1.5 * d ** -0.5 * math.log2(math.e))
+    k = bf(torch.randn(batch * skv, C, device="cuda") * 1.5)
+    v = bf(torch.randn(batch * skv, C, device="cuda") * 1.5)
+    got = ops.attention(q, k, v, batch, heads, sq, skv, d, scale=1.0 / math.log2(math.e), out_f32=True)
+    qd = q.double().reshape(batch, sq, heads, d).transpose(1, 2)
+    kd = k.double().reshape(batch, skv, heads, d).transpose(1, 2)
+    vd = v.double().reshape(batch, skv, heads, d).transpose(1, 2)
+    s = qd @ kd.transpose(-1, -2)                                     # log2 units
+    mu = s[..., :64].amax(-1, keepdim=True).float().to(torch.bfloat16).double()
+    assert (torch.exp2(s - mu).sum(-1) < 2.0 ** 32).all()             # no fast-pass rescale
+    p = torch.exp2(s - mu).float().to(torch.bfloat16).double()
+    want = ((p @ vd) / p.sum(-1, keepdim=True)).transpose(1, 2).reshape(batch * sq, C)
+    pe = torch.exp2(s - s.amax(-1, keepdim=True))
+    exact = ((pe @ vd) / pe.sum(-1, keepdim=True)).transpose(1, 2).reshape(batch * sq, C)
+    err = (got.double() - want).abs()
+    print(f"d=40 real-valued sq={sq} skv={skv}: max|O - O_ref(bf16 P)| {err.max().item():.2e}, "
+          f"max|O - O_fp64 exact| {(got.double() - exact).abs().max().item():.2e}")
+    assert torch.all(err <= 1e-4 + 1e-3 * want.abs()), err.max().item()
+
+
 @pytest.fixture(params=["mfma", "valu"])
 def temporal_path(request, cuda):
     """frames <= 16 with d in {40, 80, 160} run on the MFMA kernel unless forced to VALU."""

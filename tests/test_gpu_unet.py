@@ -7,11 +7,13 @@ test alone cannot see them (with std 0.02 weights cond and uncond eps differ by
 only 0.24%, below the bf16 storage noise of the network).
 
 Tolerance: the device path stores bf16 activations; the whole tiny UNet is
-compared by relative L2 error against the fp32 oracle with a bound of 3% (the
+compared by relative L2 error against the fp32 oracle with a bound of 1.8% (the
 oracle itself with the device's bf16 storage emulated lands at 1.4%, committed in
 tests/golden/tiny_unet.npz) and against that device-emulating oracle (act="dev":
 bf16 at every store, the kernels' folded softmax scale and bf16 probabilities) at
-0.5%; module tests use 2.5% rel-L2 (a few bf16 roundings in sequence).
+1.8% (both measured 1.33-1.38% at t in {961, 500, 1}); the tight check is per block against
+the device-emulating oracle at 0.25% (test_tiny_blocks_match_device_emulation).  Module tests
+use 2.5% rel-L2 (a few bf16 roundings in sequence).
 """
 import sys
 from pathlib import Path
@@ -137,8 +139,8 @@ def test_tiny_unet_matches_oracle(tiny_unet, gold, t):
           f"{r_dev:.5f} max|err|/max|want| {m_dev:.5f}")
     # end to end both oracles sit at the bf16 realisation floor (~1.3 %, test_oracle.py::
     # test_bf16_realisation_floor); the tight bound is per block, test_tiny_blocks_match_...
-    assert err < 0.03, err
-    assert r_dev < 0.03, r_dev
+    assert err < 0.018, err      # measured 0.0137-0.0138 (1.3x headroom)
+    assert r_dev < 0.018, r_dev  # measured 0.0133-0.0134
 
 
 def test_tiny_blocks_match_device_emulation(tiny_unet, gold):
@@ -234,8 +236,7 @@ def test_full_unet_two_frames_matches_oracle(cuda):
     """The FULL SD-1.5 + motion-adapter shapes (1.31B params; every level L1-L4, d = 40/80/160
     attention, the v2/v3/v5/v6 GEMM paths at their real shapes, split-K, concat skips) on a
     2-frame CFG batch at t = 500, against the fp32 oracle on the same bf16 weights
-    (~10 s of host CPU).  Bound: rel-L2 3 %, as for the tiny model (measured 1.64 % on the
-    MI355X; the value is printed)."""
+    (~10 s of host CPU).  Bound: rel-L2 2 % (measured 1.62 % on the MI355X; the value is printed)."""
     from vdiff.weights import materialize_synthetic
     torch.manual_seed(0)
     unet = materialize_synthetic("full", device="cuda", seed=0)
@@ -252,7 +253,7 @@ def test_full_unet_two_frames_matches_oracle(cuda):
         want = unet_ref.unet_forward(sd, unet_ref_cfg("full"), x, 500, ehs)
     err = rel_l2(got, want)
     print(f"full UNet (2 frames) rel-L2 vs oracle: {err:.4f}")
-    assert err < 0.03, err
+    assert err < 0.02, err
 
 
 def unet_ref_cfg(name):
@@ -270,7 +271,8 @@ def test_full_unet_sixteen_frames_matches_oracle(cuda):
     weights, as the committed fixture tests/golden/full_f16_t500.npz) on all 16 frames — every
     motion module attends over F = 16 — at t = 500, against the fp32 oracle and the oracle that
     emulates the device's bf16 storage and attention arithmetic (act="dev").  Printed: rel-L2
-    and max|err|/max|want| against both.  Bounds: 3 % rel-L2 against either — end to end any
+    and max|err|/max|want| against both.  Bounds: 2 % rel-L2 against the fp32 oracle (measured
+    1.48 %) and 2.2 % against the device-emulating one (measured 1.76 %) — end to end any
     two bf16 realisations of the network sit ~1.3-1.5 % apart (the fixture's own dev-vs-fp32
     is 1.48 %; test_oracle.py::test_bf16_realisation_floor), so the tight check is per block
     (test_tiny_blocks_match_device_emulation)."""
@@ -287,5 +289,5 @@ def test_full_unet_sixteen_frames_matches_oracle(cuda):
     rdv, mdv = _errs(got, torch.from_numpy(gold["eps_dev"]))
     print(f"full UNet F=16 t={T}: vs fp32 oracle rel-L2 {r32:.5f} max {m32:.5f}; "
           f"vs device-emulating oracle rel-L2 {rdv:.5f} max {mdv:.5f}")
-    assert r32 < 0.03, r32
-    assert rdv < 0.03, rdv
+    assert r32 < 0.02, r32
+    assert rdv < 0.022, rdv

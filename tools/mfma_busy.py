@@ -7,7 +7,11 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import roof_src_hash  # noqa: E402
 
 SETUP = ("at::native", "__amd_rocclr")  # weight init / copies outside the denoising step
 disp = collections.defaultdict(dict)
@@ -38,5 +42,6 @@ print(f"{'ALL (model kernels)':36s} {sum(n[f] for f in step):10d} {100.0:9.1f}% 
 key = "flash32<40,unit-c> L1 self-attn"
 if len(sys.argv) > 2 and act[key]:
     json.dump({"kernel": "flash32_kernel<40, true> (L1 spatial self-attention)", "mfma_busy_frac": round(share(key), 4),
-               "dispatches": n[key], "counters": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 x GRBM_GUI_ACTIVE / 8)"},
+               "dispatches": n[key], "counters": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 x GRBM_GUI_ACTIVE / 8)",
+               "kernel_src_hash": roof_src_hash()},
               open(sys.argv[2], "w"), indent=1)

@@ -11,7 +11,11 @@ doubled; WRITE_SIZE is taken as is.  bench.py reads the resulting JSON as the
 import csv
 import glob
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import roof_src_hash  # noqa: E402
 
 d, sub, out = sys.argv[1], sys.argv[2], sys.argv[3]
 note = sys.argv[4] if len(sys.argv) > 4 else ""
@@ -28,6 +32,7 @@ fetch = 2 * 1024 * sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
 write = 1024 * sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
 res = {"kernel": name, "match": sub, "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
        "traffic_bytes_per_launch": fetch + write, "launches": len(vals["FETCH_SIZE"]),
-       "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024", "note": note}
+       "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024", "note": note,
+       "kernel_src_hash": roof_src_hash()}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))

@@ -38,6 +38,13 @@ for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:40]:
     print(f"  {sum(v) / steps / 1e3:9.1f} us  x{len(v) / steps:5.1f}  avg {sum(v) / len(v) / 1e3:8.1f} us  "
           f"{k[0]} grid={k[1]} wg={k[2]}")
 
+# the same kernel inside the step (the L1 spatial self-attention: flash32<40, unit-c> launches
+# longer than 300 us; the shorter ones are its text cross-attention)
+ins = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win if "flash32_kernel<40, true" in r["Kernel_Name"]]
+ins = [x for x in ins if x > 300e3]
+if ins:
+    print(f"roofline kernel inside the step (L1 self-attention): {len(ins)} launches, avg {sum(ins) / len(ins) / 1e3:.1f} us")
+
 # bench.py's roofline kernel: after the last step, time_attention() launches the L1
 # self-attention kernel (10 warm-up + attn_reps timed) on its own, first on model-scale inputs
 # (the bench line's roofline.avg_launch_ms), then on the stress inputs (roofline.stress);

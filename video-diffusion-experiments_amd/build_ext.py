@@ -35,8 +35,10 @@ CFLAGS = [
     "-Wno-unused-result",
     f"-I{INCLUDE}",
 ]
-# the flags that enter the content hash (no absolute paths: the tree moves between machines)
-HASH_FLAGS = [f for f in CFLAGS if not f.startswith("-I")]
+# the flags that enter the content hash: no absolute paths (the tree moves between machines)
+# and no --offload-arch (a library built for another arch is the same sources; the arch is
+# compiled in separately as vd_build_arch(), so a loader without VDIFF_ARCH set still accepts it)
+HASH_FLAGS = [f for f in CFLAGS if not f.startswith("-I") and not f.startswith("--offload-arch")]
 
 
 def _compile(src: Path, defs, verbose: bool) -> Path:
@@ -57,7 +59,7 @@ def build(verbose: bool = True, jobs: int = 8, clean: bool = False) -> Path:
         return LIB
     shutil.rmtree(BUILD, ignore_errors=True)
     BUILD.mkdir()
-    defs = [f'-DVD_BUILD_HASH="{h}"']
+    defs = [f'-DVD_BUILD_HASH="{h}"', f'-DVD_BUILD_ARCH="{ARCH}"']
     srcs = sorted(CSRC.glob("*.hip"))
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, defs, verbose), srcs))

@@ -260,3 +260,9 @@ extern "C" int vd_version(void) { return 3; }  // 3: vd_gemm_desc grew the ln_* 
 // Content hash of the sources + flags this library was built from (build_ext.py);
 // vdiff._lib refuses to load a library whose hash differs from the tree's sources.
 extern "C" const char* vd_build_hash(void) { return VD_BUILD_HASH; }
+
+#ifndef VD_BUILD_ARCH
+#define VD_BUILD_ARCH "gfx950"
+#endif
+// The --offload-arch the library was compiled for (kept out of the content hash).
+extern "C" const char* vd_build_arch(void) { return VD_BUILD_ARCH; }

@@ -8,6 +8,7 @@ from .config import FULL, TINY, get_config  # noqa: F401
 from .models import UNetMotionModel, UNetMotionOutput  # noqa: F401
 from .models.dit import DiT3DModel, DiTDenoiseLoop, DiTOutput  # noqa: F401
 from .models.vae import AutoencoderKL, DecoderOutput  # noqa: F401
+from .pretrained import MotionAdapter  # noqa: F401
 from .pipeline import AnimateDiffPipeline, AnimateDiffPipelineOutput, DenoiseLoop  # noqa: F401
 from .sched import (DDIMScheduler, DDIMSchedulerOutput, EulerDiscreteScheduler,  # noqa: F401
                     EulerDiscreteSchedulerOutput)

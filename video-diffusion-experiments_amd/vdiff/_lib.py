@@ -24,6 +24,7 @@ SIGNATURES = {
     "vd_strerror": ([c_i32], C.c_char_p),
     "vd_version": ([], c_i32),
     "vd_build_hash": ([], C.c_char_p),
+    "vd_build_arch": ([], C.c_char_p),
     "vd_gemm": ([c_vp, c_vp], c_i32),
     "vd_gemm_force_v1": ([c_i32], c_i32),
     "vd_gemm_select_path": ([c_i32], c_i32),

@@ -131,16 +131,29 @@ def video_metrics(sse, sad, n_values: int, lpips: Optional[Sequence[float]] = No
     return rec
 
 
-def measure_videos(videos_u8: torch.Tensor, lpips=None, flow: bool = True) -> list:
+FLOW_WORKSPACE_CAP = 2 << 30   # bytes of Farneback workspace per group of videos
+
+
+def measure_videos(videos_u8: torch.Tensor, lpips=None, flow: bool = True,
+                   workspace_cap: int = FLOW_WORKSPACE_CAP) -> list:
     """uint8 [V, F, H, W, 3] (GPU) -> one record per video (flow fields from the HIP Farneback
-    pipeline unless flow=False)."""
+    pipeline unless flow=False).  The flow pass runs over groups of videos whose workspace
+    (~112 B per pixel-frame) stays under `workspace_cap`, so the reference's 78-video grid does
+    not need ~37 GB at once; videos too short or small for Farneback (fewer than 2 frames,
+    H or W < 8) keep their flow fields None, as 06 leaves them when it has no pair."""
     sse, sad = frame_sums(videos_u8)
     sse, sad = sse.cpu().tolist(), sad.cpu().tolist()
     n = int(np.prod(videos_u8.shape[2:]))
     recs = [video_metrics(sse[v], sad[v], n, None if lpips is None else lpips[v]) for v in range(len(sse))]
-    if flow:
-        hw = int(videos_u8.shape[2] * videos_u8.shape[3])
-        st = flow_sums(videos_u8, farneback_flow(videos_u8)).cpu().tolist()
+    V, Fr, H, W = videos_u8.shape[:4]
+    if flow and Fr >= 2 and H >= 8 and W >= 8:
+        hw = int(H * W)
+        per_video = max(int(lib().vd_farneback_workspace(1, Fr, H, W)), 1)
+        group = max(1, min(V, workspace_cap // per_video))
+        st = []
+        for v0 in range(0, V, group):
+            part = videos_u8[v0:v0 + group]
+            st += flow_sums(part, farneback_flow(part)).cpu().tolist()
         for rec, s in zip(recs, st):
             ff = flow_fields(s, hw)
             for fm, pm in zip(rec["frame_metrics"], ff.pop("pairs")):

@@ -148,7 +148,13 @@ class UNetMotionModel(nn.Module):
     def forward_modules(self, sample, t, ehs):
         """diffusers UNetMotionModel.forward module by module: every block
         and leaf through __call__ with diffusers-layout tensors, all on the HIP kernels — the
-        path a forward-hook trace (experiments/03_trace_forward_pass.py:105-113) observes."""
+        path a forward-hook trace (experiments/03_trace_forward_pass.py:105-113) observes.
+        Unsharded only: its motion modules attend over the frames they are given, so under a
+        FrameShard they would see the rank's local frames alone."""
+        if getattr(self, "dist", None) is not None:
+            raise NotImplementedError("forward hooks are not supported under frame sharding "
+                                      "(UNetMotionModel.dist is set): the module path has no "
+                                      "cross-rank temporal window; detach the hooks or the FrameShard")
         B, Cc, Fr, H, W = sample.shape
         L = ehs.shape[1]
         emb = self.time_embedding(self.time_proj(t))                       # (B, 1280)

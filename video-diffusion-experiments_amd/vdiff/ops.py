@@ -281,12 +281,15 @@ def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, 
         if rc != VD_EUNSUPPORTED:
             check(rc, "vd_temporal_attention_rope")
             return out
-        # no fused variant (the force-VALU test hook): rotate q/k in place, then attend;
-        # q and k must be the column slices [0, C) and [C, 2C) of one QKV row buffer
-        if k.data_ptr() - q.data_ptr() != heads * d * q.element_size():
-            raise ValueError("rope fallback needs q, k adjacent column slices of one buffer")
-        qk = torch.as_strided(q, (q.shape[0], 2 * heads * d), (q.stride(0), 1))
-        rope_qk(qk, 2 * heads * d, d, 1, frames, 1, positions, rope_theta)
+        # no fused variant (the force-VALU test hook): rotate a COPY of q|k (the caller's
+        # buffer stays un-rotated, as the fused kernel leaves it), then attend on the copy
+        C = heads * d
+        qkv = torch.empty(q.shape[0], 3 * C, device=q.device, dtype=BF16)
+        qkv[:, :C].copy_(q[:, :C])
+        qkv[:, C:2 * C].copy_(k[:, :C])
+        qkv[:, 2 * C:].copy_(v[:, :C])
+        rope_qk(qkv, 2 * C, d, 1, frames, 1, positions, rope_theta)
+        q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
     check(lib().vd_temporal_attention(_p(q), _p(k), _p(v), q.stride(0), _p(out), out.stride(0), batch,
                                       frames, positions, heads, d, scale, _stream()),
           "vd_temporal_attention")

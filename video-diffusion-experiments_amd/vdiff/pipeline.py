@@ -216,9 +216,27 @@ class AnimateDiffPipeline:
         return cls(unet, sched, dist=dist, vae=vae)
 
     @classmethod
-    def from_pretrained(cls, *args, **kwargs):
-        raise NotImplementedError("hub checkpoints are unreachable offline: build with from_config() "
-                                  "and vdiff.weights.load_diffusers_state_dict() for local safetensors")
+    def from_pretrained(cls, pretrained_model_name_or_path, motion_adapter=None, torch_dtype=None, variant=None,
+                        device="cuda", dist=None, **unused):
+        """diffusers AnimateDiffPipeline.from_pretrained(path, motion_adapter=, torch_dtype=) as
+        05:130-134 calls it, over a LOCAL diffusers-layout directory (vdiff.pretrained): unet/
+        joined with the MotionAdapter's motion modules, vae/ (decoder), scheduler/.  The text
+        encoder stays the deterministic stub (CLIP is out of scope; pass prompt_embeds for real
+        embeddings).  device="cpu" builds the modules without preparing device operands."""
+        from . import pretrained as P
+        root = P._local_dir(pretrained_model_name_or_path, "AnimateDiffPipeline.from_pretrained")
+        if motion_adapter is None:
+            raise ValueError("AnimateDiffPipeline needs motion_adapter=MotionAdapter.from_pretrained(...)")
+        unet = P.load_unet_motion(root / "unet", motion_adapter, device=device, variant=variant)
+        vae = P.load_vae(root / "vae", device=device, variant=variant) if (root / "vae").is_dir() else None
+        sched = P.load_scheduler(root / "scheduler") if (root / "scheduler").is_dir() else None
+        if torch.device(device).type == "cuda":
+            unet.prepare()
+            if vae is not None:
+                vae.prepare()
+        pipe = cls(unet, sched, dist=dist, vae=vae)
+        pipe.torch_dtype = torch_dtype
+        return pipe
 
     def enable_vae_slicing(self):
         pass  # decoding is always chunked (AutoencoderKL.frames_per_chunk)
