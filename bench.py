@@ -83,8 +83,8 @@ def time_attention(n_img, reps, stream, stress=False):
     flop = 4.0 * S * S * d * heads * n_img
     byts = 4.0 * n_img * S * C * 2            # Q, K, V read once + O written once (bf16)
     tf = flop / (ms * 1e-3) / 1e12
-    return {"kernel": "flash32_kernel<40,unit-c> (spatial self-attn, L1: S=4096, d=40, 8 heads, "
-                      f"{n_img} images)",
+    return {"kernel": "flash40_kernel<unit-c> + its flash32 exact fix-up launch (spatial self-attn, L1: "
+                      f"S=4096, d=40, 8 heads, {n_img} images)",
             "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": None,
             "avg_launch_ms": round(ms, 4), "algorithmic_flop_per_launch": flop,
@@ -125,7 +125,7 @@ def pmc_traffic(n_img):
     `bench.py --roofline-only` at 32 images, corrected as MI355X_MICROARCH.md §HBM prescribes;
     scaled linearly to this rank's image count).  None when no summary matches the sources."""
     t, name = _pmc_file("r*_traffic.json")
-    if t is None or "flash32_kernel<40" not in (t.get("kernel") or ""):
+    if t is None or "flash40_kernel" not in (t.get("kernel") or ""):
         return None, None
     return t["traffic_bytes_per_launch"] * n_img / 32.0, name
 

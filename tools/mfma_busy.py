@@ -1,7 +1,8 @@
 """Summarise tools/mfma_busy.sh: per kernel family, dispatch-weighted MFMA-busy share
 = sum SQ_VALU_MFMA_BUSY_CYCLES / sum (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs).
 usage: python tools/mfma_busy.py <pmc dir> [out.json]  (the JSON holds the L1 spatial
-self-attention's share — flash32_kernel<40, true> dispatches longer than 300 us — which
+self-attention's share — flash40_kernel<true> dispatches (round 3; flash32_kernel<40, true> longer
+than 300 us before it) — which
 bench.py reports as roofline.mfma_busy)."""
 import collections
 import csv
@@ -24,7 +25,9 @@ for d in disp.values():
         continue
     k = d["k"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
     fam = k.split("<")[0]
-    if k.startswith("flash32_kernel<40, true"):
+    if k.startswith("flash40_kernel<true"):
+        fam = "flash40<unit-c> L1 self-attn"
+    elif k.startswith("flash32_kernel<40, true"):
         # > 300 us at ~2.4 GHz x 8 XCDs: the L1 self-attention; shorter ones are cross-attention
         fam = "flash32<40,unit-c> L1 self-attn" if d["GRBM_GUI_ACTIVE"] > 8 * 2.4e9 * 300e-6 else "flash32<40,unit-c> cross-attn"
     busy[fam] += d["SQ_VALU_MFMA_BUSY_CYCLES"]
@@ -39,9 +42,10 @@ for f in sorted(step, key=lambda f: -act[f]):
     print(f"{f:36s} {n[f]:10d} {act[f] / ta * 100:9.1f}% {share(f) * 100:9.1f}%")
 print(f"{'ALL (model kernels)':36s} {sum(n[f] for f in step):10d} {100.0:9.1f}% "
       f"{sum(busy[f] for f in step) / (1024 * ta / 8) * 100:9.1f}%")
-key = "flash32<40,unit-c> L1 self-attn"
+key = "flash40<unit-c> L1 self-attn" if act["flash40<unit-c> L1 self-attn"] else "flash32<40,unit-c> L1 self-attn"
 if len(sys.argv) > 2 and act[key]:
-    json.dump({"kernel": "flash32_kernel<40, true> (L1 spatial self-attention)", "mfma_busy_frac": round(share(key), 4),
+    json.dump({"kernel": ("flash40_kernel<true>" if key.startswith("flash40") else "flash32_kernel<40, true>") +
+               " (L1 spatial self-attention)", "mfma_busy_frac": round(share(key), 4),
                "dispatches": n[key], "counters": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 x GRBM_GUI_ACTIVE / 8)",
                "kernel_src_hash": roof_src_hash()},
               open(sys.argv[2], "w"), indent=1)

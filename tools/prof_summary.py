@@ -38,9 +38,10 @@ for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:40]:
     print(f"  {sum(v) / steps / 1e3:9.1f} us  x{len(v) / steps:5.1f}  avg {sum(v) / len(v) / 1e3:8.1f} us  "
           f"{k[0]} grid={k[1]} wg={k[2]}")
 
-# the same kernel inside the step (the L1 spatial self-attention: flash32<40, unit-c> launches
-# longer than 300 us; the shorter ones are its text cross-attention)
-ins = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win if "flash32_kernel<40, true" in r["Kernel_Name"]]
+# the same kernel inside the step (the L1 spatial self-attention: flash40<unit-c>; before round 3
+# flash32<40, unit-c> launches longer than 300 us, the shorter ones being its text cross-attention)
+ROOF = "flash40_kernel<true>" if any("flash40_kernel<true>" in r["Kernel_Name"] for r in rows) else "flash32_kernel<40, true"
+ins = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win if ROOF in r["Kernel_Name"]]
 ins = [x for x in ins if x > 300e3]
 if ins:
     print(f"roofline kernel inside the step (L1 self-attention): {len(ins)} launches, avg {sum(ins) / len(ins) / 1e3:.1f} us")
@@ -49,7 +50,12 @@ if ins:
 # self-attention kernel (10 warm-up + attn_reps timed) on its own, first on model-scale inputs
 # (the bench line's roofline.avg_launch_ms), then on the stress inputs (roofline.stress);
 # those launches close the trace and their averages must agree with the bench line.
-after = [r for r in rows if int(r["Start_Timestamp"]) > t1 and "flash32_kernel" in r["Kernel_Name"]]
+after = [r for r in rows if int(r["Start_Timestamp"]) > t1 and ROOF in r["Kernel_Name"]]
+fixk = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows
+        if int(r["Start_Timestamp"]) > t1 and "flash32_kernel<40, true, false, 2, true>" in r["Kernel_Name"]]
+if fixk:
+    print(f"exact fix-up launches after the step loop (flash32_kernel<40, true, false, 2, true>): {len(fixk)}, "
+          f"avg {sum(fixk) / len(fixk) / 1e3:.1f} us")
 halves = [after[:len(after) // 2], after[len(after) // 2:]] if len(after) >= 8 else [after]
 WARM = 10  # bench.py WARM_ATTN
 for tag, part in zip(("model-scale inputs", "stress inputs"), halves):

@@ -32,7 +32,8 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int KT = 64;   // keys per tile
-int g_flash32 = 1;       // d = 40: 1 = flash32 (4-wave, default), 2 = flash32pp (8-wave pipeline), 0 = flash_attn 16x16x32
+int g_flash32 = 1;       // d = 40: 1 = automatic (flash40 for >= 4 key tiles, else flash32), 7 = flash32 only,
+                         // 6 = flash40 wherever it applies, 2 = flash32pp (8-wave pipeline), 0 = flash_attn 16x16x32
 
 template <int D>
 struct AttnCfg {
@@ -776,7 +777,10 @@ __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, cons
 
 // QB = 32-query blocks per wave: 2 (default: 256 VGPRs, two waves per SIMD) or 1 (half the
 // registers, three waves per SIMD — round 2's occupancy variant, vd_attention_select(6)).
-template <int D, bool UNITC, bool IL = false, int QB = 2>
+// FIX: flash40's exact fix-up pass — a block whose first output element is a NaN flag (flash40
+// found a score jump past its fast pass's range there) recomputes its 256 queries with the exact
+// pass; every other block returns at once.
+template <int D, bool UNITC, bool IL = false, int QB = 2, bool FIX = false>
 __global__ __launch_bounds__(NT, QB == 1 ? 3 : 2) void flash32_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
@@ -799,6 +803,11 @@ __global__ __launch_bounds__(NT, QB == 1 ? 3 : 2) void flash32_kernel(
   const bf16_t* qb_ptr = q + b * sq * ldq + (int64_t)h * D;
   const bf16_t* kb_ptr = k + bkv * skv * ldk + (int64_t)h * D;
   const bf16_t* vb_ptr = v + bkv * skv * ldv + (int64_t)h * D;
+  if constexpr (FIX) {
+    const int64_t f = (b * sq + (int64_t)qblk * (4 * 32 * QB)) * ldo + (int64_t)h * D;
+    const bool flagged = out_f32 ? __builtin_isnan(((const float*)o)[f]) : ((o[f] & 0x7FFF) > 0x7F80);
+    if (!flagged) return;
+  }
 
   // Q'^T fragments: lane holds Q'[q0 + qb*32 + r32][16*ks + 8*hh .. +7].  Q is
   // used as given (no bf16 prescale: that second rounding costs ~0.4% in P); with
@@ -846,8 +855,8 @@ __global__ __launch_bounds__(NT, QB == 1 ? 3 : 2) void flash32_kernel(
   // V^T tr-read lane offset inside a [32 d] image row block (elements)
   const int vtr = ((4 * hh + (i16 >> 2)) * 32) + 16 * (g16 & 1) + 4 * (i16 & 3);
   f32x16 oacc[C::NDB][QB];
-  const bool bad = f32_loop<D, UNITC, false, IL, QB>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv,
-                                                 qf, oacc, r32, hh, vtr, c);
+  const bool bad = FIX || f32_loop<D, UNITC, false, IL, QB>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk,
+                                                           ldsv, qf, oacc, r32, hh, vtr, c);
   if (__syncthreads_or(bad)) {  // a score jumped > ~100 (log2) past mu somewhere: exact pass
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb)
@@ -1243,12 +1252,494 @@ __global__ __launch_bounds__(2 * NT, 1) void flash32pp_kernel(
   }
 }
 
+// ============================================================ flash40
+// The d = 40 spatial self-attention (SD-1.5 level 1, the roofline kernel) as a two-group
+// ping-pong over an LDS-DMA ring (round 3).  flash32's arithmetic, tile for tile: S^T =
+// K'.Q'^T on v_mfma_f32_32x32x16_bf16 with the running offset -mu folded into Q' (K' column 40
+// = 1), P = exp2 packed to bf16 straight from the accumulator as the PV B operand, V's column
+// 40 = 1 yields the row sum, mu from tile 0's max (every tile on the exact rerun), the fast
+// pass's row-sum rescale past 2^32 and its exact rerun past 2^100 — results equal flash32's.
+//
+// What changes is the schedule.  Each wave's work per 64-key tile t splits into
+//     V(t): the softmax of S(t) -> P(t)                    VALU only (64 exp2 + 32 packs)
+//     M(t): PV(t) then QK^T(t+1) -> S(t+1)                  MFMA only (16 + 12 x 32x32x16)
+// and the workgroup's 8 waves form two groups one barrier apart (waves w and w+4 share a
+// SIMD): while group 0 runs M, group 1 runs V and vice versa, so on every SIMD the matrix
+// pipe and the VALU work side by side (MI355X_MICROARCH.md "Two waves per SIMD").  One
+// s_barrier per phase; 512 queries per workgroup (8 waves x 64) share every K/V tile.
+//
+// K/V tiles arrive by LDS-DMA (buffer_load ... lds: 12 x 1 KiB per tile, two per wave on
+// waves 0-5, issued two tiles ahead) into a 4-slot ring: no register staging, no ds_write in
+// the loop.  LDS image of a slot (12 KiB): K as [chunk c 0..5][key] 16-B rows, chunk 5 = K'
+// column 40 ({1, 0 x 7}); V as [key][d 0..31], [key][d 32..39] and [key][{1, 0 x 7}] (V column
+// 40 and the zero columns, by per-lane tr-read addresses).  The K'/V ones chunks are DMA'd from
+// a 16-byte constant like the data, so a key past skv — every K/V byte of its row out of the
+// buffer's range — reads all zeros: score 0, P = 1, V row and ones column 0, i.e. no
+// contribution, with no masking code.  The K' ds_read_b128 of 32 keys is 512 contiguous bytes
+// and the V tr-read of 4 keys x 32 d 256 contiguous bytes: conflict-free.  Tile u is issued at
+// phase 2u-4 and waited for (counted vmcnt; the DMA is inline asm so hipcc neither counts it nor
+// drains it before the LDS reads) before the barrier that ends phase 2u-1; the slot it
+// overwrites (tile u-4) was last read in phase 2u-6.
+constexpr int F4_NW = 8, F4_NT = 512, F4_QB = 2, F4_QWG = F4_NW * 32 * F4_QB;
+constexpr int F4_RING = 4;
+constexpr int F4_K = 0, F4_V0 = 6 * 1024, F4_V1 = F4_V0 + 4096, F4_VONE = F4_V1 + 1024, F4_SLOT = F4_VONE + 1024;
+constexpr int F4_LDS = F4_RING * F4_SLOT;
+
+__device__ const uint32_t f4_ones[4] = {0x3F80u, 0u, 0u, 0u};  // bf16 {1, 0 x 7}: the ones chunks
+
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+__device__ __forceinline__ u32x4 f4_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  u32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) & 0xffffu;  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane(bytes);                          // num_records: range check
+  r[3] = 0x00020000u;
+  return r;
+}
+
+// One 1 KiB LDS-DMA piece: lane l's 16 bytes at voff land at LDS byte lds + 16 l.  Inline asm:
+// M0 written in the statement that reads it, and hipcc does not count it in vmcnt (f4_wait_vm).
+__device__ __forceinline__ void f4_dma(u32x4 rs, uint32_t lds, uint32_t voff) {
+  uint32_t keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "s"(lds), "v"(voff), "s"(rs) : "memory");
+}
+
+// This wave's two pieces of every tile (waves 0-5; piece p = 2 wave + i): 0-4 = K chunk p of
+// the 64 keys (lane = key), 5 = the K' ones chunk, 6-9 = V d 0..31 of keys 16 (p-6) + lane/4
+// (lane % 4 = chunk), 10 = V d 32..39, 11 = the V ones chunk.
+struct F4Dma {
+  u32x4 rs[2];
+  uint32_t voff[2];   // lane part of the byte offset (row r, column chunk), or 0 for a ones chunk
+  uint32_t step[2];   // bytes per key (0 for a ones chunk)
+  uint32_t row[2];    // the lane's key inside the tile
+  uint32_t lds[2];    // byte offset of the piece inside a slot
+};
+
+__device__ __forceinline__ void f4_issue(const F4Dma& m, uint32_t lds0, int t, int64_t skv) {
+  const uint32_t key0 = (uint32_t)t * KT;
+  const uint32_t slot = lds0 + (uint32_t)(t % F4_RING) * F4_SLOT;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    // data: (key0 + row) * ld + col, past skv out of range -> zeros; ones chunk: offset 0, or 16
+    // (out of its 16-byte range -> zeros) for a key past skv
+    const uint32_t off = m.step[i] ? m.voff[i] + key0 * m.step[i] : ((int64_t)(key0 + m.row[i]) < skv ? 0u : 16u);
+    f4_dma(m.rs[i], slot + m.lds[i], off);
+  }
+}
+
+// Pin a value at this point of the instruction stream: hipcc's sinking passes otherwise move
+// the V phase's exp2/packs (pure register work) past the s_barrier into the M phase, next to
+// the MFMAs that use them, which undoes the ping-pong.
+template <typename T>
+__device__ __forceinline__ void f4_pin(T& x) {
+  asm volatile("" : "+v"(x));
+}
+
+template <int N>
+__device__ __forceinline__ void f4_wait_vm() {
+  if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void f4_bar() {  // this wave's LDS reads drained, DMA left in flight
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <bool UNITC>
+__device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F4Dma& dma, bool issuer,
+                                        bool g0, int64_t skv, bf16x8 (&qf)[F4_QB][3], f32x16 (&oacc)[2][F4_QB],
+                                        uint32_t kl0, uint32_t v0l, uint32_t v1l, int hh, float c) {
+  using C = F32Cfg<40>;
+  constexpr int QB = F4_QB;
+  constexpr float RESCALE = 4294967296.0f;        // 2^32
+  constexpr float BAD = 1.2676506002282294e30f;   // 2^100
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[db][qb][i] = 0.f;
+  float mu[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) mu[qb] = 0.f;
+  bool bad = false;
+  const int T = (int)((skv + KT - 1) / KT);  // >= 2 (launch condition)
+
+  f32x16 s[2][QB];
+  bf16x8 pf[2][2][QB];
+  bf16x8 vfr[2][2][2];
+  bf16x8 kfr[2][3];
+
+  // V^T fragments of tile t (PV's A operand, key order as flash32): d-block 0 in the V phase,
+  // d-block 1 at the start of the M phase (its 8 MFMAs of d-block 0 cover the latency)
+  auto read_v = [&](int t, int db) {
+    const uint32_t sb = (uint32_t)((t % F4_RING) * F4_SLOT);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const uint32_t R = (uint32_t)(kb * 32 + 16 * s2);
+        const uint32_t a = db == 0 ? sb + v0l + R * 64 : sb + v1l + R * 16;
+        const uint32_t ah = a + (db == 0 ? 512 : 128);
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(smem + a));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(smem + ah));
+        vfr[db][kb][s2] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+  };
+  auto read_k = [&](int t, int kb) {  // K' fragments of tile t, key block kb: chunk 2 ks + hh
+    const uint32_t sb = (uint32_t)((t % F4_RING) * F4_SLOT) + kl0 + 512 * kb;
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) kfr[kb][ks] = *(const bf16x8*)(smem + sb + 2048 * ks);
+  };
+  auto qk = [&](int kb) {  // S(kb) = K'.Q'^T from the fragments read_k left
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        if (ks == 0) {
+          f32x16 z;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) z[i] = 0.f;
+          s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], z, 0, 0, 0);
+        } else {
+          s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], s[kb][qb], 0, 0, 0);
+        }
+      }
+  };
+  auto pv = [&](int db) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb)
+          oacc[db][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[db][kb][s2], pf[kb][s2][qb], oacc[db][qb], 0, 0, 0);
+  };
+  auto rescale = [&](int qb, float nmu) {
+    const float delta = nmu - mu[qb];  // exact: both bf16 values
+    const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
+    mu[qb] = nmu;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[kb][qb][i] -= delta;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
+    if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
+  };
+  // flash32 tile_generic's decisions for tile t, taken right after QK^T(t) at the end of the M
+  // phase that computed S(t) (the lowest register pressure of the loop): the tile max on tile 0
+  // (every tile on the exact pass), else the fast pass's row-sum check over tiles 0..t-1 (PV(t-1)
+  // ran earlier in this phase) — the same values at the same point of the tile order as flash32
+  auto decide = [&](int t) {
+    if (t == 0) {
+      float tm[QB];
+      bool need = true;
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const float m = tile_max(s[0][qb], s[1][qb]);
+        tm[qb] = vmax2(m, partner32(m));
+        need |= (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
+      }
+      if (__any(need)) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          rescale(qb, (float)(__bf16)(mu[qb] + tm[qb]));
+        }
+      }
+    } else if (t > 1) {
+      float lq[QB];
+      bool resc = false, over = false;
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const float lown = oacc[C::L_DB][qb][C::L_I];
+        const float lp = partner32(lown);
+        lq[qb] = hh == C::L_H ? lown : lp;
+        resc |= lq[qb] > RESCALE;
+        over |= !(lq[qb] < BAD);
+      }
+      if (__any(over)) {
+        bad = true;
+      } else if (__any(resc)) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          const float step = lq[qb] > RESCALE ? __builtin_amdgcn_logf(lq[qb]) : 0.f;
+          rescale(qb, (float)(__bf16)(mu[qb] + (UNITC ? step : step / c)));
+        }
+      }
+    }
+  };
+  auto softmax = [&]() {  // V(t): S(t) -> P(t), exp2 and bf16 packs only
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            f[j] = (__bf16)__builtin_amdgcn_exp2f(UNITC ? s[kb][qb][8 * s2 + j] : s[kb][qb][8 * s2 + j] * c);
+          pf[kb][s2][qb] = f;
+        }
+  };
+  // M(t) = PV(t) then QK^T(t+1): d-block 1's V reads and key block 0's K' reads go out first,
+  // key block 1's under d-block 0's MFMAs; the decisions for tile t+1 follow its QK^T
+  auto mphase = [&](int t) {
+    const bool more = t + 1 < T;
+    read_v(t, 1);
+    if (more) read_k(t + 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    pv(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) read_k(t + 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    pv(1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      qk(0);
+      qk(1);
+      decide(t + 1);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) f4_pin(s[kb][qb]);
+    }
+  };
+  // tile u's DMA: issued at phase 2u-4 (u >= 2), waited for at the end of phase 2u-1
+  auto issue = [&](int u) {
+    if (issuer && u < T) f4_issue(dma, lds0, u, skv);
+  };
+  auto wait_tile = [&](int u) {
+    if (issuer && u < T) {
+      if (u + 1 < T) f4_wait_vm<2>();
+      else f4_wait_vm<0>();
+    }
+  };
+
+  // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere
+  issue(0);
+  issue(1);
+  wait_tile(0);
+  f4_bar();
+  // one instruction stream for both groups; group 1 (waves 4-7) runs one phase behind:
+  //   group 0: ph 0 [DMA 2, QK(0)] | ph 2t+1 [V(t), wait t+1] | ph 2t+2 [DMA t+3, M(t)] | ph 2T+1 []
+  //   group 1: ph 0 [DMA 2] | ph 1 [QK(0), wait 1] | ph 2t+2 [DMA t+3, V(t)] | ph 2t+3 [M(t), wait t+2]
+  issue(2);
+  if (!g0) f4_bar();
+  read_k(0, 0);
+  read_k(0, 1);
+  qk(0);
+  qk(1);
+  decide(0);
+  if (!g0) wait_tile(1);
+  f4_bar();
+  for (int t = 0; t < T; ++t) {
+    if (!g0) issue(t + 3);
+    softmax();
+    __builtin_amdgcn_sched_barrier(0);
+    read_v(t, 0);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        f4_pin(vfr[0][kb][s2]);
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) f4_pin(pf[kb][s2][qb]);
+      }
+    if (g0) wait_tile(t + 1);
+    f4_bar();
+    if (g0) issue(t + 3);
+    mphase(t);
+    if (!g0) wait_tile(t + 2);
+    f4_bar();
+  }
+  if (g0) f4_bar();
+  {  // the last tiles' row sums were not checked in the loop
+    bool over = false;
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      const float lown = oacc[C::L_DB][qb][C::L_I];
+      const float lp = partner32(lown);
+      over |= !((hh == C::L_H ? lown : lp) < BAD);
+    }
+    bad |= __any(over);
+  }
+  return bad;
+}
+
+// One workgroup's whole block: Q' load, DMA setup, the fast pass, the epilogue.  When a score
+// jumped > ~100 (log2) past mu somewhere in the block it stores NaN flags instead, and flash32's
+// exact pass (flash32_kernel<..., FIX>, launched right after) recomputes the flagged quarters —
+// the exact loop inlined here as well would double the kernel's register pressure.
+template <bool UNITC>
+__device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ q, int64_t ldq,
+                                         const bf16_t* __restrict__ k, int64_t ldk, const bf16_t* __restrict__ v,
+                                         int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads, int64_t sq,
+                                         int64_t skv, int64_t kv_div, float c, int out_f32) {
+  constexpr int D = 40, QB = F4_QB;
+  using C = F32Cfg<D>;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool g0 = wave < 4;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int nqb = (int)((sq + F4_QWG - 1) / F4_QWG);
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qblk = lid % nqb;
+  const int h = (lid / nqb) % heads;
+  const int64_t b = (lid / nqb) / heads;
+  const int64_t q0 = (int64_t)qblk * F4_QWG + wave * (32 * QB);
+  const int64_t bkv = b / kv_div;
+  const bf16_t* qb_ptr = q + b * sq * ldq + (int64_t)h * D;
+  const bf16_t* kb_ptr = k + bkv * skv * ldk + (int64_t)h * D;
+  const bf16_t* vb_ptr = v + bkv * skv * ldv + (int64_t)h * D;
+
+  bf16x8 qf[QB][3];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    const int64_t qi = q0 + qb * 32 + r32;
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const int dd = ks * 16 + 8 * hh;
+      uint4 u = make_uint4(0, 0, 0, 0);
+      if (qi < sq && dd < D) u = *(const uint4*)(qb_ptr + qi * ldq + dd);
+      qf[qb][ks] = __builtin_bit_cast(bf16x8, u);  // d = 40 entry starts at 0 (mu = 0)
+    }
+  }
+
+  // LDS-DMA pieces (waves 0-5)
+  F4Dma dma;
+  const bool issuer = wave < 6;
+  {
+    const uint32_t ldkb = (uint32_t)ldk * 2, ldvb = (uint32_t)ldv * 2;
+    const u32x4 rk = f4_rsrc(kb_ptr, (uint32_t)(skv - 1) * ldkb + 2 * D);
+    const u32x4 rv = f4_rsrc(vb_ptr, (uint32_t)(skv - 1) * ldvb + 2 * D);
+    const u32x4 r1 = f4_rsrc(f4_ones, 16);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = 2 * wave + i;
+      uint32_t row = lane, col = 0, step = 0, lds = 0;
+      u32x4 rs = r1;
+      if (p < 5) {
+        rs = rk; col = 16 * p; step = ldkb; lds = F4_K + 1024 * p;
+      } else if (p == 5) {
+        lds = F4_K + 1024 * 5;
+      } else if (p < 10) {
+        rs = rv; row = 16 * (p - 6) + (lane >> 2); col = 16 * (lane & 3); step = ldvb; lds = F4_V0 + 1024 * (p - 6);
+      } else if (p == 10) {
+        rs = rv; col = 64; step = ldvb; lds = F4_V1;
+      } else {
+        lds = F4_VONE;
+      }
+      dma.rs[i] = rs; dma.row[i] = row; dma.step[i] = step; dma.lds[i] = lds;
+      dma.voff[i] = row * step + col;
+    }
+  }
+  // per-lane LDS read offsets (inside a slot)
+  const uint32_t kl0 = F4_K + hh * 1024 + r32 * 16;   // + 2048 ks + 512 kb: chunk 2 ks + hh
+  const int g16 = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  const uint32_t v0l = F4_V0 + (uint32_t)(((4 * hh + qq) * 32 + 16 * (g16 & 1) + 4 * pp) * 2);
+  // d-block 1 (d 32..63): columns 32..39 from V d 32..39, column 40 = the ones chunk's 1, the
+  // rest its zero half
+  const uint32_t v1l = ((g16 & 1) == 0 && pp < 2 ? F4_V1 + 8 * pp : F4_VONE + ((g16 & 1) == 0 && pp == 2 ? 0 : 8)) +
+                       (uint32_t)((4 * hh + qq) * 16);
+
+  f32x16 oacc[2][QB];
+  if (__syncthreads_or(f4_loop<UNITC>(smem, lds0, dma, issuer, g0, skv, qf, oacc, kl0, v0l, v1l, hh, c))) {
+    // a score jumped > ~100 (log2) past mu somewhere in the block: no output here; a NaN in
+    // element (first query, d 0) of each 256-query quarter tells flash32's exact fix-up pass,
+    // launched right after, to recompute that quarter
+    if (tid == 0)
+      for (int64_t qs = (int64_t)qblk * F4_QWG; qs < (int64_t)(qblk + 1) * F4_QWG && qs < sq; qs += 256) {
+        if (out_f32) ((float*)o)[(b * sq + qs) * ldo + (int64_t)h * D] = __builtin_nanf("");
+        else o[(b * sq + qs) * ldo + (int64_t)h * D] = 0x7FC0;
+      }
+    return true;
+  }
+
+  // epilogue as flash32: O[q][d] = O^T[d][q] / l
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    const float lown = oacc[C::L_DB][qb][C::L_I];
+    const float lp = partner32(lown);
+    const float l = hh == C::L_H ? lown : lp;
+    const float inv = __builtin_amdgcn_rcpf(l);
+    const int64_t qi = q0 + qb * 32 + r32;
+    if (out_f32) {
+      float* frow = (float*)o + (b * sq + qi) * ldo + (int64_t)h * D;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d0 = 32 * db + 8 * g + 4 * hh;
+          const f32x16& a = oacc[db][qb];
+          if (qi < sq && d0 + 4 <= D)
+            *(float4*)(frow + d0) = make_float4(a[4 * g] * inv, a[4 * g + 1] * inv, a[4 * g + 2] * inv, a[4 * g + 3] * inv);
+        }
+      continue;
+    }
+    bf16_t* orow = o + (b * sq + (qi < sq ? qi : 0)) * ldo + (int64_t)h * D;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const f32x16& a = oacc[db][qb];
+        uint32_t x0 = pack2(a[8 * m + 0] * inv, a[8 * m + 1] * inv), x1 = pack2(a[8 * m + 2] * inv, a[8 * m + 3] * inv);
+        uint32_t y0 = pack2(a[8 * m + 4] * inv, a[8 * m + 5] * inv), y1 = pack2(a[8 * m + 6] * inv, a[8 * m + 7] * inv);
+        auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+        auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+        const int dd = 32 * db + 16 * m + 8 * hh;
+        if (qi < sq && dd + 8 <= D) *(uint4*)(orow + dd) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+    }
+  }
+  return false;
+}
+
+template <bool UNITC>
+__global__ __launch_bounds__(F4_NT, 1) void flash40_kernel(
+    const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
+    const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
+    int64_t sq, int64_t skv, int64_t kv_div, float c, int out_f32) {
+  __shared__ __attribute__((aligned(1024))) char smem[F4_LDS];
+  f4_block<UNITC>(smem, q, ldq, k, ldk, v, ldv, o, ldo, heads, sq, skv, kv_div, c, out_f32);
+}
+
 template <int D>
 int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                  void* o, int64_t ldo, int64_t batch, int heads, int64_t sq, int64_t skv,
                  int64_t kv_div, float scale, hipStream_t s, int out_f32 = 0) {
   const float c = scale * 1.4426950408889634f;
   if constexpr (D == 40) {
+    // flash40 (ping-pong, LDS-DMA ring): the default for the long self-attention (>= 2 key tiles)
+    if ((g_flash32 == 6 || (g_flash32 == 1 && skv >= 256)) && skv >= 2 * KT && ((uintptr_t)o & 15) == 0 &&
+        ldo % (out_f32 ? 4 : 8) == 0) {
+      const int64_t nblk = (sq + F4_QWG - 1) / F4_QWG * heads * batch;
+      if (nblk > 0x7fffffff) return VD_EINVAL;
+      const dim3 grid((unsigned)nblk);
+      const dim3 fix((unsigned)((sq + 255) / 256 * heads * batch));
+      if (c == 1.0f) {
+        hipLaunchKernelGGL((flash40_kernel<true>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,
+                           ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+      } else {
+        hipLaunchKernelGGL((flash40_kernel<false>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,
+                           ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+        hipLaunchKernelGGL((flash32_kernel<D, false, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+      }
+      return vd_launch_status();
+    }
     if (g_flash32 == 2 && !out_f32 && ((uintptr_t)o & 15) == 0 && ldo % 8 == 0) {  // ping-pong 8-wave kernel
       const int64_t nblk = (sq + 511) / 512 * heads * batch;
       if (nblk > 0x7fffffff) return VD_EINVAL;
@@ -1765,10 +2256,13 @@ extern "C" int vd_attention_force_v1(int32_t on) {
 // 2 = flash32 (4-wave 32x32x16), 3 = flash32pp (8-wave pipeline), 4 = flash32 with the
 // intra-wave interleaved steady state (unit c only), 5 = flash32 held to one workgroup per
 // CU (96 KiB of dynamic LDS: one wave per SIMD — the occupancy probe of DESIGN.md §5), 6 =
-// flash32 with one 32-query block per wave (128 VGPRs, four waves per SIMD).
+// flash32 with one 32-query block per wave (128 VGPRs, four waves per SIMD), 7 = flash40 (the
+// two-group ping-pong over an LDS-DMA ring, round 3) wherever it applies (>= 2 key tiles), 8 =
+// flash32 only (round 2's default; automatic = flash40 from 4 key tiles, flash32 below).
 extern "C" int vd_attention_select(int32_t kernel) {
-  if (kernel < 0 || kernel > 6) return VD_EINVAL;
-  g_flash32 = kernel == 1 ? 0 : (kernel == 3 ? 2 : (kernel == 4 ? 3 : (kernel == 5 ? 4 : (kernel == 6 ? 5 : 1))));
+  if (kernel < 0 || kernel > 8) return VD_EINVAL;
+  static const int map[9] = {1, 0, 7, 2, 3, 4, 5, 6, 7};
+  g_flash32 = map[kernel];
   return VD_OK;
 }
 
