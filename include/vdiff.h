@@ -197,12 +197,18 @@ int vd_attention_f32(const void* q, int64_t ldq, const void* k, int64_t ldk, con
 /* Test/benchmark hook: on != 0 routes d = 40 to the 16x16x32 flash kernel instead of
  * the 32x32x16 one (default). */
 int vd_attention_force_v1(int32_t on);
-/* Test/benchmark hook: the d = 40 kernel — 0 = automatic (flash32), 1 = the 16x16x32 flash
- * kernel, 2 = flash32 (4 waves, 32x32x16), 3 = flash32pp (8 waves: two staggered groups
- * software-pipelined PV(t-1)+QK(t) | softmax(t); bitwise equal to flash32, measured slower —
- * tools/attn_ab.py), 4 = flash32 with the intra-wave interleaved steady state, 5 = flash32 at
- * one workgroup per CU (occupancy probe). */
+/* Test/benchmark hook: the d = 40 kernel — 0 = automatic (flash40 from 4 key tiles, flash32
+ * below), 1 = the 16x16x32 flash kernel, 2 = flash32 (4 waves, 32x32x16), 3 = flash32pp (8
+ * waves: two staggered groups software-pipelined PV(t-1)+QK(t) | softmax(t); bitwise equal to
+ * flash32, measured slower — tools/attn_ab.py), 4 = flash32 with the intra-wave interleaved
+ * steady state, 5 = flash32 at one workgroup per CU (occupancy probe), 6 = flash32 with one
+ * 32-query block per wave, 7 = flash40 (round 3: two-group ping-pong over an LDS-DMA ring,
+ * bit-identical to flash32) wherever it applies (>= 2 key tiles), 8 = flash32 only, 9 = flash40's
+ * stamped diagnostic build. */
 int vd_attention_select(int32_t kernel);
+/* Diagnostic hook: copy the barrier stamps (s_memtime, 8 waves x 512, wave-major) that the last
+ * flash40 launch made under vd_attention_select(9) to dst (device memory, n <= 4096 uint64). */
+int vd_attention_stamps(void* dst, int64_t n, vd_stream_t stream);
 
 /* Temporal (motion-module) self-attention over frames (a9): token (b, f, p) is
  * row (b*frames + f)*positions + p of q/k/v/o (the NHWC layout, no permute);

@@ -142,9 +142,13 @@ def test_full_model_eight_ranks_two_frames_match_unsharded(cuda):
     frames sharded 2 per rank over 8 ranks sharing cuda:0 (collectives staged through gloo),
     one CFG DDIM step after prime(), against the unsharded 16-frame loop.  Both sides run one
     GEMM path (vd_gemm_select_path(1): the register-staged kernel, unsplit, for every shape), so
-    the ranks' smaller M cannot change a GEMM plan or a split-K summation order: what is left
-    is the collective decomposition itself (the cross-rank GroupNorm Chan merge, the all-to-all
-    re-shards) and bf16 roundings it flips.  Bound 1e-3 rel-L2 (printed)."""
+    the ranks' smaller M cannot change a GEMM plan or a split-K summation order; GroupNorm
+    splits are frame-aligned (a rank's records are the unsharded run's records of its frames,
+    all-gathered in frame order) and image norms split by image size alone.  What is left is the
+    collective decomposition itself — all-gathers and all-to-all re-shards that move bytes — so
+    the sharded loop must equal the unsharded one BIT FOR BIT (printed: max |diff|, rel-L2).
+    (Round 2 bounded this at 2e-2: any fp32 reordering anywhere decorrelates a bf16 network to
+    its ~1 % realisation floor, so only exactness is a meaningful check.)"""
     from vdiff import DenoiseLoop
     from vdiff._lib import check, lib
     lat, ehs = _inputs("full")
@@ -162,5 +166,6 @@ def test_full_model_eight_ranks_two_frames_match_unsharded(cuda):
         got = torch.load(path, weights_only=True)
     assert got.shape == ref.shape == (1, 4, FULL_FRAMES, 64, 64)
     err = ((got.double() - ref.double()).norm() / ref.double().norm()).item()
-    print(f"full model 8 ranks x 2 frames vs unsharded (one GEMM path): rel-L2 {err:.2e}")
-    assert err < 1e-3, err
+    print(f"full model 8 ranks x 2 frames vs unsharded (one GEMM path): rel-L2 {err:.2e}, "
+          f"max|diff| {(got - ref).abs().max().item():.2e}")
+    assert torch.equal(got, ref), err

@@ -33,7 +33,8 @@ namespace {
 constexpr int NT = 256;
 constexpr int KT = 64;   // keys per tile
 int g_flash32 = 1;       // d = 40: 1 = automatic (flash40 for >= 4 key tiles, else flash32), 7 = flash32 only,
-                         // 6 = flash40 wherever it applies, 2 = flash32pp (8-wave pipeline), 0 = flash_attn 16x16x32
+                         // 6 = flash40 wherever it applies, 8 = flash40 stamped (diagnostic),
+                         // 2 = flash32pp (8-wave pipeline), 0 = flash_attn 16x16x32
 
 template <int D>
 struct AttnCfg {
@@ -1333,7 +1334,9 @@ __device__ __forceinline__ void f4_issue(const F4Dma& m, uint32_t lds0, int t, i
 
 // Pin a value at this point of the instruction stream: hipcc's sinking passes otherwise move
 // the V phase's exp2/packs (pure register work) past the s_barrier into the M phase, next to
-// the MFMAs that use them, which undoes the ping-pong.
+// the MFMAs that use them, which undoes the ping-pong.  Never pin an MFMA result: hipcc pads no
+// wait states for an asm reader, and after the asm it takes the register as the asm's output, so
+// the later VALU readers lose their MFMA hazard padding (a race with the still-running MFMA).
 template <typename T>
 __device__ __forceinline__ void f4_pin(T& x) {
   asm volatile("" : "+v"(x));
@@ -1350,10 +1353,31 @@ __device__ __forceinline__ void f4_bar() {  // this wave's LDS reads drained, DM
   asm volatile("" ::: "memory");
 }
 
-template <bool UNITC>
+// Diagnostic build (ST, vd_attention_select(9)): workgroup 0's waves record s_memtime on both
+// sides of every barrier into LDS and copy them to f4_stamps at the end (vd_attention_stamps):
+// per phase, the work time (release -> arrival) and the barrier wait (arrival -> release).
+constexpr int F4_NST = 512;  // stamps per wave
+__device__ uint64_t f4_stamps[F4_NW * F4_NST];
+
+template <bool UNITC, bool ST = false>
 __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F4Dma& dma, bool issuer,
                                         bool g0, int64_t skv, bf16x8 (&qf)[F4_QB][3], f32x16 (&oacc)[2][F4_QB],
                                         uint32_t kl0, uint32_t v0l, uint32_t v1l, int hh, float c) {
+  int nst = 0;
+  const bool stw = ST && blockIdx.x == 0;
+  auto stamp = [&]() {
+    if constexpr (ST) {
+      const uint64_t tt = __builtin_amdgcn_s_memtime();
+      if (stw && (threadIdx.x & 63) == 0 && nst < F4_NST)
+        *(uint64_t*)(smem + F4_LDS + ((threadIdx.x >> 6) * F4_NST + nst) * 8) = tt;
+      ++nst;
+    }
+  };
+  auto bar = [&]() {
+    stamp();
+    f4_bar();
+    stamp();
+  };
   using C = F32Cfg<40>;
   constexpr int QB = F4_QB;
   constexpr float RESCALE = 4294967296.0f;        // 2^32
@@ -1507,10 +1531,6 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
       qk(0);
       qk(1);
       decide(t + 1);
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb) f4_pin(s[kb][qb]);
     }
   };
   // tile u's DMA: issued at phase 2u-4 (u >= 2), waited for at the end of phase 2u-1
@@ -1528,19 +1548,19 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   issue(0);
   issue(1);
   wait_tile(0);
-  f4_bar();
+  bar();
   // one instruction stream for both groups; group 1 (waves 4-7) runs one phase behind:
   //   group 0: ph 0 [DMA 2, QK(0)] | ph 2t+1 [V(t), wait t+1] | ph 2t+2 [DMA t+3, M(t)] | ph 2T+1 []
   //   group 1: ph 0 [DMA 2] | ph 1 [QK(0), wait 1] | ph 2t+2 [DMA t+3, V(t)] | ph 2t+3 [M(t), wait t+2]
   issue(2);
-  if (!g0) f4_bar();
+  if (!g0) bar();
   read_k(0, 0);
   read_k(0, 1);
   qk(0);
   qk(1);
   decide(0);
   if (!g0) wait_tile(1);
-  f4_bar();
+  bar();
   for (int t = 0; t < T; ++t) {
     if (!g0) issue(t + 3);
     softmax();
@@ -1555,13 +1575,13 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
         for (int qb = 0; qb < QB; ++qb) f4_pin(pf[kb][s2][qb]);
       }
     if (g0) wait_tile(t + 1);
-    f4_bar();
+    bar();
     if (g0) issue(t + 3);
     mphase(t);
     if (!g0) wait_tile(t + 2);
-    f4_bar();
+    bar();
   }
-  if (g0) f4_bar();
+  if (g0) bar();
   {  // the last tiles' row sums were not checked in the loop
     bool over = false;
 #pragma unroll
@@ -1572,6 +1592,11 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
     }
     bad |= __any(over);
   }
+  if constexpr (ST) {
+    if (stw && (threadIdx.x & 63) == 0)
+      for (int i = 0; i < nst && i < F4_NST; ++i)
+        f4_stamps[(threadIdx.x >> 6) * F4_NST + i] = *(const uint64_t*)(smem + F4_LDS + ((threadIdx.x >> 6) * F4_NST + i) * 8);
+  }
   return bad;
 }
 
@@ -1579,7 +1604,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
 // jumped > ~100 (log2) past mu somewhere in the block it stores NaN flags instead, and flash32's
 // exact pass (flash32_kernel<..., FIX>, launched right after) recomputes the flagged quarters —
 // the exact loop inlined here as well would double the kernel's register pressure.
-template <bool UNITC>
+template <bool UNITC, bool ST = false>
 __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ q, int64_t ldq,
                                          const bf16_t* __restrict__ k, int64_t ldk, const bf16_t* __restrict__ v,
                                          int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads, int64_t sq,
@@ -1654,7 +1679,7 @@ __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ 
                        (uint32_t)((4 * hh + qq) * 16);
 
   f32x16 oacc[2][QB];
-  if (__syncthreads_or(f4_loop<UNITC>(smem, lds0, dma, issuer, g0, skv, qf, oacc, kl0, v0l, v1l, hh, c))) {
+  if (__syncthreads_or(f4_loop<UNITC, ST>(smem, lds0, dma, issuer, g0, skv, qf, oacc, kl0, v0l, v1l, hh, c))) {
     // a score jumped > ~100 (log2) past mu somewhere in the block: no output here; a NaN in
     // element (first query, d 0) of each 256-query quarter tells flash32's exact fix-up pass,
     // launched right after, to recompute that quarter
@@ -1705,13 +1730,13 @@ __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ 
   return false;
 }
 
-template <bool UNITC>
+template <bool UNITC, bool ST = false>
 __global__ __launch_bounds__(F4_NT, 1) void flash40_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
     int64_t sq, int64_t skv, int64_t kv_div, float c, int out_f32) {
-  __shared__ __attribute__((aligned(1024))) char smem[F4_LDS];
-  f4_block<UNITC>(smem, q, ldq, k, ldk, v, ldv, o, ldo, heads, sq, skv, kv_div, c, out_f32);
+  __shared__ __attribute__((aligned(1024))) char smem[F4_LDS + (ST ? F4_NW * F4_NST * 8 : 0)];
+  f4_block<UNITC, ST>(smem, q, ldq, k, ldk, v, ldv, o, ldo, heads, sq, skv, kv_div, c, out_f32);
 }
 
 template <int D>
@@ -1721,13 +1746,19 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
   const float c = scale * 1.4426950408889634f;
   if constexpr (D == 40) {
     // flash40 (ping-pong, LDS-DMA ring): the default for the long self-attention (>= 2 key tiles)
-    if ((g_flash32 == 6 || (g_flash32 == 1 && skv >= 256)) && skv >= 2 * KT && ((uintptr_t)o & 15) == 0 &&
-        ldo % (out_f32 ? 4 : 8) == 0) {
+    if ((g_flash32 == 6 || g_flash32 == 8 || (g_flash32 == 1 && skv >= 256)) && skv >= 2 * KT &&
+        ((uintptr_t)o & 15) == 0 && ldo % (out_f32 ? 4 : 8) == 0) {
       const int64_t nblk = (sq + F4_QWG - 1) / F4_QWG * heads * batch;
       if (nblk > 0x7fffffff) return VD_EINVAL;
       const dim3 grid((unsigned)nblk);
       const dim3 fix((unsigned)((sq + 255) / 256 * heads * batch));
-      if (c == 1.0f) {
+      if (g_flash32 == 8) {  // diagnostic: stamped flash40 (unit c only)
+        if (c != 1.0f) return VD_EUNSUPPORTED;
+        hipLaunchKernelGGL((flash40_kernel<true, true>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,
+                           ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+      } else if (c == 1.0f) {
         hipLaunchKernelGGL((flash40_kernel<true>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,
                            ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
         hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
@@ -2258,12 +2289,22 @@ extern "C" int vd_attention_force_v1(int32_t on) {
 // CU (96 KiB of dynamic LDS: one wave per SIMD — the occupancy probe of DESIGN.md §5), 6 =
 // flash32 with one 32-query block per wave (128 VGPRs, four waves per SIMD), 7 = flash40 (the
 // two-group ping-pong over an LDS-DMA ring, round 3) wherever it applies (>= 2 key tiles), 8 =
-// flash32 only (round 2's default; automatic = flash40 from 4 key tiles, flash32 below).
+// flash32 only (round 2's default; automatic = flash40 from 4 key tiles, flash32 below), 9 =
+// flash40's diagnostic build (barrier stamps of workgroup 0, vd_attention_stamps).
 extern "C" int vd_attention_select(int32_t kernel) {
-  if (kernel < 0 || kernel > 8) return VD_EINVAL;
-  static const int map[9] = {1, 0, 7, 2, 3, 4, 5, 6, 7};
+  if (kernel < 0 || kernel > 9) return VD_EINVAL;
+  static const int map[10] = {1, 0, 7, 2, 3, 4, 5, 6, 7, 8};
   g_flash32 = map[kernel];
   return VD_OK;
+}
+
+// Diagnostic: copy the last stamped flash40 launch's barrier stamps (8 waves x 512 uint64
+// s_memtime values, wave-major) to dst (device memory, n <= 4096 values), stream-ordered.
+extern "C" int vd_attention_stamps(void* dst, int64_t n, vd_stream_t stream) {
+  VD_CHECK_ARG(dst && n > 0 && n <= F4_NW * F4_NST);
+  hipError_t e = hipMemcpyFromSymbolAsync(dst, HIP_SYMBOL(f4_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToDevice,
+                                          (hipStream_t)stream);
+  return e == hipSuccess ? VD_OK : (int)e;
 }
 
 static int attention_entry(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,

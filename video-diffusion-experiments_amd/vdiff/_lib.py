@@ -30,6 +30,7 @@ SIGNATURES = {
     "vd_gemm_select_path": ([c_i32], c_i32),
     "vd_attention_force_v1": ([c_i32], c_i32),
     "vd_attention_select": ([c_i32], c_i32),
+    "vd_attention_stamps": ([c_vp, c_i64, c_vp], c_i32),
     "vd_temporal_force_valu": ([c_i32], c_i32),
     "vd_gemm_ws_bytes": ([c_vp], c_i64),
     "vd_gn_partial": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp], c_i32),

@@ -259,7 +259,7 @@ class AnimateDiffTransformer3D(nn.Module):
         dist = ctx.dist
         gather = dist.gather_gn_partials if dist is not None else None
         hn = ops.group_norm(x.t, B, Fl * hw, self.groups, 1e-6, self.norm._g, self.norm._b, gather=gather,
-                            two_pass=False)
+                            two_pass=False, n_split=Fl * ops.gn_splits_per_frame(hw))
         blk = self.transformer_blocks[0]
         if dist is None:  # norm1 (+ PE by frame) fused into proj_in's epilogue
             h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b, pe=blk.pos_embed._pe,

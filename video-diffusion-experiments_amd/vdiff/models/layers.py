@@ -214,8 +214,9 @@ class GroupNorm(nn.GroupNorm):
     def forward(self, x):
         rows = fmap_rows(x)
         pix = math.prod(x.shape[2:])
-        out = ops.group_norm(rows, x.shape[0], pix, self.num_groups, self.eps, self._g, self._b,
-                             two_pass=x.dim() == 4)
+        video = x.dim() == 5  # the motion norm: frame-aligned splits, as the fused path's
+        out = ops.group_norm(rows, x.shape[0], pix, self.num_groups, self.eps, self._g, self._b, two_pass=not video,
+                             n_split=x.shape[2] * ops.gn_splits_per_frame(x.shape[3] * x.shape[4]) if video else None)
         return rows_fmap(out, tuple(x.shape))
 
 

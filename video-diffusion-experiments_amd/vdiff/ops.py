@@ -171,8 +171,17 @@ def conv3d(x, batch, frames_in, h_in, w_in, w, *, kt=3, ks=3, frames_out=None, t
 def gn_splits(n_inst: int, pix: int) -> int:
     """Pixel splits per instance for vd_gn_partial: ~2048 partial blocks in total, at
     most 256 per instance (the finalize pass combines n_split x C/groups records per
-    group; the motion-module norm has only 2 instances per rank)."""
+    group)."""
     return max(1, min(pix // 16, math.ceil(2048 / n_inst), 256))
+
+
+def gn_splits_per_frame(hw: int) -> int:
+    """Splits per frame of the motion-module norm (instance = a whole video): a function of the
+    frame size alone, so a frame-sharded rank's records for its frames are exactly the
+    unsharded run's records for those frames and the all-gathered set equals the unsharded one
+    record for record — the sharded norm is bit-identical (at F = 16 this is the same 256 / 64
+    splits per video as gn_splits)."""
+    return max(1, min(hw // 16, 16))
 
 
 def gn_partial(x, C, n_inst, pix, n_split, x1=None):
@@ -202,20 +211,21 @@ def gn_apply(x, ss, pix, silu, x1=None, out=None):
     return out
 
 
-def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, gather=None, two_pass=True):
+def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, gather=None, two_pass=True,
+               n_split=None):
     """GroupNorm(+SiLU) over NHWC rows; instance = `pix` consecutive rows.
     Image-instance norms (two_pass): per-group partial records, and an apply that finalizes
     them itself (two launches).  The motion-module norm (two_pass=False: its instance is a
     whole video, so it needs hundreds of splits) runs partial / [gather] / finalize / apply,
-    where `gather(ws) -> ws'` merges the partial statistics across frame-sharded ranks."""
+    where `gather(ws) -> ws'` merges the partial statistics across frame-sharded ranks.
+    Image instances always take the two-launch path, whose splits depend on the image size
+    alone: a frame-sharded rank normalises its images bit-identically to the unsharded run
+    (round 3; the four-launch path was 1-2 us faster on a 2-frame rank's few deep-level
+    instances, tools/gn_bench.py)."""
     C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
-    # two launches win by 2-5 us per norm at 16+ instances or 16k+ rows; on the few small
-    # instances of a 2-frame rank's deep levels the four-launch path is 1-2 us faster
-    # (tools/gn_bench.py)
-    big = n_inst >= 16 or n_inst * pix >= 16384
-    if two_pass and big and gather is None and C <= 2560 and 256 % groups == 0:
+    if two_pass and gather is None and C <= 2560 and 256 % groups == 0:
         return group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=silu, x1=x1)
-    ws = gn_partial(x, C, n_inst, pix, gn_splits(n_inst, pix), x1=x1)
+    ws = gn_partial(x, C, n_inst, pix, n_split or gn_splits(n_inst, pix), x1=x1)
     if gather is not None:
         ws = gather(ws)
     ss = gn_finalize(ws, groups, eps, gamma, beta)
@@ -224,10 +234,12 @@ def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, ga
 
 def group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, out=None):
     """vd_gn_partial_g + vd_gn_apply_g.  Splits: <= 32 per instance (the apply prologue reads
-    splits x groups records), ~2048 partial blocks in all; ~1024 apply blocks in all (tools/gn_bench.py)."""
+    splits x groups records); the split count is a function of the image size alone (the same
+    records whatever the instance count: frame-sharded ranks match the unsharded run bit for bit);
+    ~1024 apply blocks in all (tools/gn_bench.py)."""
     _dev(x, x1, gamma, beta, out)
     C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
-    n_split = max(1, min(pix // 16, math.ceil(2048 / n_inst), 32))
+    n_split = max(1, min(pix // 16, 32))
     ws = torch.empty(n_inst, n_split, groups, 4, device=x.device, dtype=torch.float32)
     x1p, ld1 = (_p(x1), _rows(x1)) if x1 is not None else (None, 0)
     check(lib().vd_gn_partial_g(_p(x), _rows(x), x.shape[1], x1p, ld1, C, n_inst, pix, n_split, groups, _p(ws),
