@@ -1464,6 +1464,11 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   // ran earlier in this phase) — the same values at the same point of the tile order as flash32
   auto decide = [&](int t) {
     if (t == 0) {
+      // tile_max reads the QK^T accumulators through inline asm (v_max3), and hipcc pads no
+      // MFMA -> asm-reader wait states: wait out the last MFMA (8-pass XDL: 12 states) here,
+      // on its own output, so the max never reads a half-written tile (the other accumulators
+      // were written by earlier MFMAs of the same in-order pipe)
+      asm volatile("s_nop 7\n\ts_nop 7" : "+v"(s[1][QB - 1]));
       float tm[QB];
       bool need = true;
 #pragma unroll
@@ -1518,6 +1523,11 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   // key block 1's under d-block 0's MFMAs; the decisions for tile t+1 follow its QK^T
   auto mphase = [&](int t) {
     const bool more = t + 1 < T;
+    // the M wave takes issue priority for its phase: its MFMAs go out every 32 cycles and the
+    // partner's V-phase exp2/packs fill the slots between them (without it the older wave's
+    // VALU stream held the issue port and the two phases ran one after the other: stamps, ~1.6k
+    // cycles per M phase against 896 of MFMA)
+    __builtin_amdgcn_s_setprio(1);
     read_v(t, 1);
     if (more) read_k(t + 1, 0);
     __builtin_amdgcn_sched_barrier(0);
@@ -1530,8 +1540,9 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
     if (more) {
       qk(0);
       qk(1);
-      decide(t + 1);
     }
+    __builtin_amdgcn_s_setprio(0);
+    if (more) decide(t + 1);
   };
   // tile u's DMA: issued at phase 2u-4 (u >= 2), waited for at the end of phase 2u-1
   auto issue = [&](int u) {
