@@ -1465,10 +1465,12 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   auto decide = [&](int t) {
     if (t == 0) {
       // tile_max reads the QK^T accumulators through inline asm (v_max3), and hipcc pads no
-      // MFMA -> asm-reader wait states: wait out the last MFMA (8-pass XDL: 12 states) here,
-      // on its own output, so the max never reads a half-written tile (the other accumulators
-      // were written by earlier MFMAs of the same in-order pipe)
-      asm volatile("s_nop 7\n\ts_nop 7" : "+v"(s[1][QB - 1]));
+      // MFMA -> asm-reader wait states: wait out the last MFMA (8-pass XDL: 12 states) in one
+      // statement that takes EVERY accumulator as an operand, so no v_max3 can be scheduled
+      // ahead of it (a pin on one accumulator let the others' reads race their MFMAs: mu off
+      // by a bf16 step on ~half the rows, run to run)
+      static_assert(QB == 2, "the pin below names the four accumulators");
+      asm volatile("s_nop 7\n\ts_nop 7" : "+v"(s[0][0]), "+v"(s[0][1]), "+v"(s[1][0]), "+v"(s[1][1]));
       float tm[QB];
       bool need = true;
 #pragma unroll
