@@ -1,10 +1,13 @@
-"""Barrier timeline of flash40 (vd_attention_select(9), the stamped diagnostic build): for
-workgroup 0's 8 waves, per phase, the work time (barrier release -> arrival at the next one) and
-the barrier wait (arrival -> release), split by group and by phase kind (V = softmax, M =
-PV + QK^T).  s_memtime ticks = shader clock cycles.  Model-scale inputs, L1 shape.
+"""Phase timeline of flash40 (vd_attention_select(9), the stamped diagnostic build): workgroup
+0's 8 waves record tagged s_memtime stamps (shader-clock cycles; tag in bits 56+):
+1 barrier arrival, 2 release, 3 exps done, 4 V reads issued, 5 DMA issued, 6 PV(db 0) issued,
+7 PV(db 1) issued, 8 QK^T issued, 9 decisions done.  Per group and phase kind (V = softmax, M =
+PV + QK^T), the median cycles of each interval between consecutive stamps.  Model-scale inputs,
+L1 shape (32 images x 8 heads x 4096 x 4096).
 
     python tools/flash40_stamps.py
 """
+import collections
 import math
 import statistics as st
 import sys
@@ -17,6 +20,7 @@ import torch  # noqa: E402
 from vdiff import ops  # noqa: E402
 from vdiff._lib import check, lib  # noqa: E402
 
+NAMES = {1: "arrive", 2: "release", 3: "exps", 4: "Vreads", 5: "DMA", 6: "PV0", 7: "PV1", 8: "QK", 9: "decide"}
 n_img, S, heads, d = 32, 4096, 8, 40
 C = heads * d
 g = torch.Generator(device="cuda").manual_seed(7)
@@ -26,22 +30,31 @@ qkv = qkv.to(torch.bfloat16)
 q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
 lib().vd_attention_select(9)
 for _ in range(5):
-    o = ops.attention(q, k, v, n_img, heads, S, S, d, scale=1.0 / math.log2(math.e))
-buf = torch.zeros(8 * 512, dtype=torch.int64, device="cuda")
+    ops.attention(q, k, v, n_img, heads, S, S, d, scale=1.0 / math.log2(math.e))
+NST = 1024
+buf = torch.zeros(8 * NST, dtype=torch.int64, device="cuda")
 check(lib().vd_attention_stamps(buf.data_ptr(), buf.numel(), torch.cuda.current_stream().cuda_stream), "stamps")
 lib().vd_attention_select(0)
 torch.cuda.synchronize()
-t = buf.cpu().view(8, 512).tolist()
-T = S // 64
-nb = 2 * (2 * T + 3)  # stamps per wave: before/after each of 2T+3 barriers
-for w in range(8):
-    ts = t[w][:nb]
-    work = [ts[2 * i] - ts[2 * i - 1] for i in range(1, nb // 2)]      # release i-1 -> arrival i
-    wait = [ts[2 * i + 1] - ts[2 * i] for i in range(nb // 2)]          # arrival i -> release i
-    # group 0: barrier 0 = prologue, 1 = phase 0 end, then (V, M) pairs; group 1 has the stagger first
-    off = 2 if w < 4 else 3
-    V = work[off - 1::2][:T - 2]
-    M = work[off::2][:T - 2]
-    print(f"wave {w} (group {w // 4}): V work median {st.median(V):6.0f}  M work median {st.median(M):6.0f}  "
-          f"barrier wait median {st.median(wait[3:-3]):6.0f}  total {ts[nb - 1] - ts[0]} cycles, "
-          f"per tile {(ts[nb - 1] - ts[0]) / T:.0f}")
+raw = buf.cpu().view(8, NST).tolist()
+for grp in (0, 1):
+    acc = collections.defaultdict(list)
+    tot = []
+    for w in range(4 * grp, 4 * grp + 4):
+        ev = [((x >> 56) & 0xFF, x & ((1 << 56) - 1)) for x in raw[w] if x]
+        tot.append((ev[-1][1] - ev[0][1]) / (S // 64))
+        phase = []
+        for tag, t in ev:
+            phase.append((tag, t))
+            if tag == 2:  # a phase = from the previous release to this release
+                tags = [p[0] for p in phase]
+                kind = "M" if 6 in tags else ("V" if 3 in tags else None)
+                if kind and len(phase) > 2:
+                    for (a, ta), (b, tb) in zip(phase, phase[1:]):
+                        acc[(kind, f"{NAMES[a]}->{NAMES[b]}")].append(tb - ta)
+                    acc[(kind, "total")].append(phase[-1][1] - phase[0][1])
+                phase = [(tag, t)]
+    print(f"group {grp}: {st.median(tot):.0f} cycles per tile per wave")
+    for key in sorted(acc):
+        vals = acc[key][2:-2] or acc[key]
+        print(f"  {key[0]} {key[1]:18s} median {st.median(vals):6.0f}  (n={len(vals)})")

@@ -1356,7 +1356,7 @@ __device__ __forceinline__ void f4_bar() {  // this wave's LDS reads drained, DM
 // Diagnostic build (ST, vd_attention_select(9)): workgroup 0's waves record s_memtime on both
 // sides of every barrier into LDS and copy them to f4_stamps at the end (vd_attention_stamps):
 // per phase, the work time (release -> arrival) and the barrier wait (arrival -> release).
-constexpr int F4_NST = 512;  // stamps per wave
+constexpr int F4_NST = 1024;  // stamps per wave: (tag << 56) | s_memtime
 __device__ uint64_t f4_stamps[F4_NW * F4_NST];
 
 template <bool UNITC, bool ST = false>
@@ -1365,18 +1365,22 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
                                         uint32_t kl0, uint32_t v0l, uint32_t v1l, int hh, float c) {
   int nst = 0;
   const bool stw = ST && blockIdx.x == 0;
-  auto stamp = [&]() {
+  // tags: 1 barrier arrival, 2 release, 3 exps done, 4 V reads issued, 5 DMA issued, 6 PV(db 0)
+  // issued, 7 PV(db 1) issued, 8 QK^T issued, 9 decisions done
+  auto stamp = [&](uint64_t tag) {
     if constexpr (ST) {
+      __builtin_amdgcn_sched_barrier(0);
       const uint64_t tt = __builtin_amdgcn_s_memtime();
       if (stw && (threadIdx.x & 63) == 0 && nst < F4_NST)
-        *(uint64_t*)(smem + F4_LDS + ((threadIdx.x >> 6) * F4_NST + nst) * 8) = tt;
+        *(uint64_t*)(smem + F4_LDS + ((threadIdx.x >> 6) * F4_NST + nst) * 8) = (tag << 56) | (tt & ((1ull << 56) - 1));
       ++nst;
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
   auto bar = [&]() {
-    stamp();
+    stamp(1);
     f4_bar();
-    stamp();
+    stamp(2);
   };
   using C = F32Cfg<40>;
   constexpr int QB = F4_QB;
@@ -1535,20 +1539,25 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
     __builtin_amdgcn_sched_barrier(0);
     pv(0);
     __builtin_amdgcn_sched_barrier(0);
+    stamp(6);
     if (more) read_k(t + 1, 1);
     __builtin_amdgcn_sched_barrier(0);
     pv(1);
     __builtin_amdgcn_sched_barrier(0);
+    stamp(7);
     if (more) {
       qk(0);
       qk(1);
     }
+    stamp(8);
     __builtin_amdgcn_s_setprio(0);
     if (more) decide(t + 1);
+    stamp(9);
   };
   // tile u's DMA: issued at phase 2u-4 (u >= 2), waited for at the end of phase 2u-1
   auto issue = [&](int u) {
     if (issuer && u < T) f4_issue(dma, lds0, u, skv);
+    stamp(5);
   };
   auto wait_tile = [&](int u) {
     if (issuer && u < T) {
@@ -1578,6 +1587,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
     if (!g0) issue(t + 3);
     softmax();
     __builtin_amdgcn_sched_barrier(0);
+    stamp(3);
     read_v(t, 0);
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -1587,6 +1597,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb) f4_pin(pf[kb][s2][qb]);
       }
+    stamp(4);
     if (g0) wait_tile(t + 1);
     bar();
     if (g0) issue(t + 3);
