@@ -26,6 +26,11 @@ def alphas_cumprod(num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012,
     return torch.cumprod(1.0 - betas, dim=0)
 
 
+def _sqrt(x):
+    """fp32 sqrt, correctly rounded whatever the host's fp32 vector sqrt does (through fp64)."""
+    return torch.sqrt(torch.as_tensor(x).double()).float()
+
+
 def timesteps_leading(n, num_train_timesteps=1000, steps_offset=1):
     ratio = num_train_timesteps // n
     ts = (np.arange(0, n) * ratio).round()[::-1].copy().astype(np.int64)
@@ -38,8 +43,8 @@ def ddim_step(eps, t, x, n_steps, acp, final_alpha_cumprod=None, num_train_times
     prev = t - num_train_timesteps // n_steps
     a_t = acp[t]
     a_p = acp[prev] if prev >= 0 else fa
-    x0 = (x - (1 - a_t) ** 0.5 * eps) / a_t ** 0.5
-    return a_p ** 0.5 * x0 + (1 - a_p) ** 0.5 * eps, x0
+    x0 = (x - _sqrt(1 - a_t) * eps) / _sqrt(a_t)
+    return _sqrt(a_p) * x0 + _sqrt(1 - a_p) * eps, x0
 
 
 def cfg_combine(eps2, g):

@@ -25,12 +25,12 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .ddim_ref import alphas_cumprod, cfg_combine
+from .ddim_ref import _sqrt, alphas_cumprod, cfg_combine
 
 
 def sigmas_train(acp=None):
     acp = alphas_cumprod() if acp is None else acp
-    return ((1 - acp) / acp) ** 0.5
+    return _sqrt((1 - acp) / acp)
 
 
 def set_timesteps(n, num_train_timesteps=1000, acp=None):
@@ -48,7 +48,7 @@ def init_noise_sigma(sigmas):
 
 def scale_model_input(x, sigma):
     sigma = torch.tensor(float(sigma), dtype=torch.float32)
-    return x / ((sigma ** 2 + 1) ** 0.5)
+    return x / _sqrt(sigma ** 2 + 1)
 
 
 def euler_step(eps, x, sigma, sigma_next):

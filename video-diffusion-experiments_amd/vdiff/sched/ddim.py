@@ -39,6 +39,13 @@ DEFAULT_CONFIG = dict(
 )
 
 
+def sqrt32(x: torch.Tensor) -> torch.Tensor:
+    """Correctly rounded fp32 square root (through fp64), i.e. what IEEE fp32 `x ** 0.5` gives.
+    Some hosts' torch fp32 sqrt is off by one ulp on ~20 % of inputs, which would make the
+    scheduler tables depend on the machine."""
+    return torch.sqrt(x.double()).float()
+
+
 class _Cfg(dict):
     def __getattr__(self, k):
         try:
@@ -119,9 +126,10 @@ class DDIMScheduler:
         return a_t, a_p
 
     def coefficients(self, timestep) -> torch.Tensor:
-        """fp32 {sqrt(a_t), sqrt(1-a_t), sqrt(a_prev), sqrt(1-a_prev)} (fp32 torch math, as diffusers)."""
+        """fp32 {sqrt(a_t), sqrt(1-a_t), sqrt(a_prev), sqrt(1-a_prev)}: diffusers' fp32 torch math
+        with every square root correctly rounded (`sqrt32`)."""
         a_t, a_p = self._alphas(timestep)
-        return torch.stack([a_t ** 0.5, (1 - a_t) ** 0.5, a_p ** 0.5, (1 - a_p) ** 0.5]).float()
+        return torch.stack([sqrt32(a_t), sqrt32(1 - a_t), sqrt32(a_p), sqrt32(1 - a_p)]).float()
 
     def coefficient_table(self, timesteps=None) -> torch.Tensor:
         ts = self.timesteps if timesteps is None else timesteps

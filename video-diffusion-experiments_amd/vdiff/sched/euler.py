@@ -19,7 +19,7 @@ import numpy as np
 import torch
 
 from .. import ops
-from .ddim import DEFAULT_CONFIG as _SD15, _Cfg
+from .ddim import DEFAULT_CONFIG as _SD15, _Cfg, sqrt32
 
 EulerDiscreteSchedulerOutput = namedtuple("EulerDiscreteSchedulerOutput", ["prev_sample", "pred_original_sample"])
 
@@ -65,7 +65,7 @@ class EulerDiscreteScheduler:
         self.betas = betas
         self.alphas = 1.0 - betas
         self.alphas_cumprod = torch.cumprod(self.alphas, dim=0)
-        sig = (((1 - self.alphas_cumprod) / self.alphas_cumprod) ** 0.5).numpy()
+        sig = sqrt32((1 - self.alphas_cumprod) / self.alphas_cumprod).numpy()
         self._sigmas_train = sig
         # diffusers' __init__ state (before set_timesteps): the full training schedule
         self.sigmas = torch.from_numpy(np.concatenate([sig[::-1], [0.0]]).astype(np.float32))
@@ -129,7 +129,7 @@ class EulerDiscreteScheduler:
     def input_divisor(self, i: int) -> float:
         """scale_model_input's divisor at step i: (sigma_i^2 + 1) ** 0.5 in fp32 torch math."""
         s = self.sigmas[i]
-        return float((s ** 2 + 1) ** 0.5)
+        return float(sqrt32(s ** 2 + 1))
 
     def scale_model_input(self, sample, timestep):
         if self._step_index is None:
@@ -140,7 +140,7 @@ class EulerDiscreteScheduler:
         """fp32 {sigma_i, sigma_{i+1}, sqrt(sigma_{i+1}^2 + 1), 0} for step index i (the last
         step's next-input divisor is that of sigma = 0, i.e. 1)."""
         s, sn = self.sigmas[i], self.sigmas[i + 1]
-        return torch.stack([s, sn, (sn ** 2 + 1) ** 0.5, torch.zeros(())]).float()
+        return torch.stack([s, sn, sqrt32(sn ** 2 + 1), torch.zeros(())]).float()
 
     def coefficient_table(self, timesteps=None) -> torch.Tensor:
         """Rows for the given schedule timesteps (default: the whole schedule), indexed by
