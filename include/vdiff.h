@@ -183,7 +183,10 @@ int vd_layernorm_select(int32_t multi_row);
  * self-attention, a7 cross-attention).  Row (b, s) of q at q + (b*sq + s)*ldq,
  * head h at column h*d.  K/V batch index = b / kv_div (cross-attention reads the
  * un-repeated encoder_hidden_states projection once per video).
- * d in {32, 40, 64, 80, 128, 160}; flash (online softmax) with bf16 MFMA.
+ * d in {32, 40, 64, 80, 128, 160, 512}; flash (online softmax) with bf16 MFMA.  d = 512
+ * (round 3) is the VAE decoder's single-head mid-block Attention (diffusers AttnProcessor2_0
+ * over the 64x64 latent pixels of each frame): flash512_kernel,
+ * o 16-byte aligned with ldo % 8 == 0 (bf16) / % 4 == 0 (fp32).
  */
 int vd_attention(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                  int64_t ldv, void* o, int64_t ldo, int64_t batch, int32_t heads, int64_t sq,
@@ -204,7 +207,10 @@ int vd_attention_force_v1(int32_t on);
  * steady state, 5 = flash32 at one workgroup per CU (occupancy probe), 6 = flash32 with one
  * 32-query block per wave, 7 = flash40 (round 3: two-group ping-pong over an LDS-DMA ring,
  * bit-identical to flash32) wherever it applies (>= 2 key tiles), 8 = flash32 only, 9 = flash40's
- * stamped diagnostic build. */
+ * stamped diagnostic build; 20 / 21 = the d = 512 kernel (flash512, the VAE mid-block
+ * attention) with each step's K/V DMA issued after its barrier (default) / one row per MFMA
+ * gap of QK^T, 22 = DMA ablation (tile 0 only: WRONG results, timing only) (A/B hooks; the
+ * d = 40 choice is left as it was). */
 int vd_attention_select(int32_t kernel);
 /* Diagnostic hook: copy the barrier stamps (s_memtime, 8 waves x 512, wave-major) that the last
  * flash40 launch made under vd_attention_select(9) to dst (device memory, n <= 4096 uint64). */
@@ -253,9 +259,9 @@ int vd_temporal_attention_rope(const void* q, const void* k, const void* v, int6
  * for frames <= 16 and d in {32, 40, 64, 80, 160}, frames 17..32 and d in {40, 64, 80, 160}). */
 int vd_temporal_force_valu(int32_t on);
 
-/* Row softmax over fp32 scores in log2 units (p = exp2(s - max) / sum, bf16 out):
- * the materialised-score attention of the VAE decoder's single-head (d = 512) mid-block
- * Attention (diffusers AttnProcessor2_0 with upcast softmax).
+/* Row softmax over fp32 scores in log2 units (p = exp2(s - max) / sum, bf16 out): round 2's
+ * materialised-score form of the VAE mid-block attention (now vd_attention with d = 512;
+ * kept for tools/vae_attn_ab.py's A/B and as a general row softmax).
  * rows x cols, cols % 4 == 0, row strides ld_s / ld_p in elements. */
 int vd_softmax_rows(const float* s, int64_t ld_s, int64_t rows, int64_t cols, void* p,
                     int64_t ld_p, vd_stream_t stream);

@@ -41,6 +41,77 @@ def test_softmax_rows_matches_torch(cuda):
                                rtol=2 ** -7, atol=1e-6)
 
 
+def _flash512_emulated(q, k, v, n, S, m_mode):
+    """fp64 restatement of flash512_kernel's arithmetic: per query the offset m is the first
+    32-key tile's row max (m_mode "tile0") or the exact row max (the block's exact rerun,
+    "exact"); e = 2^(s - m), P = bf16(e) for P.V, the row sum l over the unrounded e.  The
+    one freedom left is the last ulps of s (fp32 MFMA accumulation) and of v_exp_f32: where e
+    lies within 2^-15 (relative) of a bf16 rounding midpoint the kernel's P may round the other
+    way; `slack` is exactly what those flips can move O by (as the d = 40 real-valued test)."""
+    outs, slacks = [], []
+    for i in range(n):
+        r = slice(i * S, (i + 1) * S)
+        s = q[r].double() @ k[r].double().T                   # log2 units (scale folded into q)
+        m = s[:, :32].amax(1, keepdim=True) if m_mode == "tile0" else s.amax(1, keepdim=True)
+        e = torch.exp2(s - m)
+        del s
+        p = e.float().to(torch.bfloat16).double()
+        l = e.sum(1, keepdim=True)
+        vd = v[r].double()
+        want = (p @ vd) / l
+        _, ex = torch.frexp(e)
+        ulp = torch.ldexp(torch.full_like(e, 2.0 ** -8), ex)
+        mid = (torch.floor(e / ulp) + 0.5) * ulp
+        dp = torch.where((e - mid).abs() <= e * 2.0 ** -15, ulp, torch.zeros_like(e))
+        slacks.append((dp @ vd.abs()) / l)
+        outs.append(want)
+    return torch.cat(outs), torch.cat(slacks)
+
+
+@pytest.mark.parametrize("S", [4096, 1000, 96])
+def test_flash512_matches_fp64(cuda, S):
+    """vd_attention at d = 512 (flash512_kernel, the VAE mid-block attention) with fp32 output
+    against the fp64 emulation of its rounding points, at the north-star tolerance rtol 1e-3 /
+    atol 1e-4: S = 4096 (the decode's 64x64 latents), a ragged 1000 (last key tile masked, last
+    query block partial) and a single query block (96)."""
+    n, d = 2, 512
+    g = torch.Generator(device=cuda).manual_seed(11)
+    qkv = torch.randn(n * S, 3 * d, device=cuda, generator=g)
+    qkv[:, :d] *= 0.06   # scores of a few log2 units, as the model's folded q gives
+    qkv = qkv.to(torch.bfloat16)
+    q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
+    scale = 1.0 / np.log2(np.e)
+    got = ops.attention(q, k, v, n, 1, S, S, d, scale=scale, out_f32=True).double().cpu()
+    want, slack = _flash512_emulated(q.cpu(), k.cpu(), v.cpu(), n, S, "tile0")
+    err = (got - want).abs()
+    print(f"flash512 S={S}: max |O - O_ref(bf16 P)| {err.max().item():.2e}, max flip allowance "
+          f"{slack.max().item():.2e}, |O| max {want.abs().max().item():.3f}")
+    assert torch.all(err <= 1e-4 + 1e-3 * want.abs() + slack), (err - 1e-3 * want.abs() - slack).max().item()
+    # the bf16-output kernel rounds the same values once
+    got16 = ops.attention(q, k, v, n, 1, S, S, d, scale=scale).double().cpu()
+    assert torch.all((got16 - want).abs() <= 1e-4 + 2 ** -8 * want.abs() + slack)
+
+
+def test_flash512_exact_rerun(cuda):
+    """A key far above every query's first-tile max (+40 log2 units: P would reach 2^40 against
+    the fast pass's fixed offset) sends the block through the exact rerun (QK-only max sweep,
+    then the flash sweep with the true row max); the result matches the emulation with m =
+    the exact row max."""
+    n, S, d = 1, 512, 512
+    g = torch.Generator(device=cuda).manual_seed(5)
+    u = torch.randn(d, device=cuda, generator=g)
+    u = u / u.norm()
+    q = torch.randn(n * S, d, device=cuda, generator=g) * 0.02 + u
+    k = torch.randn(n * S, d, device=cuda, generator=g) * 0.02
+    k[300] = 40.0 * u
+    v = torch.randn(n * S, d, device=cuda, generator=g)
+    q, k, v = (t.to(torch.bfloat16) for t in (q, k, v))
+    got = ops.attention(q, k, v, n, 1, S, S, d, scale=1.0 / np.log2(np.e), out_f32=True).double().cpu()
+    want, slack = _flash512_emulated(q.cpu(), k.cpu(), v.cpu(), n, S, "exact")
+    err = (got - want).abs()
+    assert torch.all(err <= 1e-4 + 1e-3 * want.abs() + slack), (err - 1e-3 * want.abs() - slack).max().item()
+
+
 def test_vae_attention_block_matches_oracle(cuda):
     C, n, h, w = 64, 2, 16, 16
     g = torch.Generator().manual_seed(3)

@@ -2315,7 +2315,13 @@ extern "C" int vd_attention_force_v1(int32_t on) {
 // two-group ping-pong over an LDS-DMA ring, round 3) wherever it applies (>= 2 key tiles), 8 =
 // flash32 only (round 2's default; automatic = flash40 from 4 key tiles, flash32 below), 9 =
 // flash40's diagnostic build (barrier stamps of workgroup 0, vd_attention_stamps).
+extern int g_a5_var;  // attention_d512.hip
+
 extern "C" int vd_attention_select(int32_t kernel) {
+  if (kernel >= 20 && kernel <= 22) {  // d = 512 (flash512): DMA placement A/B, 22 = ablation
+    g_a5_var = kernel - 20;
+    return VD_OK;
+  }
   if (kernel < 0 || kernel > 9) return VD_EINVAL;
   static const int map[10] = {1, 0, 7, 2, 3, 4, 5, 6, 7, 8};
   g_flash32 = map[kernel];
@@ -2330,6 +2336,11 @@ extern "C" int vd_attention_stamps(void* dst, int64_t n, vd_stream_t stream) {
                                           (hipStream_t)stream);
   return e == hipSuccess ? VD_OK : (int)e;
 }
+
+// attention_d512.hip: the VAE mid-block attention (d = 512)
+int launch_flash512(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
+                    int64_t ldo, int64_t batch, int heads, int64_t sq, int64_t skv, int64_t kv_div, float scale,
+                    hipStream_t s, int out_f32);
 
 static int attention_entry(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                             int64_t ldv, void* o, int64_t ldo, int64_t batch, int32_t heads,
@@ -2349,6 +2360,7 @@ static int attention_entry(const void* q, int64_t ldq, const void* k, int64_t ld
     case 80: return launch_flash<80>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
     case 128: return launch_flash<128>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
     case 160: return launch_flash<160>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
+    case 512: return launch_flash512(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
     default: return VD_EUNSUPPORTED;
   }
 }

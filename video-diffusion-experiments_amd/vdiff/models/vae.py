@@ -14,11 +14,11 @@ bf16 rows over (frame, y, x), and each op is a vdiff kernel:
   * every conv (3x3, nearest-x2 upsample folded into the loader, 1x1 shortcut) is the
     implicit-GEMM MFMA kernel with bias / residual fused into its epilogue;
   * GroupNorm(+SiLU) is the partial / finalize / apply trio of the UNet;
-  * the single-head (d = 512) mid-block attention runs on materialised scores:
-    q,k = one GEMM over the normed rows (softmax scale * log2 e folded into q); V^T is
-    produced directly by GEMM(W_v, rows) so the P.V GEMM needs no transpose (v's bias
-    moves to the P.V epilogue: softmax rows sum to 1); S = q.k^T per frame in fp32;
-    P = vd_softmax_rows(S) in bf16; O = P.V^T^T + b_v; out = O.W_o^T + b_o + x.
+  * the single-head (d = 512) mid-block attention: q,k,v = one GEMM over the normed rows
+    (softmax scale * log2 e folded into q's weight and bias), then ONE flash pass over every
+    frame (vd_attention with d = 512 -> flash512_kernel, csrc/attention_d512.hip: no score
+    matrix in memory; round 2 materialised a 64 MB fp32 S per frame and ran GEMM ->
+    vd_softmax_rows -> GEMM), out = O.W_o^T + b_o + x.
 """
 from __future__ import annotations
 
@@ -103,23 +103,20 @@ class VAEAttention(nn.Module):
     def prepare(self):
         c = self.channels ** -0.5 * math.log2(math.e)  # softmax scale in log2 units, folded into q
         self._gg, self._gb = f32(self.group_norm.weight), f32(self.group_norm.bias)
-        self._wqk = bf(torch.cat([self.to_q.weight.float() * c, self.to_k.weight.float()], 0))
-        self._bqk = f32(torch.cat([self.to_q.bias.float() * c, self.to_k.bias.float()], 0))
-        self._wv, self._bv = bf(self.to_v.weight), f32(self.to_v.bias)
+        self._wqkv = bf(torch.cat([self.to_q.weight.float() * c, self.to_k.weight.float(),
+                                   self.to_v.weight.float()], 0))
+        self._bqkv = f32(torch.cat([self.to_q.bias.float() * c, self.to_k.bias.float(),
+                                    self.to_v.bias.float()], 0))
         self._wo, self._bo = bf(self.to_out[0].weight), f32(self.to_out[0].bias)
 
     def forward(self, x: Act) -> Act:
         C, hw = self.channels, x.h * x.w
         n = ops.group_norm(x.t, x.n, hw, self.groups, self.eps, self._gg, self._gb)
-        qk = ops.gemm(n, self._wqk, bias=self._bqk)                 # [n*hw, 2C]
-        vt = ops.gemm(self._wv, n)                                 # V^T [C, n*hw] (bias in P.V)
-        o = torch.empty(x.n * hw, C, device=n.device, dtype=torch.bfloat16)
-        s = torch.empty(hw, hw, device=n.device, dtype=torch.float32)
-        for i in range(x.n):
-            r = slice(i * hw, (i + 1) * hw)
-            ops.gemm(qk[r, :C], qk[r, C:], out=s, out_f32=True)     # S = q.k^T (log2 units)
-            p = ops.softmax_rows(s)
-            ops.gemm(p, vt[:, r], bias=self._bv, out=o[r])          # O = P.V + b_v
+        qkv = ops.gemm(n, self._wqkv, bias=self._bqkv)             # [n*hw, 3C], q pre-scaled
+        # one flash pass over every frame (vd_attention d = 512: flash512_kernel); the scale
+        # (C^-1/2 log2 e) is already in q, so the kernel's exp2 argument is the score itself
+        o = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], x.n, 1, hw, hw, C,
+                          scale=1.0 / math.log2(math.e))
         out = ops.gemm(o, self._wo, bias=self._bo, res=x.t)
         return Act(out, x.n, x.h, x.w)
 
