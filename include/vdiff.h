@@ -208,8 +208,8 @@ int vd_attention_force_v1(int32_t on);
  * 32-query block per wave, 7 = flash40 (round 3: two-group ping-pong over an LDS-DMA ring,
  * bit-identical to flash32) wherever it applies (>= 2 key tiles), 8 = flash32 only, 9 = flash40's
  * stamped diagnostic build; 20 / 21 = the d = 512 kernel (flash512, the VAE mid-block
- * attention) with each step's K/V DMA issued after its barrier (default) / one row per MFMA
- * gap of QK^T, 22 = DMA ablation (tile 0 only: WRONG results, timing only) (A/B hooks; the
+ * attention) with K two tiles ahead in a 3-slot LDS ring and V one ahead / K and V one tile
+ * ahead (the default), 22 = DMA ablation (tile 0 only: WRONG results, timing only) (A/B hooks; the
  * d = 40 choice is left as it was). */
 int vd_attention_select(int32_t kernel);
 /* Diagnostic hook: copy the barrier stamps (s_memtime, 8 waves x 512, wave-major) that the last

@@ -930,7 +930,8 @@ def test_ddim_cfg_step_matches_oracle(cuda):
     eps_rows = torch.randn(2 * Fr * H * W, 4, device=cuda)
     t, n = 961, 50
     prev = t - 1000 // n
-    coef = torch.stack([acp[t] ** 0.5, (1 - acp[t]) ** 0.5, acp[prev] ** 0.5, (1 - acp[prev]) ** 0.5]).float()
+    sq = ddim_ref._sqrt  # correctly rounded fp32 sqrt, as the product host tables
+    coef = torch.stack([sq(acp[t]), sq(1 - acp[t]), sq(acp[prev]), sq(1 - acp[prev])]).float()
     x = lat.clone()
     x0 = torch.empty_like(x)
     nxt = torch.empty(2 * Fr * H * W, 8, device=cuda, dtype=BF)

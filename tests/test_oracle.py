@@ -144,7 +144,7 @@ def test_euler_product_scheduler_matches_oracle_tables():
     x = torch.randn(4, 8)
     y = s.scale_model_input(x, s.timesteps[0])
     assert s.step_index == 0
-    torch.testing.assert_close(y, x / float((s.sigmas[0] ** 2 + 1) ** 0.5), rtol=0, atol=0)
+    torch.testing.assert_close(y, x / float(torch.sqrt((s.sigmas[0] ** 2 + 1).double()).float()), rtol=0, atol=0)
     assert s.index_for_timestep(s.timesteps[3]) == 3 and s.order == 1
     with pytest.raises(ValueError):
         s.index_for_timestep(123.456)

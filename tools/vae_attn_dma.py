@@ -1,6 +1,6 @@
-"""flash512 (d = 512 VAE attention) DMA-placement A/B: vd_attention_select(20 / 21 / 22) = each
-step's K/V DMA right after its barrier / one row per MFMA gap of QK^T / none after tile 0 (the
-ablation: wrong results, timing only), 16 frames x S 4096, interleaved rounds."""
+"""flash512 (d = 512 VAE attention) DMA A/B: vd_attention_select(20 / 21 / 22) = K two tiles
+ahead in a 3-slot ring, V one ahead / K and V one tile ahead (2 + 2 slots, the default) / no DMA
+after tile 0 (the ablation: wrong results, timing only), 16 frames x S 4096, interleaved rounds."""
 import math
 import sys
 from pathlib import Path
@@ -34,7 +34,7 @@ for _ in range(7):
         e1.record()
         e1.synchronize()
         res[pd].append(e0.elapsed_time(e1) / 5)
-lib().vd_attention_select(20)
+lib().vd_attention_select(21)
 for pd, ms in res.items():
     ms = sorted(ms)
     med = ms[len(ms) // 2]

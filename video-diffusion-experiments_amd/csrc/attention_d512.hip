@@ -37,7 +37,7 @@ constexpr int A5_D = 512, A5_NT = 256, A5_QW = 32, A5_QWG = 4 * A5_QW, A5_KT = 3
 constexpr int A5_ROW = A5_D * 2;            // bytes per K / V row
 constexpr int A5_TILE = A5_KT * A5_ROW;     // 32 KiB
 constexpr int A5_BUF = 2 * A5_TILE;         // K tile + V tile
-constexpr int A5_LDS = 2 * A5_BUF;          // double-buffered: 128 KiB
+constexpr int A5_LDS = 5 * A5_TILE;         // K ring of 3 + V ring of 2 slots: 160 KiB
 
 // XOR swizzles of the 16-byte chunk index inside each 256-byte group of a 1 KiB row.
 // K: rows r = 0..15 of a b128 lane group read the same chunk -> spread by r & 15.
@@ -75,9 +75,11 @@ __device__ __forceinline__ float a5_partner(float x) {  // the value of lane l ^
   return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
 }
 
-// PD: LDS fragment reads issued PD MFMAs ahead; DV (A/B): 0 = the step's DMA issued after its
-// barrier, 1 = one DMA row per MFMA gap of QK^T, 2 = no DMA after the first tile (ablation only:
-// wrong results, measures what the DMA costs)
+// PD: LDS fragment reads issued PD MFMAs ahead; DV (A/B): 1 = K and V one tile ahead in 2 + 2
+// slots (the default), 0 = K two tiles ahead in a 3-slot ring and V one ahead (measured 15 %
+// SLOWER: 608 vs 529 us at 16 x 4096, tools/vae_attn_dma.py), 2 = no DMA after the first tile
+// (ablation only: wrong results; 439 us — the LDS-DMA issue, ~60 cycles per 1 KiB piece and 16
+// pieces per wave per tile, is the kernel's largest non-MFMA cost)
 template <bool RAGGED, int PD, int DV = 0>
 __global__ __launch_bounds__(A5_NT, 1) void flash512_kernel(const bf16_t* __restrict__ q, int64_t ldq,
                                                             const bf16_t* __restrict__ k, int64_t ldk,
@@ -106,9 +108,12 @@ __global__ __launch_bounds__(A5_NT, 1) void flash512_kernel(const bf16_t* __rest
   const uint32_t ldkb = (uint32_t)ldk * 2, ldvb = (uint32_t)ldv * 2;
   const u32x4_5 rk = a5_rsrc(kb_ptr, (uint32_t)(skv - 1) * ldkb + A5_ROW);
   const u32x4_5 rv = a5_rsrc(vb_ptr, (uint32_t)(skv - 1) * ldvb + A5_ROW);
-  // LDS: K slots at 0 / 32 KiB, V slots at 64 / 96 KiB (tile t in slot t & 1)
+  // LDS slots of 32 KiB: DV 0 (default) K(t) in slot t % 3 (0 / 32 / 64 KiB) and V(t) in slot
+  // 3 + (t & 1) (96 / 128 KiB): K streams two tiles ahead, V one; DV 1 / 2: two slots each
+  auto ks_off = [&](int t) -> uint32_t { return (uint32_t)(DV == 0 ? t % 3 : (t & 1)) * A5_TILE; };
+  auto vs_off = [&](int t) -> uint32_t { return (uint32_t)(DV == 0 ? 3 + (t & 1) : 2 + (t & 1)) * A5_TILE; };
   auto issue_k = [&](int t) {  // rows past skv: every byte out of the buffer's range -> zeros
-    const uint32_t key0 = (uint32_t)t * A5_KT, kl = lds0 + (uint32_t)(t & 1) * A5_TILE;
+    const uint32_t key0 = (uint32_t)t * A5_KT, kl = lds0 + ks_off(t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint32_t r = (uint32_t)(8 * wave + j);
@@ -116,15 +121,15 @@ __global__ __launch_bounds__(A5_NT, 1) void flash512_kernel(const bf16_t* __rest
     }
   };
   auto issue_v = [&](int t) {
-    const uint32_t key0 = (uint32_t)t * A5_KT, vl = lds0 + (uint32_t)(2 + (t & 1)) * A5_TILE;
+    const uint32_t key0 = (uint32_t)t * A5_KT, vl = lds0 + vs_off(t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint32_t r = (uint32_t)(8 * wave + j);
       a5_dma(rv, vl + r * A5_ROW, (key0 + r) * ldvb + 16u * ((uint32_t)lane ^ a5_vswz(r)));
     }
   };
-  auto kslot = [&](int t) { return (const char*)smem + (t & 1) * A5_TILE; };
-  auto vslot = [&](int t) { return (const char*)smem + (2 + (t & 1)) * A5_TILE; };
+  auto kslot = [&](int t) { return (const char*)smem + ks_off(t); };
+  auto vslot = [&](int t) { return (const char*)smem + vs_off(t); };
 
   // ---- Q'^T fragments (B operand of S^T = K.Q^T): lane holds Q[q0 + r32][16 ks + 8 hh .. +7]
   const int64_t qi = q0 + r32;
@@ -159,14 +164,15 @@ __global__ __launch_bounds__(A5_NT, 1) void flash512_kernel(const bf16_t* __rest
   const int T = (int)((skv + A5_KT - 1) / A5_KT);
   // one barrier per step: this wave's DMAs of the previous step landed (vmcnt(0)), every
   // wave's LDS reads of the step before retired (lgkmcnt(0)) — the slots they read are free
-  auto sync = [&]() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  auto sync = [&](bool keep8 = false) {  // keep8: the youngest 8 DMAs (one K tile) stay in flight
+    if (keep8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
   // S^T = K'.Q'^T of tile t: 32 MFMAs, K' fragments two ahead; keys past skv -> -inf
-  auto qk = [&](const char* kl, int t, int u) {  // u >= 0: DMA K(u)/V(u) between the MFMAs
+  auto qk = [&](const char* kl, int t, int) {
     f32x16 s;
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = 0.f;
@@ -180,23 +186,11 @@ __global__ __launch_bounds__(A5_NT, 1) void flash512_kernel(const bf16_t* __rest
       const bf16x8 kc = kw[ks % PD];
       if (ks + PD < 32) kw[ks % PD] = kfrag(ks + PD);
       s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kc, qf[ks], s, 0, 0, 0);
-      if (u >= 0 && ks < 16) {  // one DMA row per MFMA gap (the asm stays where it is written)
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t key0 = (uint32_t)u * A5_KT, r = (uint32_t)(8 * wave + (ks & 7));
-        if (ks < 8)
-          a5_dma(rk, lds0 + (uint32_t)(u & 1) * A5_TILE + r * A5_ROW, (key0 + r) * ldkb + 16u * ((uint32_t)lane ^ a5_kswz(r)));
-        else
-          a5_dma(rv, lds0 + (uint32_t)(2 + (u & 1)) * A5_TILE + r * A5_ROW,
-                 (key0 + r) * ldvb + 16u * ((uint32_t)lane ^ a5_vswz(r)));
-        __builtin_amdgcn_sched_barrier(0);
-      }
     }
-    if (u < 0) {
 #pragma unroll
-      for (int ks = 0; ks < 32; ++ks) {
-        if (ks + PD < 32) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      }
+    for (int ks = 0; ks < 32; ++ks) {
+      if (ks + PD < 32) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     }
     if (RAGGED && t == T - 1) {
       const int64_t kbase = (int64_t)t * A5_KT + 4 * hh;
@@ -275,23 +269,46 @@ __global__ __launch_bounds__(A5_NT, 1) void flash512_kernel(const bf16_t* __rest
       for (int i = 0; i < 16; ++i) oacc[db][i] = 0.f;
     lsum = 0.f;
     sync();  // (the exact rerun's max sweep may still be reading K slot 0 in other waves)
-    issue_k(0);
-    issue_v(0);
-    for (int t = 0; t < T; ++t) {
-      sync();
-      if (t + 1 < T && DV == 0) {
-        issue_k(t + 1);
-        issue_v(t + 1);
+    if (DV == 0) {
+      // step t: K(t), V(t) landed (only K(t+1) may still fly); DMA V(t+1), then K(t+2)
+      issue_v(0);
+      issue_k(0);
+      if (T > 1) issue_k(1);
+      for (int t = 0; t < T; ++t) {
+        sync(t + 1 < T);
+        if (t + 1 < T) issue_v(t + 1);
+        if (t + 2 < T) issue_k(t + 2);
+        const f32x16 s = qk(kslot(t), t, -1);
+        bf16x8 pf[2];
+        softmax(s, fast, t == 0, pf);
+        pv(vslot(t), pf);
       }
-      const f32x16 s = qk(kslot(t), t, DV == 1 && t + 1 < T ? t + 1 : -1);
-      bf16x8 pf[2];
-      softmax(s, fast, t == 0, pf);
-      pv(vslot(t), pf);
+    } else {
+      issue_k(0);
+      issue_v(0);
+      for (int t = 0; t < T; ++t) {
+        sync();
+        if (t + 1 < T && DV == 1) {
+          issue_k(t + 1);
+          issue_v(t + 1);
+        }
+        const f32x16 s = qk(kslot(t), t, -1);
+        bf16x8 pf[2];
+        softmax(s, fast, t == 0, pf);
+        pv(vslot(t), pf);
+      }
     }
   };
 
   sweep(true);
-  if (__syncthreads_or(bad)) {
+  // the block-wide OR of `bad` through LDS (__syncthreads_or takes 256 B of LDS of its own, and
+  // the rings use all 160 KiB): every wave is past its last LDS read after the first barrier
+  sync();
+  if (lane == 0) *(volatile uint32_t*)(smem + 4 * wave) = __any(bad) ? 1u : 0u;
+  sync();
+  const bool any_bad = (*(volatile const uint32_t*)(smem) | *(volatile const uint32_t*)(smem + 4) |
+                        *(volatile const uint32_t*)(smem + 8) | *(volatile const uint32_t*)(smem + 12)) != 0;
+  if (any_bad) {
     // rare: a row max jumped > 32 (log2) past the first tile's somewhere in the block.  The
     // block reruns exactly: a QK-only sweep for the exact row max, then the flash sweep.
     m = -INFINITY;
@@ -337,7 +354,7 @@ __global__ __launch_bounds__(A5_NT, 1) void flash512_kernel(const bf16_t* __rest
 
 }  // namespace
 
-int g_a5_var = 0;  // DMA placement (vd_attention_select(20 + DV): A/B hook, 22 = ablation)
+int g_a5_var = 1;  // DMA ring (vd_attention_select(20 + DV): A/B hook, 22 = ablation)
 
 // d = 512 (the VAE mid-block attention) for attention_entry (attention.hip).
 int launch_flash512(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
