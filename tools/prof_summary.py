@@ -40,7 +40,7 @@ for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:40]:
 
 # the same kernel inside the step (the L1 spatial self-attention: flash40<unit-c>; before round 3
 # flash32<40, unit-c> launches longer than 300 us, the shorter ones being its text cross-attention)
-ROOF = "flash40_kernel<true>" if any("flash40_kernel<true>" in r["Kernel_Name"] for r in rows) else "flash32_kernel<40, true"
+ROOF = "flash40_kernel<true," if any("flash40_kernel<true," in r["Kernel_Name"] for r in rows) else "flash32_kernel<40, true, false, 2>"
 ins = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win if ROOF in r["Kernel_Name"]]
 ins = [x for x in ins if x > 300e3]
 if ins:
