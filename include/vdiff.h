@@ -209,8 +209,10 @@ int vd_attention_force_v1(int32_t on);
  * bit-identical to flash32) wherever it applies (>= 2 key tiles), 8 = flash32 only, 9 = flash40's
  * stamped diagnostic build; 20 / 21 = the d = 512 kernel (flash512, the VAE mid-block
  * attention) with K two tiles ahead in a 3-slot LDS ring and V one ahead / K and V one tile
- * ahead (the default), 22 = DMA ablation (tile 0 only: WRONG results, timing only) (A/B hooks; the
- * d = 40 choice is left as it was). */
+ * ahead (the default), 22 = DMA ablation (tile 0 only: WRONG results, timing only); 25 / 26 /
+ * 27 = flash40's K/V LDS-DMA issued by waves 4-7 only, in their softmax phase / by waves 0-5
+ * (the default) / by waves 0-3 only, in their MFMA phase (A/B hooks; the d = 40 choice is left
+ * as it was). */
 int vd_attention_select(int32_t kernel);
 /* Diagnostic hook: copy the barrier stamps (s_memtime, 8 waves x 512, wave-major) that the last
  * flash40 launch made under vd_attention_select(9) to dst (device memory, n <= 4096 uint64). */

@@ -32,6 +32,7 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int KT = 64;   // keys per tile
+int g_f4_g1 = 0;         // flash40 LDS-DMA issued by the second wave group only (A/B, vd_attention_select 25/26)
 int g_flash32 = 1;       // d = 40: 1 = automatic (flash40 for >= 4 key tiles, else flash32), 7 = flash32 only,
                          // 6 = flash40 wherever it applies, 8 = flash40 stamped (diagnostic),
                          // 2 = flash32pp (8-wave pipeline), 0 = flash_attn 16x16x32
@@ -1312,19 +1313,20 @@ __device__ __forceinline__ void f4_dma(u32x4 rs, uint32_t lds, uint32_t voff) {
 // This wave's two pieces of every tile (waves 0-5; piece p = 2 wave + i): 0-4 = K chunk p of
 // the 64 keys (lane = key), 5 = the K' ones chunk, 6-9 = V d 0..31 of keys 16 (p-6) + lane/4
 // (lane % 4 = chunk), 10 = V d 32..39, 11 = the V ones chunk.
-struct F4Dma {
-  u32x4 rs[2];
-  uint32_t voff[2];   // lane part of the byte offset (row r, column chunk), or 0 for a ones chunk
-  uint32_t step[2];   // bytes per key (0 for a ones chunk)
-  uint32_t row[2];    // the lane's key inside the tile
-  uint32_t lds[2];    // byte offset of the piece inside a slot
+struct F4Dma {  // up to 3 pieces per issuing wave (G1: waves 4-7 issue all 12)
+  u32x4 rs[3];
+  uint32_t voff[3];   // lane part of the byte offset (row r, column chunk), or 0 for a ones chunk
+  uint32_t step[3];   // bytes per key (0 for a ones chunk)
+  uint32_t row[3];    // the lane's key inside the tile
+  uint32_t lds[3];    // byte offset of the piece inside a slot
 };
 
+template <int NP>
 __device__ __forceinline__ void f4_issue(const F4Dma& m, uint32_t lds0, int t, int64_t skv) {
   const uint32_t key0 = (uint32_t)t * KT;
   const uint32_t slot = lds0 + (uint32_t)(t % F4_RING) * F4_SLOT;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < NP; ++i) {
     // data: (key0 + row) * ld + col, past skv out of range -> zeros; ones chunk: offset 0, or 16
     // (out of its 16-byte range -> zeros) for a key past skv
     const uint32_t off = m.step[i] ? m.voff[i] + key0 * m.step[i] : ((int64_t)(key0 + m.row[i]) < skv ? 0u : 16u);
@@ -1344,7 +1346,9 @@ __device__ __forceinline__ void f4_pin(T& x) {
 
 template <int N>
 __device__ __forceinline__ void f4_wait_vm() {
-  if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 __device__ __forceinline__ void f4_bar() {  // this wave's LDS reads drained, DMA left in flight
@@ -1359,7 +1363,7 @@ __device__ __forceinline__ void f4_bar() {  // this wave's LDS reads drained, DM
 constexpr int F4_NST = 1024;  // stamps per wave: (tag << 56) | s_memtime
 __device__ uint64_t f4_stamps[F4_NW * F4_NST];
 
-template <bool UNITC, bool ST = false>
+template <bool UNITC, bool ST = false, int G1 = 0>
 __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F4Dma& dma, bool issuer,
                                         bool g0, int64_t skv, bf16x8 (&qf)[F4_QB][3], f32x16 (&oacc)[2][F4_QB],
                                         uint32_t kl0, uint32_t v0l, uint32_t v1l, int hh, float c) {
@@ -1556,12 +1560,18 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   };
   // tile u's DMA: issued at phase 2u-4 (u >= 2), waited for at the end of phase 2u-1
   auto issue = [&](int u) {
-    if (issuer && u < T) f4_issue(dma, lds0, u, skv);
+    if (issuer && u < T) {
+      if (G1 == 3 && !g0) f4_issue<1>(dma, lds0, u, skv);
+      else f4_issue<G1 == 1 || G1 == 2 ? 3 : 2>(dma, lds0, u, skv);
+    }
     stamp(5);
   };
   auto wait_tile = [&](int u) {
     if (issuer && u < T) {
-      if (u + 1 < T) f4_wait_vm<2>();
+      if (u + 1 < T) {
+        if (G1 == 3 && !g0) f4_wait_vm<1>();
+        else f4_wait_vm<G1 == 1 || G1 == 2 ? 3 : 2>();
+      }
       else f4_wait_vm<0>();
     }
   };
@@ -1628,7 +1638,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
 // jumped > ~100 (log2) past mu somewhere in the block it stores NaN flags instead, and flash32's
 // exact pass (flash32_kernel<..., FIX>, launched right after) recomputes the flagged quarters —
 // the exact loop inlined here as well would double the kernel's register pressure.
-template <bool UNITC, bool ST = false>
+template <bool UNITC, bool ST = false, int G1 = 0>
 __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ q, int64_t ldq,
                                          const bf16_t* __restrict__ k, int64_t ldk, const bf16_t* __restrict__ v,
                                          int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads, int64_t sq,
@@ -1667,15 +1677,20 @@ __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ 
 
   // LDS-DMA pieces (waves 0-5)
   F4Dma dma;
-  const bool issuer = wave < 6;
+  // LDS-DMA issuers: waves 0-5 with two pieces each (G1 = 0), or one group's four waves with
+  // three each: G1 = 1 the second group (waves 4-7, in its softmax phase: measured 930 vs 805 us),
+  // G1 = 2 the first group (waves 0-3, in its PV / QK^T phase: 912 us), G1 = 3 all eight waves
+  // (waves 0-3 two pieces each in their M phase, waves 4-7 one each in their V phase)
+  const bool issuer = G1 == 1 ? wave >= 4 : (G1 == 2 ? wave < 4 : (G1 == 3 ? true : wave < 6));
   {
     const uint32_t ldkb = (uint32_t)ldk * 2, ldvb = (uint32_t)ldv * 2;
     const u32x4 rk = f4_rsrc(kb_ptr, (uint32_t)(skv - 1) * ldkb + 2 * D);
     const u32x4 rv = f4_rsrc(vb_ptr, (uint32_t)(skv - 1) * ldvb + 2 * D);
     const u32x4 r1 = f4_rsrc(f4_ones, 16);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int p = 2 * wave + i;
+    for (int i = 0; i < (G1 == 1 || G1 == 2 ? 3 : 2); ++i) {
+      const int p = G1 == 1 ? 3 * (wave - 4) + i
+                            : (G1 == 2 ? 3 * wave + i : (G1 == 3 && wave >= 4 ? 8 + (wave - 4) : 2 * wave + i));
       uint32_t row = lane, col = 0, step = 0, lds = 0;
       u32x4 rs = r1;
       if (p < 5) {
@@ -1703,7 +1718,7 @@ __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ 
                        (uint32_t)((4 * hh + qq) * 16);
 
   f32x16 oacc[2][QB];
-  if (__syncthreads_or(f4_loop<UNITC, ST>(smem, lds0, dma, issuer, g0, skv, qf, oacc, kl0, v0l, v1l, hh, c))) {
+  if (__syncthreads_or(f4_loop<UNITC, ST, G1>(smem, lds0, dma, issuer, g0, skv, qf, oacc, kl0, v0l, v1l, hh, c))) {
     // a score jumped > ~100 (log2) past mu somewhere in the block: no output here; a NaN in
     // element (first query, d 0) of each 256-query quarter tells flash32's exact fix-up pass,
     // launched right after, to recompute that quarter
@@ -1754,13 +1769,13 @@ __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ 
   return false;
 }
 
-template <bool UNITC, bool ST = false>
+template <bool UNITC, bool ST = false, int G1 = 0>
 __global__ __launch_bounds__(F4_NT, 1) void flash40_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
     int64_t sq, int64_t skv, int64_t kv_div, float c, int out_f32) {
   __shared__ __attribute__((aligned(1024))) char smem[F4_LDS + (ST ? F4_NW * F4_NST * 8 : 0)];
-  f4_block<UNITC, ST>(smem, q, ldq, k, ldk, v, ldv, o, ldo, heads, sq, skv, kv_div, c, out_f32);
+  f4_block<UNITC, ST, G1>(smem, q, ldq, k, ldk, v, ldv, o, ldo, heads, sq, skv, kv_div, c, out_f32);
 }
 
 template <int D>
@@ -1780,6 +1795,24 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
         if (c != 1.0f) return VD_EUNSUPPORTED;
         hipLaunchKernelGGL((flash40_kernel<true, true>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,
                            ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+      } else if (c == 1.0f && g_f4_g1 == 3) {
+        hipLaunchKernelGGL((flash40_kernel<true, false, 3>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
+                           out_f32);
+        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+      } else if (c == 1.0f && g_f4_g1 == 2) {
+        hipLaunchKernelGGL((flash40_kernel<true, false, 2>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
+                           out_f32);
+        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+      } else if (c == 1.0f && g_f4_g1 == 1) {
+        hipLaunchKernelGGL((flash40_kernel<true, false, 1>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
+                           out_f32);
         hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                            (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
       } else if (c == 1.0f) {
@@ -2318,6 +2351,10 @@ extern "C" int vd_attention_force_v1(int32_t on) {
 extern int g_a5_var;  // attention_d512.hip
 
 extern "C" int vd_attention_select(int32_t kernel) {
+  if (kernel >= 25 && kernel <= 28) {  // flash40 DMA issuers: 25 waves 4-7, 26 waves 0-5 (default), 27 waves 0-3,
+    g_f4_g1 = kernel == 25 ? 1 : (kernel == 27 ? 2 : (kernel == 28 ? 3 : 0));  // 28 all eight (2 / 1 pieces)
+    return VD_OK;
+  }
   if (kernel >= 20 && kernel <= 22) {  // d = 512 (flash512): DMA placement A/B, 22 = ablation
     g_a5_var = kernel - 20;
     return VD_OK;
