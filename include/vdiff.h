@@ -211,7 +211,9 @@ int vd_attention_force_v1(int32_t on);
  * attention) with K two tiles ahead in a 3-slot LDS ring and V one ahead / K and V one tile
  * ahead (the default), 22 = DMA ablation (tile 0 only: WRONG results, timing only); 25 / 26 /
  * 27 = flash40's K/V LDS-DMA issued by waves 4-7 only, in their softmax phase / by waves 0-5
- * (the default) / by waves 0-3 only, in their MFMA phase (A/B hooks; the d = 40 choice is left
+ * (the default) / by waves 0-3 only, in their MFMA phase; 31 / 32 = vd_motion_qkv_attention's
+ * round-2 kernel / round-3 kernel (the default); 33 / 34 = the fused motion kernel at any grid
+ * size / only from one round of the chip (the default) (A/B hooks; the d = 40 choice is left
  * as it was). */
 int vd_attention_select(int32_t kernel);
 /* Diagnostic hook: copy the barrier stamps (s_memtime, 8 waves x 512, wave-major) that the last

@@ -1,7 +1,8 @@
 """Level-1 motion-module attention: Q/K/V projection fused into the temporal attention
 (vd_motion_qkv_attention) vs the QKV GEMM + vd_temporal_attention, one GPU.
 
-python tools/motion_qkv_bench.py  -> us per call of each form (M = 2 x 16 x 4096 rows)."""
+python tools/motion_qkv_bench.py [batch] [positions] -> us per call of each form (default M = 2 x 16 x 4096
+rows; 2 512 = a 2-frame rank of the 8-way frame-sharded step, whose motion blocks run position-sharded)."""
 import math
 import sys
 from pathlib import Path
@@ -12,7 +13,7 @@ import torch  # noqa: E402
 
 from vdiff import ops  # noqa: E402
 
-B, F, P, C, heads, d = int(sys.argv[1]) if len(sys.argv) > 1 else 2, 16, 4096, 320, 8, 40
+B, F, P, C, heads, d = int(sys.argv[1]) if len(sys.argv) > 1 else 2, 16, int(sys.argv[2]) if len(sys.argv) > 2 else 4096, 320, 8, 40
 g = torch.Generator(device="cuda").manual_seed(0)
 x = (torch.randn(B * F * P, C, device="cuda", generator=g)).to(torch.bfloat16)
 w = (torch.randn(3 * C, C, device="cuda", generator=g) * C ** -0.5).to(torch.bfloat16)
@@ -37,8 +38,23 @@ def unfused():
     ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], B, F, P, heads, d, scale=sc, out=out)
 
 
-t_f = timeit(lambda: ops.motion_qkv_attention(x, w, B, F, P, heads, d, scale=sc, out=out))
-t_u = timeit(unfused)
+from vdiff._lib import lib  # noqa: E402
+
+lib().vd_attention_select(33)  # the fused kernels at any grid size (the A/B below)
+
 flop = 2.0 * B * F * P * 3 * C * C
-print(f"rows {B * F * P}: fused {t_f:.1f} us ({flop / t_f / 1e6:.0f} TF/s on the projection), "
-      f"gemm + temporal attention {t_u:.1f} us", flush=True)
+outs = {}
+for ver in (1, 2):  # vd_attention_select(30 + ver): round 2's / round 3's fused kernel
+    lib().vd_attention_select(30 + ver)
+    outs[ver] = ops.motion_qkv_attention(x, w, B, F, P, heads, d, scale=sc).clone()
+res = {1: [], 2: []}
+for _ in range(5):
+    for ver in (1, 2):
+        lib().vd_attention_select(30 + ver)
+        res[ver].append(timeit(lambda: ops.motion_qkv_attention(x, w, B, F, P, heads, d, scale=sc, out=out)))
+lib().vd_attention_select(32)
+t_u = timeit(unfused)
+for ver in (1, 2):
+    t_f = sorted(res[ver])[2]
+    print(f"rows {B * F * P}: fused v{ver} {t_f:.1f} us ({flop / t_f / 1e6:.0f} TF/s on the projection)", flush=True)
+print(f"gemm + temporal attention {t_u:.1f} us; v1 == v2 bitwise: {torch.equal(outs[1], outs[2])}", flush=True)

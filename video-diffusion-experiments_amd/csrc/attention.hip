@@ -2349,8 +2349,17 @@ extern "C" int vd_attention_force_v1(int32_t on) {
 // flash32 only (round 2's default; automatic = flash40 from 4 key tiles, flash32 below), 9 =
 // flash40's diagnostic build (barrier stamps of workgroup 0, vd_attention_stamps).
 extern int g_a5_var;  // attention_d512.hip
+extern int g_mq_ver, g_mq_any;  // motion.hip
 
 extern "C" int vd_attention_select(int32_t kernel) {
+  if (kernel == 33 || kernel == 34) {  // fused motion QKV-attention at any grid size (33) / from 2 WGs per CU (34)
+    g_mq_any = kernel == 33;
+    return VD_OK;
+  }
+  if (kernel == 31 || kernel == 32) {  // fused motion QKV-attention: round 2's kernel (31) / round 3's (32)
+    g_mq_ver = kernel - 30;
+    return VD_OK;
+  }
   if (kernel >= 25 && kernel <= 28) {  // flash40 DMA issuers: 25 waves 4-7, 26 waves 0-5 (default), 27 waves 0-3,
     g_f4_g1 = kernel == 25 ? 1 : (kernel == 27 ? 2 : (kernel == 28 ? 3 : 0));  // 28 all eight (2 / 1 pieces)
     return VD_OK;

@@ -234,9 +234,216 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn_kernel(
 #undef MQ_W_STORE
 }
 
+// ---------------------------------------------------------------- v2 (round 3)
+// The same arithmetic (bit-identical output), re-staged: a wave only ever reads ITS OWN 16
+// token rows, so their A fragments live in registers (40 VGPRs: all 10 32-deep k-steps, loaded
+// once) instead of an 80 KiB LDS tile, and the 80 KiB go to the weight stream: a 6-slot ring of
+// 16 KiB chunks (128 ring rows x 64 k) filled by LDS-DMA (16 x 1 KiB pieces per chunk, two per
+// wave, the sw64 swizzle applied on the source address, pad rows zero-filled by the buffer
+// range check), five chunks in flight behind counted vmcnt waits — v1 staged one chunk through
+// registers one step ahead and waited out an L2 round trip per 256 cycles of MFMA.
+constexpr int MQ2_S = 6;  // ring slots
+
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4m;
+
+__device__ __forceinline__ u32x4m mq_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  u32x4m r;
+  r[0] = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) & 0xffffu;  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane(bytes);                          // num_records: range check
+  r[3] = 0x00020000u;
+  return r;
+}
+// one 1 KiB LDS-DMA piece (lane l's 16 bytes at voff land at LDS byte lds + 16 l); inline asm so
+// hipcc neither counts it in vmcnt nor drains it before the ring's LDS reads
+__device__ __forceinline__ void mq_dma(u32x4m rs_, uint32_t lds, uint32_t voff) {
+  u32x4m rs;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) rs[i] = __builtin_amdgcn_readfirstlane(rs_[i]);
+  uint32_t keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(rs) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void mq_wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+template <int D>
+struct Mq2Cfg {
+  using B = MqCfg<D>;
+  static constexpr int W_BYTES = B::NWP * B::KC * 2;               // 16 KiB ring slot
+  static constexpr int S_BYTES = B::S_ELEMS * 2;                   // per-wave scratch
+  static constexpr int LDS_BYTES = MQ2_S * W_BYTES + B::P * S_BYTES;
+  static_assert(B::NWP == 128 && B::KC == 64, "16 pieces of 8 ring rows x 128 B per chunk");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+};
+
+template <int D>
+__global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
+    const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw, bf16_t* __restrict__ o,
+    int64_t ldo, int64_t batch, int64_t positions, float c) {
+  using Cf = MqCfg<D>;
+  using C2 = Mq2Cfg<D>;
+  extern __shared__ __attribute__((aligned(1024))) char lds2[];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16_t* s_l = (bf16_t*)(lds2 + MQ2_S * C2::W_BYTES + wave * C2::S_BYTES);
+  bf16_t* q_s = s_l;                                     // [16][DPAD]
+  bf16_t* k_s = s_l + MF * Cf::DPAD;                     // [16][DPAD]
+  bf16_t* v_s = s_l + 2 * MF * Cf::DPAD;                 // V image [16][VS]
+
+  const int64_t nblk_p = (positions + Cf::P - 1) / Cf::P;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t b = lid / nblk_p;
+  const int64_t p0 = (lid - b * nblk_p) * Cf::P;
+  const bool pok = p0 + wave < positions;
+
+  // ---- weight-chunk DMA: chunk t = (head h, k-chunk kc) -> slot t % S; wave w moves pieces 2w,
+  // 2w + 1 = ring rows 8g .. 8g + 7; ring row n < 3D is W row (n / D) * C + h * D + n % D
+  const u32x4m rw = mq_rsrc(w, (uint32_t)(3 * Cf::C * ldw * 2));
+  const uint32_t rsub = (uint32_t)lane >> 3, pch = (uint32_t)lane & 7;  // row in the piece, physical chunk
+  auto issue = [&](int t) {
+    const int h = t / Cf::NCH, kc = t % Cf::NCH;
+    const uint32_t slot = lds0 + (uint32_t)(t % MQ2_S) * C2::W_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int g = 2 * wave + i;
+      const uint32_t r = (uint32_t)(8 * g) + rsub;                      // ring row
+      const uint32_t lc = pch ^ (r & 7);                                 // logical chunk (sw64)
+      const uint32_t n = (r / D) * Cf::C + (uint32_t)h * D + r % D;      // W row
+      const uint32_t off = r < 3 * D ? n * (uint32_t)ldw * 2 + (uint32_t)kc * (Cf::KC * 2) + lc * 16 : 0x80000000u;
+      mq_dma(rw, slot + (uint32_t)g * 1024, off);
+    }
+  };
+  constexpr int T = 8 * Cf::NCH;
+#pragma unroll
+  for (int t = 0; t < MQ2_S - 1; ++t) issue(t);
+
+  // ---- scratch padding (written once; the heads only write columns < D): Q/K columns
+  // [D, DPAD) zero; the V image zero except column D = 1.0 (the row-sum column)
+  for (int i = lane; i < Cf::S_ELEMS / 8; i += 64) *(uint4*)(s_l + i * 8) = make_uint4(0, 0, 0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane < MF) v_s[lane * Cf::VS + D] = (bf16_t)0x3F80;
+
+  // ---- this wave's A fragments: token (frame fr, position p0 + wave), k = 32 kk + 8 fq .. +7
+  bf16x8 xf[Cf::C / 32];
+  {
+    int64_t p = p0 + wave;
+    p = p < positions ? p : positions - 1;
+    const bf16_t* xr = x + ((b * MF + fr) * positions + p) * ldx + 8 * fq;
+#pragma unroll
+    for (int kk = 0; kk < Cf::C / 32; ++kk) xf[kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(xr + 32 * kk));
+  }
+
+  const bool unitc = c == 1.0f;
+  const int vtr = (4 * fq + (fr >> 2)) * Cf::VS + 4 * (fr & 3);  // tr-read lane offset (temporal_mfma_kernel)
+  f32x4 acc[Cf::NBLK];
+#pragma unroll
+  for (int a = 0; a < Cf::NBLK; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int h = 0; h < 8; ++h) {
+#pragma unroll
+   for (int kc = 0; kc < Cf::NCH; ++kc) {  // unrolled: the A fragment index 2 kc + ks is static
+    const int t = h * Cf::NCH + kc;
+    // this wave's pieces of chunk t landed: the younger ones are chunks t+1 .. min(t+S-2, T-1)
+    const int ahead = (T - 1 - t) < (MQ2_S - 2) ? (T - 1 - t) : (MQ2_S - 2);
+    if (ahead >= 4) mq_wait_vm<8>();
+    else if (ahead == 3) mq_wait_vm<6>();
+    else if (ahead == 2) mq_wait_vm<4>();
+    else if (ahead == 1) mq_wait_vm<2>();
+    else mq_wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of chunk t landed; slot (t-1) % S free
+    asm volatile("" ::: "memory");
+    if (t + MQ2_S - 1 < T) issue(t + MQ2_S - 1);
+    const bf16_t* ws = (const bf16_t*)(lds2 + (t % MQ2_S) * C2::W_BYTES);
+    // all 16 weight fragments of the chunk read ahead of its 16 MFMAs (counted lgkmcnt waits)
+    bf16x8 wf[2][Cf::NBLK];
+#pragma unroll
+    for (int ks = 0; ks < Cf::KC / 32; ++ks)
+#pragma unroll
+      for (int a = 0; a < Cf::NBLK; ++a) wf[ks][a] = *(const bf16x8*)(ws + sw64(a * 16 + fr, ks * 4 + fq));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < Cf::KC / 32; ++ks)
+#pragma unroll
+      for (int a = 0; a < Cf::NBLK; ++a)
+        acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][a], xf[2 * kc + ks], acc[a], 0, 0, 0);
+   }
+    {  // ---- head h done: attention of (position p0 + wave, head h)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous head's scratch reads
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int a = 0; a < Cf::NBLK; ++a) {
+        const int ch = a * 16 + 4 * fq;
+        if (ch < 3 * D) {
+          const int part = ch / D, cd = ch - part * D;
+          bf16_t* dst = part == 0 ? q_s + fr * Cf::DPAD + cd : (part == 1 ? k_s + fr * Cf::DPAD + cd : v_s + fr * Cf::VS + cd);
+          *(uint2*)dst = make_uint2(pack2(acc[a][0], acc[a][1]), pack2(acc[a][2], acc[a][3]));
+        }
+        acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < Cf::KSTEPS; ++ks) {
+        const bf16x8 kq = *(const bf16x8*)(k_s + fr * Cf::DPAD + ks * 32 + 8 * fq);
+        const bf16x8 qq = *(const bf16x8*)(q_s + fr * Cf::DPAD + ks * 32 + 8 * fq);
+        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kq, qq, s, 0, 0, 0);
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!unitc) s[j] *= c;
+        mx = fmaxf(mx, s[j]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pf[j] = (__bf16)__builtin_amdgcn_exp2f(s[j] - mx);
+        pf[4 + j] = (__bf16)0.0f;
+      }
+      f32x4 ot[Cf::DB];
+#pragma unroll
+      for (int a = 0; a < Cf::DB; ++a) {
+        const bf16x4 tv = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (bf16x4 __attribute__((address_space(3)))*)(v_s + vtr + 16 * a));
+        const bf16x8 vf = {tv[0], tv[1], tv[2], tv[3], (__bf16)0.0f, (__bf16)0.0f, (__bf16)0.0f, (__bf16)0.0f};
+        ot[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+      const float l = __shfl(ot[D / 16][(D % 16) % 4], ((D % 16) / 4) * 16 + fr, 64);
+      const float inv = __builtin_amdgcn_rcpf(l);
+      if (pok) {
+        bf16_t* orow = o + ((b * MF + fr) * positions + p0 + wave) * ldo + (int64_t)h * D;
+#pragma unroll
+        for (int a = 0; a < Cf::DB; ++a) {
+          const int dd = 16 * a + 4 * fq;
+          if (dd + 4 <= D)
+            *(uint2*)(orow + dd) =
+                make_uint2(pack2(ot[a][0] * inv, ot[a][1] * inv), pack2(ot[a][2] * inv, ot[a][3] * inv));
+        }
+      }
+    }
+  }
+}
+
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
+
+int g_mq_any = 0;  // 1: take the fused kernel at any grid size (A/B hook, vd_attention_select(33 / 34))
+int g_mq_ver = 2;  // 1: round 2's kernel (LDS token tile, register-staged weight chunks); vd_attention_select(31 / 32)
 
 extern "C" int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* wqkv, int64_t ldw, void* o,
                                        int64_t ldo, int64_t batch, int32_t frames, int64_t positions,
@@ -248,14 +455,28 @@ extern "C" int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* w
   VD_CHECK_ARG(ldx >= Cf::C && ldw >= Cf::C && ldo >= Cf::C);
   const int64_t nwg = batch * ((positions + Cf::P - 1) / Cf::P);
   VD_CHECK_ARG(nwg < 0x7fffffff && batch * MF * positions < 0x7fffffff);
-  // one workgroup per CU (156 KiB of LDS): below two rounds of the chip the unfused GEMM +
-  // attention is faster (a 2-frame rank of the 8-way run, 128 workgroups: 13.92 vs 13.66
-  // ms/step, tools/rank_emulate.py --mq both; the full 16-frame step, 1024: -0.31 ms/step)
+  // one workgroup per CU: below one round of the chip (v2; two rounds for v1) the unfused GEMM +
+  // attention is faster (tools/motion_qkv_bench.py: 2-frame rank, 128 workgroups: v2 39.1 vs
+  // unfused 34.8 us; 4-frame rank, 256: v2 42.4 vs 56.8 us; the full step, 1024: v2 157 vs 250)
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess &&
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
-  if (nwg < 2 * (int64_t)cus) return VD_EUNSUPPORTED;
+  if (nwg < (g_mq_ver == 2 ? 1 : 2) * (int64_t)cus && !g_mq_any) return VD_EUNSUPPORTED;
+  if (g_mq_ver == 2) {
+    using C2 = Mq2Cfg<40>;
+    static bool attr2_set = false;
+    if (!attr2_set) {
+      if (hipFuncSetAttribute((const void*)motion_qkv_attn2_kernel<40>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              C2::LDS_BYTES) != hipSuccess)
+        return vd_launch_status();
+      attr2_set = true;
+    }
+    hipLaunchKernelGGL(motion_qkv_attn2_kernel<40>, dim3((unsigned)nwg), dim3(Cf::NT), C2::LDS_BYTES,
+                       (hipStream_t)stream, (const bf16_t*)x, ldx, (const bf16_t*)wqkv, ldw, (bf16_t*)o, ldo, batch,
+                       positions, scale * 1.4426950408889634f);
+    return vd_launch_status();
+  }
   static bool attr_set = false;
   if (!attr_set) {  // > 64 KiB of dynamic LDS
     if (hipFuncSetAttribute((const void*)motion_qkv_attn_kernel<40>, hipFuncAttributeMaxDynamicSharedMemorySize,
