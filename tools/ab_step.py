@@ -4,6 +4,7 @@ variance is ~3 %): python tools/ab_step.py MODE [frames] — alternates two capt
   ln   LayerNorm fused into the residual GEMM's epilogue (ops.gemm_ln) vs GEMM + vd_layernorm
   v3p  persistent v3 GEMM vs one unit per workgroup (vd_gemm_select_path 0 vs 11)
   mq   motion-module Q/K/V projection fused into the temporal attention (L1) vs GEMM + attention
+  mq2  the fused motion kernel of round 3 (register tokens, LDS-DMA weight ring) vs round 2's
   pf   v2/v6 GEMM fragment-read order: the default vs round 1's, k-step-pipelined and all-ahead
        (vd_gemm_select_path 0 / 12 / 13 / 14)
   v3e  v3 GEMM with the LDS-bias load-free epilogue vs gemm_epilogue (vd_gemm_select_path 0 vs 15)
@@ -83,6 +84,12 @@ elif mode == "mq":
         loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
     for m in blocks:
         m.fuse_qkv_attention = True
+elif mode == "mq2":
+    from vdiff._lib import lib
+    for name, sel in (("motion-qkv v2", 32), ("motion-qkv v1", 31)):
+        lib().vd_attention_select(sel)  # kernel version fixed at capture
+        loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
+    lib().vd_attention_select(32)
 else:
     sys.exit(f"unknown mode {mode}")
 res = {k: [] for k in loops}
