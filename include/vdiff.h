@@ -213,8 +213,10 @@ int vd_attention_force_v1(int32_t on);
  * 27 = flash40's K/V LDS-DMA issued by waves 4-7 only, in their softmax phase / by waves 0-5
  * (the default) / by waves 0-3 only, in their MFMA phase; 31 / 32 = vd_motion_qkv_attention's
  * round-2 kernel / round-3 kernel (the default); 33 / 34 = the fused motion kernel at any grid
- * size / only from one round of the chip (the default) (A/B hooks; the d = 40 choice is left
- * as it was). */
+ * size / only from one round of the chip (the default); 35 = vd_attention_fp8's round-1 kernel,
+ * 36-39 = round 3's LDS-DMA-ring kernel with lazy offset + MFMA row sum / eager offset + MFMA
+ * row sum / lazy offset + fp32 row sum (the default, 38) / eager + fp32 row sum (A/B hooks; the
+ * d = 40 choice is left as it was). */
 int vd_attention_select(int32_t kernel);
 /* Diagnostic hook: copy the barrier stamps (s_memtime, 8 waves x 512, wave-major) that the last
  * flash40 launch made under vd_attention_select(9) to dst (device memory, n <= 4096 uint64). */

@@ -7,6 +7,7 @@ patch rows); RoPE and the adaLN row pass compute in fp32 from bf16 inputs and st
 against the fp32 oracle fixture (3 % / 1 %, the bounds the UNet uses).  Parity of the DiT
 to any external implementation is unpinned (the reference has none).
 """
+import math
 from pathlib import Path
 
 import numpy as np
@@ -260,10 +261,13 @@ def test_attention_fp8_quant_rope_fused(cuda):
     assert err_f < 0.10 and err_f <= 1.1 * err_u + 0.005, (err_f, err_u)
 
 
-def _fp8_emulated_attention(qkv, B, heads, S, d):
+def _fp8_emulated_attention(qkv, B, heads, S, d, lazy=True):
     """fp32 torch restatement of vd_attention_fp8's arithmetic: Q/K rounded to e4m3 with
-    per-(token, head) power-of-two scales, V per (image, head, 64-key tile), P = exp2(s - max)
-    rounded to e4m3 (unit scale), fp32 row sum of the unrounded P."""
+    per-(token, head) power-of-two scales, V per (image, head, 64-key tile); per 64-key tile,
+    P = exp2(s - m) rounded to e4m3 (unit scale) against the running offset m, O and the fp32
+    row sum of the unrounded P rescaled when m moves.  lazy: m moves only when some row of a
+    32-query group (one wave) has a tile max above its m + 8 (the default kernel); else every
+    row whose tile max passes m (round 1's kernel)."""
     f8 = torch.float8_e4m3fn
     D = heads * d
     x = qkv.float().reshape(B, S, 3, heads, d).permute(2, 0, 3, 1, 4)  # qkv b h s d
@@ -278,17 +282,31 @@ def _fp8_emulated_attention(qkv, B, heads, S, d):
     v = x[2].reshape(B, heads, S // 64, 64, d)
     v = q8(v, (-2, -1)).reshape(B, heads, S, d)
     s = (q @ k.transpose(-1, -2)) * (d ** -0.5 * 1.4426950408889634)
-    p = torch.exp2(s - s.amax(-1, keepdim=True))
-    o = (p.to(f8).float() @ v) / p.sum(-1, keepdim=True)
-    return o.permute(0, 2, 1, 3).reshape(B * S, D)
+    m = torch.full((B, heads, S, 1), -math.inf)
+    o = torch.zeros(B, heads, S, d)
+    lsum = torch.zeros(B, heads, S, 1)
+    for t in range(S // 64):
+        st = s[..., 64 * t:64 * t + 64]
+        mt = st.amax(-1, keepdim=True)
+        if lazy:
+            up = (mt > m + 8).reshape(B, heads, S // 32, 32).any(-1, keepdim=True)
+            up = up.expand(B, heads, S // 32, 32).reshape(B, heads, S, 1)
+        else:
+            up = mt > m
+        mn = torch.where(up, torch.maximum(m, mt), m)
+        alpha = torch.where(up, torch.exp2(m - mn), torch.ones_like(m))
+        m = mn
+        p = torch.exp2(st - m)
+        o = o * alpha + p.to(f8).float() @ v[..., 64 * t:64 * t + 64, :]
+        lsum = lsum * alpha + p.sum(-1, keepdim=True)
+    return (o / lsum).permute(0, 2, 1, 3).reshape(B * S, D)
 
 
 @pytest.mark.parametrize("S", [64, 256, 2304])
 def test_attention_fp8_matches_fp32(cuda, S):
-    """fp8 QK^T / PV (e4m3 operands, fp32 accumulation and softmax statistics): within 3 %
-    rel-L2 of the fp32 emulation of its own quantization (the kernel is right: measured 0.2 %
-    at S = 64 growing to 1.6 % at S = 2304, because the kernel rounds each tile's P against
-    the running max — fewer subnormals — while the emulation uses the final max), and within
+    """fp8 QK^T / PV (e4m3 operands, fp32 accumulation and softmax statistics): within 1 %
+    rel-L2 of the fp32 emulation of its own quantization (tile by tile, the same lazy offset;
+    measured 0.17-0.21 %: fp32 summation order and the MFMA's block-scale application), and within
     10 % of exact fp32 SDPA (what e4m3's 3 mantissa bits cost; the bf16 kernel's error on the
     same data is printed for comparison)."""
     g = torch.Generator().manual_seed(S)
@@ -305,7 +323,7 @@ def test_attention_fp8_matches_fp32(cuda, S):
     print(f"S={S}: fp8 vs emulation {err_emu:.4f}, fp8 vs fp32 {err:.4f} (emulation vs fp32 "
           f"{rel_l2(emu, want):.4f}), bf16 kernel vs fp32 {err_bf:.4f}")
     assert torch.isfinite(got).all()
-    assert err_emu < 0.03, err_emu
+    assert err_emu < 0.01, err_emu
     assert err < 0.10, err
 
 

@@ -318,6 +318,198 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_kernel(
   }
 }
 
+// ---------------------------------------------------------------- v2 (round 3)
+// flash_fp8_kernel's arithmetic re-staged.  v1 loaded each 64-key tile into registers one
+// tile ahead, wrote it to LDS and synchronised per tile (an L2 round trip exposed every tile),
+// rescaled O whenever a row max grew, clamped every P to the e4m3 range and summed P on the
+// VALU.  v2: K, V^T and the K scales reach a 6-stage LDS ring by LDS-DMA (9 pieces per tile:
+// K and V^T rows of 64 B XOR-swizzled on the source chunk, conflict-free b128 reads; the 64
+// per-key scale bytes by one buffer_load_ubyte ... lds, one dword each), five tiles in flight behind counted
+// vmcnt waits; the running offset m moves only when a row max passes it by 8 (P <= 2^8 < 448:
+// no clamp; cdna_hip_programming.md T13).  A/B forms (tools/fp8_variants.py, DiT shape, rel-L2 vs
+// fp32 SDPA at S = 2304): v1 1.580 ms / 8.60 %; LAZY + row sum on the MFMA (an all-ones e4m3 A
+// operand against P) 1.389 ms / 8.93 %; LAZY + fp32 VALU row sum (the default, v = 4) 1.426 ms /
+// 8.78 %; eager offset + VALU sum (v1's arithmetic on the ring) 1.520 ms / 8.60 %.  The MFMA row
+// sum is faster but sums the e4m3-rounded P, which costs accuracy.
+constexpr int F8S = 6;  // ring stages
+constexpr int F8_K = 0, F8_V = 4096, F8_KS = 8192, F8_STAGE = 8192 + 256;
+
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4f;
+
+__device__ __forceinline__ u32x4f f8_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  u32x4f r;
+  r[0] = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) & 0xffffu;  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane(bytes);                          // num_records: range check
+  r[3] = 0x00020000u;
+  return r;
+}
+// LDS-DMA: lane l's 16 bytes (x4) at voff land at LDS lds + 16 l; a ubyte load lands zero-extended
+// in the dword at lds + 4 l;
+// inline asm so hipcc neither counts them in vmcnt nor drains them before the LDS reads
+__device__ __forceinline__ void f8_dma16(u32x4f rs, uint32_t lds, uint32_t voff) {
+  uint32_t keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+               "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(rs) : "memory");
+}
+__device__ __forceinline__ void f8_dma1(u32x4f rs, uint32_t lds, uint32_t voff) {
+  uint32_t keep;
+  asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+               "buffer_load_ubyte %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(rs) : "memory");
+}
+__device__ __forceinline__ void f8_wait(int n) {  // s_waitcnt vmcnt(n), n in {0, 2, 3, 4, 6, 8, 9, 12}
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+  }
+}
+// physical 16-byte chunk of logical chunk c in a 64-byte row r of a K / V^T tile image
+__device__ __forceinline__ uint32_t f8_chunk(uint32_t r, uint32_t c) { return c ^ ((r >> 2) & 3); }
+
+template <bool LAZY, bool ONES>  // lazy offset (P <= 2^8) / row sum on the MFMA (A/B: both on by default)
+__global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
+    const uint8_t* __restrict__ q8, const uint8_t* __restrict__ k8, int64_t ld8,
+    const uint8_t* __restrict__ qs, const uint8_t* __restrict__ ks, const uint8_t* __restrict__ vt8,
+    const uint8_t* __restrict__ vs, bf16_t* __restrict__ o, int64_t ldo, int heads, int64_t sq, int64_t skv,
+    float c) {
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[F8S * F8_STAGE];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = (int)((sq + 127) / 128);
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qblk = lid % nqb;
+  const int h = (lid / nqb) % heads;
+  const int64_t b = lid / (nqb * heads);
+  const int64_t bh = b * heads + h;
+  const int64_t q0 = (int64_t)qblk * 128 + wave * 32;
+  const bool qvalid = q0 < sq;
+  const int64_t qrow = b * sq + (qvalid ? q0 + r : 0);
+  const int ntiles = (int)(skv / KT8);
+
+  // ---- ring: wave w moves K rows and V^T rows 16w .. 16w + 15 of each tile, wave 0 the scales
+  const u32x4f rk = f8_rsrc(k8 + b * skv * ld8 + h * FD, (uint32_t)((skv - 1) * ld8 + FD));
+  const u32x4f rv = f8_rsrc(vt8 + bh * FD * skv, (uint32_t)(FD * skv));
+  const u32x4f rks = f8_rsrc(ks + b * skv * heads + h, (uint32_t)((skv - 1) * heads + 1));
+  const uint32_t prow = (uint32_t)(16 * wave) + ((uint32_t)lane >> 2);       // row of this lane's 16 bytes
+  const uint32_t pchk = f8_chunk(prow, (uint32_t)lane & 3);                  // the source chunk they hold
+  const uint32_t kdo = prow * (uint32_t)ld8 + 16u * pchk, vdo = prow * (uint32_t)skv + 16u * pchk;
+  const uint32_t sdo = (uint32_t)lane * (uint32_t)heads;
+  const int npc = wave == 0 ? 3 : 2;  // this wave's DMA instructions per tile
+  auto issue = [&](int t) {
+    const uint32_t slot = lds0 + (uint32_t)(t % F8S) * F8_STAGE;
+    f8_dma16(rk, slot + F8_K + 1024u * wave, kdo + (uint32_t)t * KT8 * (uint32_t)ld8);
+    f8_dma16(rv, slot + F8_V + 1024u * wave, vdo + (uint32_t)t * KT8);
+    if (wave == 0) f8_dma1(rks, slot + F8_KS, sdo + (uint32_t)t * KT8 * (uint32_t)heads);
+  };
+  for (int t = 0; t < F8S - 1 && t < ntiles; ++t) issue(t);
+
+  // Q^T fragment: d = 32 hh + j of this lane's query, and its scale
+  const i32x8 qf = *(const i32x8*)(q8 + qrow * ld8 + h * FD + 32 * hh);
+  const int qsc = qs[qrow * heads + h];
+  const i32x8 ones = {0x38383838, 0x38383838, 0x38383838, 0x38383838,
+                      0x38383838, 0x38383838, 0x38383838, 0x38383838};  // e4m3 1.0
+  // per-lane LDS read offsets: K row 32 kb + r and V^T row 32 a + r, logical chunks 2 hh, 2 hh + 1
+  uint32_t kro[2][2], vro[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t row = (uint32_t)(32 * x + r);
+      kro[x][j] = F8_K + row * 64 + 16u * f8_chunk(row, (uint32_t)(2 * hh + j));
+      vro[x][j] = F8_V + row * 64 + 16u * f8_chunk(row, (uint32_t)(2 * hh + j));
+    }
+
+  f32x16 ot[2], lacc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { ot[0][i] = 0.f; ot[1][i] = 0.f; lacc[i] = 0.f; }
+  float m = -INFINITY, lsum = 0.f;
+  for (int t = 0; t < ntiles; ++t) {
+    const int ahead = (ntiles - 1 - t) < (F8S - 2) ? (ntiles - 1 - t) : (F8S - 2);
+    f8_wait(ahead * npc);                               // this wave's pieces of tile t landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                       // everyone's; stage (t-1) % S free
+    asm volatile("" ::: "memory");
+    if (t + F8S - 1 < ntiles) issue(t + F8S - 1);
+    const uint8_t* st = lds + (t % F8S) * F8_STAGE;
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const uint4 k0 = *(const uint4*)(st + kro[kb][0]), k1 = *(const uint4*)(st + kro[kb][1]);
+      const i32x8 kf = {(int)k0.x, (int)k0.y, (int)k0.z, (int)k0.w, (int)k1.x, (int)k1.y, (int)k1.z, (int)k1.w};
+      const int ksc = st[F8_KS + 4 * (32 * kb + r)];  // sub-dword LDS-DMA writes one dword per lane
+      f32x16 z;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) z[i] = 0.f;
+      s[kb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, z, 0, 0, 0, ksc, 0, qsc);
+    }
+    i32x8 vf[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const uint4 v0 = *(const uint4*)(st + vro[a][0]), v1 = *(const uint4*)(st + vro[a][1]);
+      vf[a] = i32x8{(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
+    }
+    const int vsc = vs[bh * ntiles + t];
+    // ---- softmax against the lazily moved offset m (P <= 2^8)
+    float mt = s[0][0];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kb][i]);
+    mt = fmaxf(mt, partner32f(mt)) * c;
+    if (LAZY ? __any(mt > m + 8.f) : mt > m) {  // lazy: wave-uniform; always on the first tile (m = -inf)
+      const float mn = fmaxf(m, mt);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      m = mn;
+      lsum *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { ot[0][i] *= alpha; ot[1][i] *= alpha; lacc[i] *= alpha; }
+    }
+    uint32_t pw[8];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float p0 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 0], c, -m));
+        const float p1 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 1], c, -m));
+        const float p2 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 2], c, -m));
+        const float p3 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 3], c, -m));
+        if (!ONES) lsum += (p0 + p1) + (p2 + p3);
+        int w = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, 0, false);
+        pw[4 * kb + g] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(p2, p3, w, true);
+      }
+    const i32x8 pf = {(int)pw[0], (int)pw[1], (int)pw[2], (int)pw[3], (int)pw[4], (int)pw[5], (int)pw[6], (int)pw[7]};
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+      ot[a] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf[a], pf, ot[a], 0, 0, 0, vsc, 0, 127);
+    if (ONES) lacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones, pf, lacc, 0, 0, 0, 127, 0, 127);
+  }
+  // ONES: every row of the ones-product is this query's row sum (over the e4m3 P); else the
+  // lane's fp32 partial over its 32 unrounded scores plus its partner's
+  const float inv = 1.0f / (ONES ? lacc[0] : lsum + partner32f(lsum));
+  if (qvalid) {
+    bf16_t* orow = o + (b * sq + q0 + r) * ldo + h * FD;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = 32 * a + 8 * g + 4 * hh;
+        *(uint2*)(orow + dd) = make_uint2(pack2(ot[a][4 * g] * inv, ot[a][4 * g + 1] * inv),
+                                          pack2(ot[a][4 * g + 2] * inv, ot[a][4 * g + 3] * inv));
+      }
+  }
+}
+
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 int quant_operands(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
@@ -355,6 +547,8 @@ int quant_operands(const void* q, int64_t ldq, const void* k, int64_t ldk, const
 
 }  // namespace
 
+int g_fp8_ver = 4;  // 1: round 1's flash_fp8_kernel; 2-5: round 3's forms (vd_attention_select(34 + v): A/B hook)
+
 extern "C" int vd_attention_fp8_quant(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                                       int64_t ldv, int64_t batch, int32_t heads, int64_t sq, int64_t skv,
                                       int32_t d, void* q8, void* k8, int64_t ld8, void* vt8, void* qs,
@@ -382,8 +576,19 @@ extern "C" int vd_attention_fp8(const void* q8, const void* k8, int64_t ld8, con
   const int64_t nblk = (sq + 127) / 128 * heads * batch;
   VD_CHECK_ARG(nblk < 0x7fffffff);
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(flash_fp8_kernel, dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream, (const uint8_t*)q8,
-                     (const uint8_t*)k8, ld8, (const uint8_t*)qs, (const uint8_t*)ks, (const uint8_t*)vt8,
-                     (const uint8_t*)vs, (bf16_t*)o, ldo, (int)heads, sq, skv, c, 127);
+  const bool v2ok = skv * ld8 < 0x7fffffff && skv * FD < 0x7fffffff && skv * heads < 0x7fffffff;
+#define F8V2(L, O)                                                                                               \
+  hipLaunchKernelGGL((flash_fp8_v2_kernel<L, O>), dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream,        \
+                     (const uint8_t*)q8, (const uint8_t*)k8, ld8, (const uint8_t*)qs, (const uint8_t*)ks,        \
+                     (const uint8_t*)vt8, (const uint8_t*)vs, (bf16_t*)o, ldo, (int)heads, sq, skv, c)
+  if (v2ok && g_fp8_ver == 2) F8V2(true, true);
+  else if (v2ok && g_fp8_ver == 3) F8V2(false, true);
+  else if (v2ok && g_fp8_ver == 4) F8V2(true, false);
+  else if (v2ok && g_fp8_ver == 5) F8V2(false, false);
+#undef F8V2
+  else
+    hipLaunchKernelGGL(flash_fp8_kernel, dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream, (const uint8_t*)q8,
+                       (const uint8_t*)k8, ld8, (const uint8_t*)qs, (const uint8_t*)ks, (const uint8_t*)vt8,
+                       (const uint8_t*)vs, (bf16_t*)o, ldo, (int)heads, sq, skv, c, 127);
   return vd_launch_status();
 }
