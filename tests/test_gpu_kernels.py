@@ -98,11 +98,12 @@ def test_gemm_geglu(cuda):
 
 
 # ---------------------------------------------------------------- v2 (LDS-DMA) paths
-@pytest.fixture(params=["v6", "v5", "v3", "v2", "v1"])
+@pytest.fixture(params=["v6", "v5", "v3", "v2", "v1", "v2mf"])
 def gemm_path(request, cuda):
-    """Force one GEMM kernel (v3 only takes dense A; other shapes fall back to auto)."""
+    """Force one GEMM kernel (v3 only takes dense A; other shapes fall back to auto; v2mf = the
+    automatic plan with v2's 256 x 160 tiles in the 32x32x16 form for convs and dense GEMMs)."""
     from vdiff._lib import lib
-    lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6}[request.param])
+    lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6, "v2mf": 18}[request.param])
     yield request.param
     lib().vd_gemm_select_path(0)
 
@@ -374,6 +375,44 @@ def test_conv3x3_splitk(cuda):
     img = x.float().reshape(n, h, w, ci).permute(0, 3, 1, 2)
     want = F.conv2d(img, wt.float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, co) + res.float()
     close_bf16(out, want)
+
+
+@pytest.mark.parametrize("kind", ["conv", "conv_splitk", "dense_res", "dense_silu_f32", "dense_splitk"])
+def test_gemm_v2_mfma32(cuda, kind):
+    """v2 in the 32x32x16 form (vd_gemm_select_path(18)): one output row per lane, the
+    permlane32-paired 16-B epilogue (bias, row bias, SiLU, residual, fp32 out) and the split-K
+    slab in that layout, against fp32 / fp64 references."""
+    from vdiff._lib import lib
+    lib().vd_gemm_select_path(18)
+    try:
+        if kind.startswith("conv"):
+            n, h, w, ci, co = (8, 64, 64, 128, 320) if kind == "conv" else (32, 8, 8, 256, 1280)
+            x0, x1 = rnd(n * h * w, ci // 2), rnd(n * h * w, ci - ci // 2)
+            wt = bf(torch.randn(co, ci, 3, 3, device=cuda) * 0.03)
+            b = torch.randn(co, device=cuda)
+            temb = torch.randn(n, co, device=cuda)
+            res = rnd(n * h * w, co)
+            out, _, _ = ops.conv3x3(x0, n, h, w, pack_conv3x3(wt), x1=x1, bias=b, rowbias=temb, rb_div=h * w,
+                                    res=res)
+            img = torch.cat([x0, x1], 1).float().reshape(n, h, w, ci).permute(0, 3, 1, 2)
+            want = (F.conv2d(img, wt.float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, co) +
+                    temb.repeat_interleave(h * w, 0) + res.float())
+            close_bf16(out, want)
+            return
+        M, N, K = (32768, 640, 640) if kind != "dense_splitk" else (2048, 1280, 2560)
+        a, w = rnd(M, K), rnd(N, K, std=K ** -0.5)
+        b = torch.randn(N, device=cuda)
+        if kind == "dense_silu_f32":
+            got = ops.gemm(a, w, bias=b, act=ops.ACT_SILU, out_f32=True)
+            close_f32(got, F.silu(a.double() @ w.double().T + b.double()), rtol=1e-3, atol=1e-3)
+            return
+        temb = torch.randn(2, N, device=cuda)
+        res = rnd(M, N)
+        got = ops.gemm(a, w, bias=b, rowbias=temb, rb_div=M // 2, res=res)
+        want = a.float() @ w.float().T + b + temb.repeat_interleave(M // 2, 0) + res.float()
+        close_bf16(got, want)
+    finally:
+        lib().vd_gemm_select_path(0)
 
 
 # ---------------------------------------------------------------- conv

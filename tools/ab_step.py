@@ -8,7 +8,9 @@ variance is ~3 %): python tools/ab_step.py MODE [frames] — alternates two capt
   pf   v2/v6 GEMM fragment-read order: the default vs round 1's, k-step-pipelined and all-ahead
        (vd_gemm_select_path 0 / 12 / 13 / 14)
   v3e  v3 GEMM with the LDS-bias load-free epilogue vs gemm_epilogue (vd_gemm_select_path 0 vs 15)
-  roll v5 GEMM with the rolling W-fragment window vs round 1's halves (vd_gemm_select_path 0 vs 16)"""
+  roll v5 GEMM with the rolling W-fragment window vs round 1's halves (vd_gemm_select_path 0 vs 16)
+  mf   v2 in the 32x32x16 form on the short-K level-1 convs (the automatic plan) vs never
+       (vd_gemm_select_path 0 vs 19)"""
 import sys
 import time
 from pathlib import Path
@@ -51,6 +53,12 @@ elif mode == "ln":
         ops.gemm_ln = fn
         loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
     ops.gemm_ln = orig
+elif mode == "mf":
+    from vdiff._lib import lib
+    for name, path in (("mf32-auto", 0), ("mf32-never", 19)):
+        lib().vd_gemm_select_path(path)  # the plan is fixed at capture
+        loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
+    lib().vd_gemm_select_path(0)
 elif mode == "v3p":
     from vdiff._lib import lib
     for name, path in (("v3-persistent", 0), ("v3-per-tile", 11)):

@@ -416,12 +416,72 @@ __device__ __forceinline__ void wait_vm() {
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+// Epilogue of the 32x32x16 form (MF = 1): acc[a][4 g + i] = C[m = mbase + (lane & 31)]
+// [n = nbase + 32 a + 8 g + 4 (lane >> 5) + i] — one output row per lane, its 8-column groups
+// split across the half-waves.  bias / row bias / activation / residual in fp32 in that layout
+// (8-B residual loads), then bf16 packs and one v_permlane32_swap per dword of a group pair
+// (cdna_hip_programming.md T21), so each lane stores 16 contiguous bytes: lanes 0-31 columns
+// 16 h .. 16 h + 7, lanes 32-63 the next 8.  fp32 output: 16-B stores in the MFMA layout.
+// Requires (host plan) N % 32 == 0, ldc % 8 == 0, a 16-B aligned output, no GEGLU.
+template <int NB>
+__device__ __forceinline__ void gemm_epilogue32(const vd_gemm_desc& d, f32x16 (&acc)[NB], int mbase, int nbase,
+                                                int lane) {
+  const int M = (int)d.M, N = (int)d.N;
+  const int m = mbase + (lane & 31), hh = lane >> 5;
+  if (m >= M) return;
+  const float* rbrow = d.rowbias ? d.rowbias + (int64_t)(m / (int)d.rb_div) * d.ld_rb : nullptr;
+#pragma unroll
+  for (int a = 0; a < NB; ++a) {
+    const int n0 = nbase + 32 * a;
+    if (n0 >= N) continue;
+    float o[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int n = n0 + 8 * g + 4 * hh;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (d.bias) bv = *(const float4*)(d.bias + n);
+      o[g][0] = acc[a][4 * g] + bv.x; o[g][1] = acc[a][4 * g + 1] + bv.y;
+      o[g][2] = acc[a][4 * g + 2] + bv.z; o[g][3] = acc[a][4 * g + 3] + bv.w;
+      if (rbrow) {
+        const float4 t = *(const float4*)(rbrow + n);
+        o[g][0] += t.x; o[g][1] += t.y; o[g][2] += t.z; o[g][3] += t.w;
+      }
+      if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[g][j] = act_pw(d.act, o[g][j]);
+      }
+      if (d.res) {
+        const uint2 r = *(const uint2*)((const bf16_t*)d.res + (uint32_t)(m * (int)d.ld_res + n));
+        o[g][0] += bf_lo(r.x); o[g][1] += bf_hi(r.x); o[g][2] += bf_lo(r.y); o[g][3] += bf_hi(r.y);
+      }
+    }
+    if (d.out_f32) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *(float4*)((float*)d.out + (uint32_t)(m * (int)d.ldc + n0 + 8 * g + 4 * hh)) =
+            make_float4(o[g][0], o[g][1], o[g][2], o[g][3]);
+      continue;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t x0 = pack2(o[2 * h][0], o[2 * h][1]), x1 = pack2(o[2 * h][2], o[2 * h][3]);
+      uint32_t y0 = pack2(o[2 * h + 1][0], o[2 * h + 1][1]), y1 = pack2(o[2 * h + 1][2], o[2 * h + 1][3]);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+      *(uint4*)((bf16_t*)d.out + (uint32_t)(m * (int)d.ldc + n0 + 16 * h + 8 * hh)) =
+          make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+  }
+}
+
 // PF (fragment-read order, round 2): without a pin hipcc sinks each X fragment read to its 4
 // MFMAs behind an lgkmcnt(0) — 8 exposed LDS latencies per K-tile (PF = 0, round 1's order).
 // PF = 1 issues all 18 reads of the K-tile right after the barrier (sched_barrier), PF = 2 (the
 // default) issues k-step 0's 9 reads, then interleaves k-step 1's reads one per two of k-step
 // 0's MFMAs (sched_group_barrier), so the MFMA chain waits on counted lgkmcnt only.
-template <int BN, int MODE, int PF = 1>
+template <int BN, int MODE, int PF = 1, int MF = 0>
 __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                          uint32_t a1_bytes, uint32_t w_bytes,
                                                          int split) {
@@ -449,6 +509,13 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
 
   const int rb = lane >> 3;                                  // row within the 8-row DMA block
   const uint32_t lc16 = (uint32_t)(((lane & 7) ^ rb) * 16);  // swizzled source chunk (bytes)
+  // MF = 1: the image's XOR is (row >> 1) & 7 (conflict-free 32-row fragment reads), which for
+  // row = 8 p + rb depends on the piece parity p & 1: A pieces wid * 4 + j (parity j & 1), W
+  // pieces 8 j + wid (parity wid & 1)
+  auto lcs = [&](int par) -> uint32_t {
+    return MF ? (uint32_t)(((lane & 7) ^ ((4 * par + (rb >> 1)) & 7)) * 16) : lc16;
+  };
+  const uint32_t lcb = lcs(wid & 1);
   const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)d.a0, 0, a0_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ra1 =
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.a1 ? d.a1 : d.a0), 0, d.a1 ? a1_bytes : 0, 0x00020000);
@@ -479,15 +546,15 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     for (int j = 0; j < C::NBMAX; ++j) {
       int64_t n = n0 + (j * 8 + wid) * 8 + rb;
       n = n < N ? n : N - 1;
-      boff[j] = (uint32_t)(n * d.ldw * 2) + lc16;
+      boff[j] = (uint32_t)(n * d.ldw * 2) + lcb;
     }
     if constexpr (MODE == VD_A_DENSE) {
 #pragma unroll
       for (int j = 0; j < C::NA; ++j) {
         int64_t m = m0 + (wid * 4 + j) * 8 + rb;
         m = m < M ? m : M - 1;
-        aoff0[j] = (uint32_t)(m * d.lda0 * 2) + lc16;
-        aoff1[j] = (uint32_t)(m * d.lda1 * 2) + lc16;
+        aoff0[j] = (uint32_t)(m * d.lda0 * 2) + lcs(j & 1);
+        aoff1[j] = (uint32_t)(m * d.lda1 * 2) + lcs(j & 1);
       }
     } else {
       const int hw = d.h_out * d.w_out;
@@ -532,8 +599,8 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
           ih >>= d.upsample;
           iw >>= d.upsample;
           const uint32_t pix = (uint32_t)(((pimg[j] + dt) * d.h_in + ih) * d.w_in + iw);
-          aoff0[j] = ok ? pix * (uint32_t)(d.lda0 * 2) + lc16 : G2_OOB;
-          aoff1[j] = ok ? pix * (uint32_t)(d.lda1 * 2) + lc16 : G2_OOB;
+          aoff0[j] = ok ? pix * (uint32_t)(d.lda0 * 2) + lcs(j & 1) : G2_OOB;
+          aoff1[j] = ok ? pix * (uint32_t)(d.lda1 * 2) + lcs(j & 1) : G2_OOB;
         }
       }
       const bool s0 = c_ci < d.k0;
@@ -552,11 +619,21 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     if (++ikt == ikt1 && (iu += G) < units) setup_unit(iu);
   };
 
-  f32x4 acc[C::NB][C::MB];
+  f32x4 acc[MF ? 1 : C::NB][MF ? 1 : C::MB];
 #pragma unroll
-  for (int a = 0; a < C::NB; ++a)
+  for (int a = 0; a < (MF ? 1 : C::NB); ++a)
 #pragma unroll
-    for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < (MF ? 1 : C::MB); ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // MF = 1: 8 waves as 8(M) x 1(N), each 32 rows x BN columns in BN / 32 accumulators of
+  // v_mfma_f32_32x32x16_bf16 — half the MFMA instructions of the 16x16x32 form for the same
+  // work (an MFMA holds the SIMD's vector issue for 8 cycles either way), 24 fragment reads
+  // per K-tile instead of 18
+  constexpr int NB32 = BN / 32;
+  f32x16 acc32[MF ? NB32 : 1];
+#pragma unroll
+  for (int a = 0; a < (MF ? NB32 : 1); ++a)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc32[a][i] = 0.f;
 
   // total k-tiles this workgroup streams
   int n_it = 0;
@@ -578,6 +655,16 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     wlane[ks] = C::A_BYTES + 2 * lds_off(wn * (BN / 2) + (lane & 15), ks * 4 + (lane >> 4));
     xlane[ks] = 2 * lds_off(wm * 64 + (lane & 15), ks * 4 + (lane >> 4));
   }
+  // MF = 1 fragment offsets, k-steps of 16: row r, chunk 2 ks + lane / 32, XOR (r >> 1) & 7
+  // (W block a adds 32 a rows = 4096 a bytes, the XOR unchanged)
+  uint32_t w32[BK / 16], x32[BK / 16];
+#pragma unroll
+  for (int ks = 0; ks < BK / 16; ++ks) {
+    const int r = lane & 31, c = 2 * ks + (lane >> 5);
+    w32[ks] = C::A_BYTES + (uint32_t)(r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+    const int rx = 32 * wid + r;
+    x32[ks] = (uint32_t)(rx * 128 + ((c ^ ((rx >> 1) & 7)) << 4));
+  }
   // ---- compute cursor
   int cu = u_begin, ckt, ckt1;
   unit_kr(cu, ckt, ckt1);
@@ -595,7 +682,20 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's DMA for `it` landed; stage (it-1)%3 fully read
     const char* sbase = smem + stage * C::STAGE;
-    if constexpr (PF != 0) {
+    if constexpr (MF) {
+      bf16x8 wf[BK / 16][NB32], xf[BK / 16];
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        xf[ks] = *(const bf16x8*)(sbase + x32[ks]);
+#pragma unroll
+        for (int a = 0; a < NB32; ++a) wf[ks][a] = *(const bf16x8*)(sbase + w32[ks] + a * 4096);
+      }
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks)
+#pragma unroll
+        for (int a = 0; a < NB32; ++a)
+          acc32[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks][a], xf[ks], acc32[a], 0, 0, 0);
+    } else if constexpr (PF != 0) {
       bf16x8 wf[BK / 32][C::NB], xf[BK / 32][C::MB];
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks) {
@@ -641,7 +741,23 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     if (++ckt == ckt1) {  // unit finished: epilogue (its memory ops precede the next DMA)
       const int tile = cu / split, sp = cu % split;
       const int64_t m0 = (int64_t)(tile / tiles_n) * G2_BM, n0 = (int64_t)(tile % tiles_n) * BN;
-      if (split == 1) {
+      if constexpr (MF) {
+        if (split == 1) {
+          gemm_epilogue32<NB32>(d, acc32, (int)m0 + 32 * wid, (int)n0, lane);
+        } else {  // split-K slab in the 32x32 layout
+          float* slab = (float*)d.ws + (int64_t)sp * M * N;
+          const int64_t m = m0 + 32 * wid + (lane & 31);
+#pragma unroll
+          for (int a = 0; a < NB32; ++a)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int64_t n = n0 + 32 * a + 8 * g + 4 * (lane >> 5);
+              if (m < M && n < N)
+                *(float4*)(slab + m * N + n) =
+                    make_float4(acc32[a][4 * g], acc32[a][4 * g + 1], acc32[a][4 * g + 2], acc32[a][4 * g + 3]);
+            }
+        }
+      } else if (split == 1) {
         gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::MB * 16, (int)n0 + wn * (BN / 2), lane);
       } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
         float* slab = (float*)d.ws + (int64_t)sp * M * N;
@@ -658,9 +774,13 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
         }
       }
 #pragma unroll
-      for (int a = 0; a < C::NB; ++a)
+      for (int a = 0; a < (MF ? 1 : C::NB); ++a)
 #pragma unroll
-        for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int b = 0; b < (MF ? 1 : C::MB); ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int a = 0; a < (MF ? NB32 : 1); ++a)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc32[a][i] = 0.f;
       if ((cu += G) < units) unit_kr(cu, ckt, ckt1);
     }
     if (it + 2 < n_it) issue(stage == 0 ? 2 : stage - 1);
@@ -1828,6 +1948,19 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
   }
 }
 
+// v2 in the 32x32x16 form (gemm2_kernel<160, *, 1, 1>; round 3): half the MFMA instructions, a
+// third more fragment reads.  Measured (tools/kbench.py, profiles/r03m_gemm_mfma32_ab.txt): 5 %
+// faster on the level-1 320 -> 320 conv (K 2880), 7-11 % slower on the longer-K convs and most
+// dense shapes — so the automatic plan (g_g2_mf -1) takes it for convs with K <= 2880 at
+// M >= 65536 only; 1 = every conv, 2 = convs and dense GEMMs, 0 = never (vd_gemm_select_path
+// 17 / 18 / 19, A/B).  Not for GEGLU (gemm_epilogue32 has none).
+int g_g2_mf = -1;
+inline bool mf32_ok(const vd_gemm_desc& d) {
+  if (d.act == VD_ACT_GEGLU || d.N % 32 || d.ldc % 8 || ((uintptr_t)d.out & 15)) return false;
+  if (g_g2_mf < 0) return d.a_mode == VD_A_CONV3X3 && d.K <= 2880 && d.M >= 65536;
+  return g_g2_mf == 2 || (g_g2_mf == 1 && d.a_mode == VD_A_CONV3X3);
+}
+
 template <int BN>
 int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
   const int64_t units = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + BN - 1) / BN) * split;
@@ -1837,6 +1970,17 @@ int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   const int pf = g_g2_pf >= 0 ? g_g2_pf : 2;
 #define G2_LAUNCH(MODE_, PF_) \
   hipLaunchKernelGGL((gemm2_kernel<BN, MODE_, PF_>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split)
+  if constexpr (BN == 160) {
+    if (mf32_ok(d)) {
+      if (d.a_mode == VD_A_CONV3X3)
+        hipLaunchKernelGGL((gemm2_kernel<160, VD_A_CONV3X3, 1, 1>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b,
+                           a1b, wb, split);
+      else
+        hipLaunchKernelGGL((gemm2_kernel<160, VD_A_DENSE, 1, 1>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b,
+                           a1b, wb, split);
+      goto launched;
+    }
+  }
   if (d.a_mode == VD_A_CONV3X3) {
     if (pf == 0) G2_LAUNCH(VD_A_CONV3X3, 0);
     else if (pf == 1) G2_LAUNCH(VD_A_CONV3X3, 1);
@@ -1847,6 +1991,7 @@ int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
     else G2_LAUNCH(VD_A_DENSE, 2);
   }
 #undef G2_LAUNCH
+launched:
   int rc = vd_launch_status();
   if (rc != VD_OK || split == 1) return rc;
   const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
@@ -2138,7 +2283,9 @@ extern "C" int vd_gemm_force_v1(int32_t on) {
   return VD_OK;
 }
 extern "C" int vd_gemm_select_path(int32_t path) {
-  if (path < 0 || path > 16 || path == 4) return VD_EINVAL;
+  if (path < 0 || path > 19 || path == 4) return VD_EINVAL;
+  g_g2_mf = path == 17 ? 1 : path == 18 ? 2 : path == 19 ? 0 : -1;
+  if (path >= 17) path = 0;  // auto plan, v2 in the 32x32x16 form for convs / convs + dense (A/B)
   g_g4_roll = path != 16;
   if (path == 16) path = 0;  // auto plan, v5 with round 1's fragment halves (A/B)
   g_g3_fast = path != 15;
