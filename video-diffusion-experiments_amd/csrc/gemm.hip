@@ -580,7 +580,7 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     char* lb = la + C::A_BYTES;
     const int kb = ikt * BK;
     if constexpr (MODE == VD_A_DENSE) {
-      const bool s0 = kb < d.k0;
+      const bool s0 = kb < (int)d.k0;
       const uint32_t koff = (uint32_t)(s0 ? kb : kb - (int)d.k0) * 2;
 #pragma unroll
       for (int j = 0; j < C::NA; ++j)
@@ -591,25 +591,26 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
         const int ks2 = d.ks * d.ks;
         const int dt = c_tap / ks2, t9 = c_tap - ks2 * dt;
         const int dy = d.ks == 3 ? t9 / 3 : 1, dx = d.ks == 3 ? t9 - 3 * (t9 / 3) : 1;
+        // branch-free (round 3): unsigned range checks combined with &, so hipcc emits no
+        // exec-mask branches per row (the && chain compiled to three nested saveexec blocks)
 #pragma unroll
         for (int j = 0; j < C::NA; ++j) {
-          int ih = poh[j] * d.stride + dy - 1, iw = pow_[j] * d.stride + dx - 1;
+          const int ih = poh[j] * d.stride + dy - 1, iw = pow_[j] * d.stride + dx - 1;
           const int fin = pfr[j] + dt;
-          const bool ok = ih >= 0 && ih < hgrid && iw >= 0 && iw < wgrid && fin >= 0 && fin < d.frames_in;
-          ih >>= d.upsample;
-          iw >>= d.upsample;
-          const uint32_t pix = (uint32_t)(((pimg[j] + dt) * d.h_in + ih) * d.w_in + iw);
+          const bool ok = ((uint32_t)ih < (uint32_t)hgrid) & ((uint32_t)iw < (uint32_t)wgrid) &
+                          ((uint32_t)fin < (uint32_t)d.frames_in);
+          const uint32_t pix = (uint32_t)(((pimg[j] + dt) * d.h_in + (ih >> d.upsample)) * d.w_in + (iw >> d.upsample));
           aoff0[j] = ok ? pix * (uint32_t)(d.lda0 * 2) + lcs(j & 1) : G2_OOB;
           aoff1[j] = ok ? pix * (uint32_t)(d.lda1 * 2) + lcs(j & 1) : G2_OOB;
         }
       }
-      const bool s0 = c_ci < d.k0;
+      const bool s0 = c_ci < (int)d.k0;
       const uint32_t coff = (uint32_t)(s0 ? c_ci : c_ci - (int)d.k0) * 2;
+      // a tap outside the image keeps G2_OOB + coff >= 2^31 > the buffer's num_records (< 2^31,
+      // checked by plan()): still out of range, read as zeros — no per-piece select
 #pragma unroll
-      for (int j = 0; j < C::NA; ++j) {
-        const uint32_t o = s0 ? aoff0[j] : aoff1[j];
-        dma16(s0 ? ra0 : ra1, la + (wid * 4 + j) * 1024, o == G2_OOB ? G2_OOB : o + coff);
-      }
+      for (int j = 0; j < C::NA; ++j)
+        dma16(s0 ? ra0 : ra1, la + (wid * 4 + j) * 1024, (s0 ? aoff0[j] : aoff1[j]) + coff);
       c_ci += BK;
       if (c_ci == cin) { c_ci = 0; ++c_tap; c_new = true; }
     }
@@ -995,7 +996,7 @@ __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, u
   auto dma_x = [&](int q, const G3Cursor& c, int T) {  // X part q of flat K-tile T (at cursor c)
     char* st = smem + (T & 1) * G3_STAGE;
     const int kb = (c.kt0 + c.t) * BK;
-    const bool s0 = kb < d.k0;
+    const bool s0 = kb < (int)d.k0;
     const uint32_t koff = (uint32_t)(s0 ? kb : kb - (int)d.k0) * 2;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -1435,7 +1436,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
         dma16(rbias, bs + 1024, nb0 + 1024);
       }
       if constexpr (MODE == VD_A_DENSE) {
-        const bool s0 = kb < d.k0;
+        const bool s0 = kb < (int)d.k0;
         const uint32_t koff = (uint32_t)(s0 ? kb : kb - (int)d.k0) * 2;
 #pragma unroll
         for (int j = 0; j < C::NAMAX; ++j)
@@ -1447,7 +1448,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
 #pragma unroll
           for (int j = 0; j < C::NAMAX; ++j) {
             int ih = (pohw[j] >> 16) * d.stride + dy - 1, iw = (pohw[j] & 0xffff) * d.stride + dx - 1;
-            const bool ok = ih >= 0 && ih < hgrid && iw >= 0 && iw < wgrid;
+            const bool ok = ((uint32_t)ih < (uint32_t)hgrid) & ((uint32_t)iw < (uint32_t)wgrid);  // branch-free
             ih >>= d.upsample;
             iw >>= d.upsample;
             const uint32_t pix = (uint32_t)(pimg[j] + ih * d.w_in + iw);
@@ -1455,12 +1456,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
             aoff1[j] = ok ? pix * (uint32_t)(d.lda1 * 2) + lc16 : G2_OOB;
           }
         }
-        const bool s0 = c_ci < d.k0;
+        const bool s0 = c_ci < (int)d.k0;
         const uint32_t coff = (uint32_t)(s0 ? c_ci : c_ci - (int)d.k0) * 2;
 #pragma unroll
         for (int j = 0; j < C::NAMAX; ++j) {
           const uint32_t o = s0 ? aoff0[j] : aoff1[j];
-          if (j < na_w) dma16(s0 ? ra0 : ra1, la + (wid + C::NW * j) * 1024, o == G2_OOB ? G2_OOB : o + coff);
+          if (j < na_w) dma16(s0 ? ra0 : ra1, la + (wid + C::NW * j) * 1024, o + coff);
         }
       }
 #pragma unroll
@@ -1700,7 +1701,7 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
     char* lb = la + G6_A;
     const int kb = ikt * BK;
     if constexpr (MODE == VD_A_DENSE) {
-      const bool s0 = kb < d.k0;
+      const bool s0 = kb < (int)d.k0;
       const uint32_t koff = (uint32_t)(s0 ? kb : kb - (int)d.k0) * 2;
 #pragma unroll
       for (int j = 0; j < 2; ++j) dma16(s0 ? ra0 : ra1, la + (2 * wid + j) * 1024, (s0 ? aoff0[j] : aoff1[j]) + koff);
@@ -1711,7 +1712,7 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           int ih = (pohw[j] >> 16) * d.stride + dy - 1, iw = (pohw[j] & 0xffff) * d.stride + dx - 1;
-          const bool ok = ih >= 0 && ih < hgrid && iw >= 0 && iw < wgrid;
+          const bool ok = ((uint32_t)ih < (uint32_t)hgrid) & ((uint32_t)iw < (uint32_t)wgrid);  // branch-free
           ih >>= d.upsample;
           iw >>= d.upsample;
           const uint32_t pix = (uint32_t)(pimg[j] + ih * d.w_in + iw);
@@ -1719,12 +1720,12 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
           aoff1[j] = ok ? pix * (uint32_t)(d.lda1 * 2) + lc16 : G2_OOB;
         }
       }
-      const bool s0 = c_ci < d.k0;
+      const bool s0 = c_ci < (int)d.k0;
       const uint32_t coff = (uint32_t)(s0 ? c_ci : c_ci - (int)d.k0) * 2;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const uint32_t o = s0 ? aoff0[j] : aoff1[j];
-        dma16(s0 ? ra0 : ra1, la + (2 * wid + j) * 1024, o == G2_OOB ? G2_OOB : o + coff);
+        dma16(s0 ? ra0 : ra1, la + (2 * wid + j) * 1024, o + coff);
       }
       c_ci += BK;
       if (c_ci == cin) { c_ci = 0; ++c_tap; c_new = true; }
