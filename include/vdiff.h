@@ -125,9 +125,9 @@ int vd_gemm_force_v1(int32_t on);
  * automatic plan with one change undone: 12 = v2 / v6 fragment reads in round 1's order,
  * 13 / 14 = v2 fragment reads pipelined (the default) / all ahead, 15 = v3 with gemm_epilogue
  * instead of the LDS-bias epilogue, 16 = v5 W fragments in halves instead of the rolling window;
- * round 3: 17 / 18 = the automatic plan with v2's 256 x 160 tiles in the 32x32x16 MFMA form
- * (8 waves of 32 rows) for every conv / for convs and dense GEMMs (not GEGLU), 19 = never
- * (the automatic plan takes it for convs with K <= 2880 at M >= 65536 only).
+ * round 3: 17 / 18 / 19 = the automatic plan with v2's 256 x 160 tiles in the 32x32x16 MFMA form
+ * (8 waves of 32 rows) for every conv / for convs and dense GEMMs (not GEGLU) / for convs with
+ * K <= 2880 at M >= 65536 (the automatic plan itself never takes it: measured slower).
  * Every path computes the same arithmetic (the K order of each output is fixed). */
 int vd_gemm_select_path(int32_t path);
 

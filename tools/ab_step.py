@@ -9,8 +9,8 @@ variance is ~3 %): python tools/ab_step.py MODE [frames] — alternates two capt
        (vd_gemm_select_path 0 / 12 / 13 / 14)
   v3e  v3 GEMM with the LDS-bias load-free epilogue vs gemm_epilogue (vd_gemm_select_path 0 vs 15)
   roll v5 GEMM with the rolling W-fragment window vs round 1's halves (vd_gemm_select_path 0 vs 16)
-  mf   v2 in the 32x32x16 form on the short-K level-1 convs (the automatic plan) vs never
-       (vd_gemm_select_path 0 vs 19)"""
+  mf   v2 in the 32x32x16 form on the short-K level-1 convs vs the automatic plan (16x16x32)
+       (vd_gemm_select_path 19 vs 0)"""
 import sys
 import time
 from pathlib import Path
@@ -55,7 +55,7 @@ elif mode == "ln":
     ops.gemm_ln = orig
 elif mode == "mf":
     from vdiff._lib import lib
-    for name, path in (("mf32-auto", 0), ("mf32-never", 19)):
+    for name, path in (("mf32-L1conv", 19), ("mf32-never", 0)):
         lib().vd_gemm_select_path(path)  # the plan is fixed at capture
         loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
     lib().vd_gemm_select_path(0)

@@ -1950,12 +1950,13 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
 }
 
 // v2 in the 32x32x16 form (gemm2_kernel<160, *, 1, 1>; round 3): half the MFMA instructions, a
-// third more fragment reads.  Measured (tools/kbench.py, profiles/r03m_gemm_mfma32_ab.txt): 5 %
-// faster on the level-1 320 -> 320 conv (K 2880), 7-11 % slower on the longer-K convs and most
-// dense shapes — so the automatic plan (g_g2_mf -1) takes it for convs with K <= 2880 at
-// M >= 65536 only; 1 = every conv, 2 = convs and dense GEMMs, 0 = never (vd_gemm_select_path
-// 17 / 18 / 19, A/B).  Not for GEGLU (gemm_epilogue32 has none).
-int g_g2_mf = -1;
+// third more fragment reads.  Measured (tools/kbench.py, tools/ab_step.py mf,
+// profiles/r03m_gemm_mfma32_ab.txt): 7-11 % slower on the longer-K convs and most dense shapes;
+// on the level-1 320 -> 320 conv it won 5 % (-0.18 ms/step in-process) until the branch-free conv
+// loader took the same VALU out of the 16x16 form, after which it lost (+0.18 ms/step) — so the
+// automatic plan never takes it (g_g2_mf 0); -1 = the short-K level-1 convs only, 1 = every conv,
+// 2 = convs and dense GEMMs (vd_gemm_select_path 17 / 18, A/B).  Not for GEGLU.
+int g_g2_mf = 0;
 inline bool mf32_ok(const vd_gemm_desc& d) {
   if (d.act == VD_ACT_GEGLU || d.N % 32 || d.ldc % 8 || ((uintptr_t)d.out & 15)) return false;
   if (g_g2_mf < 0) return d.a_mode == VD_A_CONV3X3 && d.K <= 2880 && d.M >= 65536;
@@ -2285,8 +2286,8 @@ extern "C" int vd_gemm_force_v1(int32_t on) {
 }
 extern "C" int vd_gemm_select_path(int32_t path) {
   if (path < 0 || path > 19 || path == 4) return VD_EINVAL;
-  g_g2_mf = path == 17 ? 1 : path == 18 ? 2 : path == 19 ? 0 : -1;
-  if (path >= 17) path = 0;  // auto plan, v2 in the 32x32x16 form for convs / convs + dense (A/B)
+  g_g2_mf = path == 17 ? 1 : path == 18 ? 2 : path == 19 ? -1 : 0;
+  if (path >= 17) path = 0;  // auto plan, v2 in the 32x32x16 form for convs / convs + dense / short-K L1 convs (A/B)
   g_g4_roll = path != 16;
   if (path == 16) path = 0;  // auto plan, v5 with round 1's fragment halves (A/B)
   g_g3_fast = path != 15;
