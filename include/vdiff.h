@@ -214,7 +214,9 @@ int vd_attention_force_v1(int32_t on);
  * attention) with K two tiles ahead in a 3-slot LDS ring and V one ahead / K and V one tile
  * ahead (the default), 22 = DMA ablation (tile 0 only: WRONG results, timing only); 25 / 26 /
  * 27 = flash40's K/V LDS-DMA issued by waves 4-7 only, in their softmax phase / by waves 0-5
- * (the default) / by waves 0-3 only, in their MFMA phase; 31 / 32 = vd_motion_qkv_attention's
+ * (the default) / by waves 0-3 only, in their MFMA phase, 28 = by all eight waves, 29 = as 26
+ * with waves 4-5 issuing in their MFMA phase, 30 = all eight waves (2, 2, 1, 1 pieces per
+ * group) each in its MFMA phase (half the pieces in each barrier interval); 31 / 32 = vd_motion_qkv_attention's
  * round-2 kernel / round-3 kernel (the default); 33 / 34 = the fused motion kernel at any grid
  * size / only from one round of the chip (the default); 35 = vd_attention_fp8's round-1 kernel,
  * 36-39 = round 3's LDS-DMA-ring kernel with lazy offset + MFMA row sum / eager offset + MFMA

@@ -32,7 +32,7 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int KT = 64;   // keys per tile
-int g_f4_g1 = 0;         // flash40 LDS-DMA issued by the second wave group only (A/B, vd_attention_select 25/26)
+int g_f4_g1 = 0;         // flash40 LDS-DMA issuer placement (A/B, vd_attention_select 25-30; 26 = 0 the default)
 int g_flash32 = 1;       // d = 40: 1 = automatic (flash40 for >= 4 key tiles, else flash32), 7 = flash32 only,
                          // 6 = flash40 wherever it applies, 8 = flash40 stamped (diagnostic),
                          // 2 = flash32pp (8-wave pipeline), 0 = flash_attn 16x16x32
@@ -1365,7 +1365,7 @@ __device__ uint64_t f4_stamps[F4_NW * F4_NST];
 
 template <bool UNITC, bool ST = false, int G1 = 0>
 __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F4Dma& dma, bool issuer,
-                                        bool g0, int64_t skv, bf16x8 (&qf)[F4_QB][3], f32x16 (&oacc)[2][F4_QB],
+                                        bool g0, bool one, int64_t skv, bf16x8 (&qf)[F4_QB][3], f32x16 (&oacc)[2][F4_QB],
                                         uint32_t kl0, uint32_t v0l, uint32_t v1l, int hh, float c) {
   int nst = 0;
   const bool stw = ST && blockIdx.x == 0;
@@ -1561,7 +1561,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   // tile u's DMA: issued at phase 2u-4 (u >= 2), waited for at the end of phase 2u-1
   auto issue = [&](int u) {
     if (issuer && u < T) {
-      if (G1 == 3 && !g0) f4_issue<1>(dma, lds0, u, skv);
+      if (one) f4_issue<1>(dma, lds0, u, skv);
       else f4_issue<G1 == 1 || G1 == 2 ? 3 : 2>(dma, lds0, u, skv);
     }
     stamp(5);
@@ -1569,12 +1569,16 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   auto wait_tile = [&](int u) {
     if (issuer && u < T) {
       if (u + 1 < T) {
-        if (G1 == 3 && !g0) f4_wait_vm<1>();
+        if (one) f4_wait_vm<1>();
         else f4_wait_vm<G1 == 1 || G1 == 2 ? 3 : 2>();
       }
       else f4_wait_vm<0>();
     }
   };
+  // G1 = 4 / 5: the second group issues at the start of its M phase instead of its V phase, so
+  // half the pieces go out in each of the two barrier intervals (the other group's M phase runs
+  // in the other interval) instead of all twelve in one
+  constexpr bool G1M = G1 == 4 || G1 == 5;
 
   // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere
   issue(0);
@@ -1594,7 +1598,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   if (!g0) wait_tile(1);
   bar();
   for (int t = 0; t < T; ++t) {
-    if (!g0) issue(t + 3);
+    if (!g0 && !G1M) issue(t + 3);
     softmax();
     __builtin_amdgcn_sched_barrier(0);
     stamp(3);
@@ -1610,7 +1614,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
     stamp(4);
     if (g0) wait_tile(t + 1);
     bar();
-    if (g0) issue(t + 3);
+    if (g0 || G1M) issue(t + 3);
     mphase(t);
     if (!g0) wait_tile(t + 2);
     bar();
@@ -1681,7 +1685,9 @@ __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ 
   // three each: G1 = 1 the second group (waves 4-7, in its softmax phase: measured 930 vs 805 us),
   // G1 = 2 the first group (waves 0-3, in its PV / QK^T phase: 912 us), G1 = 3 all eight waves
   // (waves 0-3 two pieces each in their M phase, waves 4-7 one each in their V phase)
-  const bool issuer = G1 == 1 ? wave >= 4 : (G1 == 2 ? wave < 4 : (G1 == 3 ? true : wave < 6));
+  // G1 = 5: all eight waves, group g's pieces 6g..6g+5 as 2, 2, 1, 1 over its waves
+  const bool issuer = G1 == 1 ? wave >= 4 : (G1 == 2 ? wave < 4 : (G1 == 3 || G1 == 5 ? true : wave < 6));
+  const bool one = (G1 == 3 && wave >= 4) || (G1 == 5 && (wave & 3) >= 2);
   {
     const uint32_t ldkb = (uint32_t)ldk * 2, ldvb = (uint32_t)ldv * 2;
     const u32x4 rk = f4_rsrc(kb_ptr, (uint32_t)(skv - 1) * ldkb + 2 * D);
@@ -1690,7 +1696,9 @@ __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ 
 #pragma unroll
     for (int i = 0; i < (G1 == 1 || G1 == 2 ? 3 : 2); ++i) {
       const int p = G1 == 1 ? 3 * (wave - 4) + i
-                            : (G1 == 2 ? 3 * wave + i : (G1 == 3 && wave >= 4 ? 8 + (wave - 4) : 2 * wave + i));
+                    : G1 == 2 ? 3 * wave + i
+                    : G1 == 5 ? 6 * (wave >> 2) + ((wave & 3) < 2 ? 2 * (wave & 3) + i : 2 + (wave & 3))
+                    : (G1 == 3 && wave >= 4 ? 8 + (wave - 4) : 2 * wave + i);
       uint32_t row = lane, col = 0, step = 0, lds = 0;
       u32x4 rs = r1;
       if (p < 5) {
@@ -1718,7 +1726,7 @@ __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ 
                        (uint32_t)((4 * hh + qq) * 16);
 
   f32x16 oacc[2][QB];
-  if (__syncthreads_or(f4_loop<UNITC, ST, G1>(smem, lds0, dma, issuer, g0, skv, qf, oacc, kl0, v0l, v1l, hh, c))) {
+  if (__syncthreads_or(f4_loop<UNITC, ST, G1>(smem, lds0, dma, issuer, g0, one, skv, qf, oacc, kl0, v0l, v1l, hh, c))) {
     // a score jumped > ~100 (log2) past mu somewhere in the block: no output here; a NaN in
     // element (first query, d 0) of each 256-query quarter tells flash32's exact fix-up pass,
     // launched right after, to recompute that quarter
@@ -1795,6 +1803,17 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
         if (c != 1.0f) return VD_EUNSUPPORTED;
         hipLaunchKernelGGL((flash40_kernel<true, true>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,
                            ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+      } else if (c == 1.0f && (g_f4_g1 == 4 || g_f4_g1 == 5)) {
+        if (g_f4_g1 == 4)
+          hipLaunchKernelGGL((flash40_kernel<true, false, 4>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
+                             (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
+                             out_f32);
+        else
+          hipLaunchKernelGGL((flash40_kernel<true, false, 5>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
+                             (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
+                             out_f32);
         hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                            (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
       } else if (c == 1.0f && g_f4_g1 == 3) {
@@ -2365,8 +2384,10 @@ extern "C" int vd_attention_select(int32_t kernel) {
     g_mq_ver = kernel - 30;
     return VD_OK;
   }
-  if (kernel >= 25 && kernel <= 28) {  // flash40 DMA issuers: 25 waves 4-7, 26 waves 0-5 (default), 27 waves 0-3,
-    g_f4_g1 = kernel == 25 ? 1 : (kernel == 27 ? 2 : (kernel == 28 ? 3 : 0));  // 28 all eight (2 / 1 pieces)
+  if (kernel >= 25 && kernel <= 30) {  // flash40 DMA issuers: 25 waves 4-7, 26 waves 0-5 (default), 27 waves 0-3,
+    // 28 all eight (2 / 1 pieces); 29 = 26 with the second group issuing in its M phase, 30 = all eight
+    // waves (2, 2, 1, 1 per group), each group in its M phase
+    g_f4_g1 = kernel == 25 ? 1 : kernel == 27 ? 2 : kernel == 28 ? 3 : kernel == 29 ? 4 : kernel == 30 ? 5 : 0;
     return VD_OK;
   }
   if (kernel >= 20 && kernel <= 22) {  // d = 512 (flash512): DMA placement A/B, 22 = ablation
