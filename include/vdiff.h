@@ -127,7 +127,8 @@ int vd_gemm_force_v1(int32_t on);
  * instead of the LDS-bias epilogue, 16 = v5 W fragments in halves instead of the rolling window;
  * round 3: 17 / 18 / 19 = the automatic plan with v2's 256 x 160 tiles in the 32x32x16 MFMA form
  * (8 waves of 32 rows) for every conv / for convs and dense GEMMs (not GEGLU) / for convs with
- * K <= 2880 at M >= 65536 (the automatic plan itself never takes it: measured slower).
+ * K <= 2880 at M >= 65536 (the automatic plan itself never takes it: measured slower); 20 = v2's
+ * conv rows set up with round 2's int64 divisions instead of 32-bit shifts.
  * Every path computes the same arithmetic (the K order of each output is fixed). */
 int vd_gemm_select_path(int32_t path);
 

@@ -10,7 +10,8 @@ variance is ~3 %): python tools/ab_step.py MODE [frames] — alternates two capt
   v3e  v3 GEMM with the LDS-bias load-free epilogue vs gemm_epilogue (vd_gemm_select_path 0 vs 15)
   roll v5 GEMM with the rolling W-fragment window vs round 1's halves (vd_gemm_select_path 0 vs 16)
   mf   v2 in the 32x32x16 form on the short-K level-1 convs vs the automatic plan (16x16x32)
-       (vd_gemm_select_path 19 vs 0)"""
+       (vd_gemm_select_path 19 vs 0)
+  fd   v2 conv row setup with 32-bit shifts (the default) vs round 2's int64 divisions (0 vs 20)"""
 import sys
 import time
 from pathlib import Path
@@ -53,6 +54,12 @@ elif mode == "ln":
         ops.gemm_ln = fn
         loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
     ops.gemm_ln = orig
+elif mode == "fd":
+    from vdiff._lib import lib
+    for name, path in (("div-shift", 0), ("div-int64", 20)):
+        lib().vd_gemm_select_path(path)  # the plan is fixed at capture
+        loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
+    lib().vd_gemm_select_path(0)
 elif mode == "mf":
     from vdiff._lib import lib
     for name, path in (("mf32-L1conv", 19), ("mf32-never", 0)):

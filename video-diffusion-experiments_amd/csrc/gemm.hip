@@ -30,6 +30,17 @@ __device__ __forceinline__ int lds_off(int row, int chunk) {
   return row * BK + ((chunk ^ (row & 7)) << 3);
 }
 
+// a / b for 0 <= a < 2^31 and a wave-uniform b > 0 (round 3): every image size, row width and
+// frame count of the UNet is a power of two, so the common case is a shift; hipcc's 32-bit
+// division is ~25 VALU, the 64-bit one (an int64 row index) ~100
+struct Div {
+  int b, sh;
+  __device__ __forceinline__ explicit Div(int b_) : b(b_), sh((b_ & (b_ - 1)) == 0 ? __builtin_ctz((uint32_t)b_) : -1) {}
+  __device__ __forceinline__ int operator()(int a) const {
+    return sh >= 0 ? (int)((uint32_t)a >> sh) : (int)((uint32_t)a / (uint32_t)b);
+  }
+};
+
 template <int MB, int NB>
 __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], int mbase,
                                               int nbase, int lane) {
@@ -52,6 +63,16 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
   const bool wide = (N % 8) == 0 && !d.out_f32 && (d.ldc % 8) == 0 && (((uintptr_t)d.out) & 15) == 0 &&
                     (!d.res || ((d.ld_res % 8) == 0 && (((uintptr_t)d.res) & 15) == 0));
   const int wcol = 16 * (fq & 1) + 8 * (fq >> 1);  // lane's column offset inside a swapped pair
+  // the row-bias row of each of the lane's MB rows, divided once (not per column block)
+  int rbr[MB];
+  if (d.rowbias) {
+    const Div rdiv((int)d.rb_div);
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      const int m = mbase + b * 16 + fr;
+      rbr[b] = rdiv(m < M ? m : 0);
+    }
+  }
   if (d.act == VD_ACT_GEGLU) {
     if constexpr (NB % 4 == 0) {
       if (wide) {
@@ -156,7 +177,7 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
         }
         if (!mok_ || !nok) continue;
         if (d.rowbias) {
-          const float* rbrow = d.rowbias + (int64_t)(mrow_ / (int)d.rb_div) * d.ld_rb;
+          const float* rbrow = d.rowbias + (int64_t)rbr[b] * d.ld_rb;
           const float4 t0 = *(const float4*)(rbrow + n), t1 = *(const float4*)(rbrow + n + 4);
           o[0] += t0.x; o[1] += t0.y; o[2] += t0.z; o[3] += t0.w;
           o[4] += t1.x; o[5] += t1.y; o[6] += t1.z; o[7] += t1.w;
@@ -194,7 +215,7 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = acc[a][b][j] + bv[j];
       if (d.rowbias) {
-        const float4 t = *(const float4*)(d.rowbias + (int64_t)(mrow_ / (int)d.rb_div) * d.ld_rb + n);
+        const float4 t = *(const float4*)(d.rowbias + (int64_t)rbr[b] * d.ld_rb + n);
         o[0] += t.x; o[1] += t.y; o[2] += t.z; o[3] += t.w;
       }
       if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU) {
@@ -431,7 +452,7 @@ __device__ __forceinline__ void gemm_epilogue32(const vd_gemm_desc& d, f32x16 (&
   const int M = (int)d.M, N = (int)d.N;
   const int m = mbase + (lane & 31), hh = lane >> 5;
   if (m >= M) return;
-  const float* rbrow = d.rowbias ? d.rowbias + (int64_t)(m / (int)d.rb_div) * d.ld_rb : nullptr;
+  const float* rbrow = d.rowbias ? d.rowbias + (int64_t)Div((int)d.rb_div)(m) * d.ld_rb : nullptr;
 #pragma unroll
   for (int a = 0; a < NB; ++a) {
     const int n0 = nbase + 32 * a;
@@ -481,7 +502,7 @@ __device__ __forceinline__ void gemm_epilogue32(const vd_gemm_desc& d, f32x16 (&
 // PF = 1 issues all 18 reads of the K-tile right after the barrier (sched_barrier), PF = 2 (the
 // default) issues k-step 0's 9 reads, then interleaves k-step 1's reads one per two of k-step
 // 0's MFMAs (sched_group_barrier), so the MFMA chain waits on counted lgkmcnt only.
-template <int BN, int MODE, int PF = 1, int MF = 0>
+template <int BN, int MODE, int PF = 1, int MF = 0, bool FD = true>
 __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                          uint32_t a1_bytes, uint32_t w_bytes,
                                                          int split) {
@@ -532,9 +553,14 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
   int c_tap = 0, c_ci = 0;
   bool c_new = true;
   auto unit_kr = [&](int u, int& kt0, int& kt1) {
+    if (split == 1) {  // (the unsplit common case: no division)
+      kt0 = 0;
+      kt1 = nk_all;
+      return;
+    }
     const int sp = u % split;
-    kt0 = (int)((int64_t)nk_all * sp / split);
-    kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
+    kt0 = nk_all * sp / split;  // nk_all * split < 2^31
+    kt1 = nk_all * (sp + 1) / split;
   };
   auto setup_unit = [&](int u) {  // per-unit row offsets for the issue cursor
     const int tile = u / split;
@@ -556,7 +582,22 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
         aoff0[j] = (uint32_t)(m * d.lda0 * 2) + lcs(j & 1);
         aoff1[j] = (uint32_t)(m * d.lda1 * 2) + lcs(j & 1);
       }
-    } else {
+    } else if constexpr (FD) {  // 32-bit rows, shifts for power-of-two sizes (round 3)
+      const int hw = d.h_out * d.w_out;
+      const Div dhw(hw), dfr(d.frames_out), dw(d.w_out);
+#pragma unroll
+      for (int j = 0; j < C::NA; ++j) {
+        int m = (int)m0 + (wid * 4 + j) * 8 + rb;
+        m = m < (int)M ? m : (int)M - 1;
+        const int img = dhw(m);
+        const int vid = dfr(img);
+        pfr[j] = img - vid * d.frames_out + d.t_off - d.kt / 2;  // frame of temporal tap 0
+        pimg[j] = vid * d.frames_in + pfr[j];
+        const int p = m - img * hw;
+        poh[j] = dw(p);
+        pow_[j] = p - poh[j] * d.w_out;
+      }
+    } else {  // round 2's form (int64 rows, divisions): the A/B arm
       const int hw = d.h_out * d.w_out;
 #pragma unroll
       for (int j = 0; j < C::NA; ++j) {
@@ -564,12 +605,14 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
         m = m < M ? m : M - 1;
         const int img = (int)(m / hw);
         const int vid = img / d.frames_out;
-        pfr[j] = img - vid * d.frames_out + d.t_off - d.kt / 2;  // frame of temporal tap 0
+        pfr[j] = img - vid * d.frames_out + d.t_off - d.kt / 2;
         pimg[j] = vid * d.frames_in + pfr[j];
         const int p = (int)(m - (int64_t)img * hw);
         poh[j] = p / d.w_out;
         pow_[j] = p - poh[j] * d.w_out;
       }
+    }
+    if constexpr (MODE != VD_A_DENSE) {
       c_tap = kt0 * BK / cin;
       c_ci = kt0 * BK - c_tap * cin;
       c_new = true;
@@ -1382,9 +1425,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
   int c_tap = 0, c_ci = 0;
   bool c_new = true;
   auto unit_kr = [&](int u, int& kt0, int& kt1) {
+    if (split == 1) {  // (the unsplit common case: no division)
+      kt0 = 0;
+      kt1 = nk_all;
+      return;
+    }
     const int sp = u % split;
-    kt0 = (int)((int64_t)nk_all * sp / split);
-    kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
+    kt0 = nk_all * sp / split;  // nk_all * split < 2^31
+    kt1 = nk_all * (sp + 1) / split;
   };
   auto setup_unit = [&](int u) {
     const int tile = u / split;
@@ -1408,13 +1456,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
       }
     } else {
       const int hw = d.h_out * d.w_out;
+      const Div dhw(hw), dw(d.w_out);
 #pragma unroll
       for (int j = 0; j < C::NAMAX; ++j) {
-        int64_t m = m0 + (wid + C::NW * j) * 16 + rb;
-        m = m < M ? m : M - 1;
-        const int img = (int)(m / hw);
-        const int p = (int)(m - (int64_t)img * hw);
-        const int oh = p / d.w_out;
+        int m = (int)m0 + (wid + C::NW * j) * 16 + rb;
+        m = m < (int)M ? m : (int)M - 1;
+        const int img = dhw(m);
+        const int p = m - img * hw;
+        const int oh = dw(p);
         pimg[j] = img * d.h_in * d.w_in;
         pohw[j] = (oh << 16) | (p - oh * d.w_out);
       }
@@ -1680,9 +1729,9 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
       aoff1[j] = (uint32_t)(m * d.lda1 * 2) + lc16;
     } else {
       const int hw = d.h_out * d.w_out;
-      const int img = (int)(m / hw);
-      const int p = (int)(m - (int64_t)img * hw);
-      const int oh = p / d.w_out;
+      const int img = Div(hw)((int)m);
+      const int p = (int)m - img * hw;
+      const int oh = Div(d.w_out)(p);
       pimg[j] = img * d.h_in * d.w_in;
       pohw[j] = (oh << 16) | (p - oh * d.w_out);
     }
@@ -1877,7 +1926,7 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
       v[0] += a4.x; v[1] += a4.y; v[2] += a4.z; v[3] += a4.w;
     }
     if (d.rowbias) {
-      const float4 a4 = *(const float4*)(d.rowbias + (m / d.rb_div) * d.ld_rb + o);
+      const float4 a4 = *(const float4*)(d.rowbias + (int64_t)Div((int)d.rb_div)((int)m) * d.ld_rb + o);
       v[0] += a4.x; v[1] += a4.y; v[2] += a4.z; v[3] += a4.w;
     }
     if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU)
@@ -1894,15 +1943,19 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
 }
 
 // Sum the split-K slabs and apply the GEMM epilogue (4 output columns per thread).
+// Index math in 32 bits (M * N < 2^31, checked by vd_gemm: M * ldc): a 64-bit division per element
+// was most of this memory-bound kernel's instructions (round 3).
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, int split) {
   const int64_t M = d.M, N = d.N;
   const bool geglu = d.act == VD_ACT_GEGLU;
   const int64_t nout = geglu ? N / 2 : N;
-  const int64_t total = M * (nout / 4);
+  const int total = (int)(M * (nout / 4));
+  const Div dq((int)(nout / 4)), drb(d.rowbias ? (int)d.rb_div : 1);
   const float* ws = (const float*)d.ws;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t m = i / (nout / 4);
-    const int64_t o = (i - m * (nout / 4)) * 4;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int m32 = dq(i);
+    const int64_t m = m32;
+    const int64_t o = (int64_t)(i - m32 * (int)(nout / 4)) * 4;
     float o4[4];
     if (geglu) {
       const int64_t nh = (o / 16) * 32 + (o % 16), ng = nh + 16;
@@ -1931,7 +1984,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
         v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
       }
       if (d.rowbias) {
-        const float4 a = *(const float4*)(d.rowbias + (m / d.rb_div) * d.ld_rb + o);
+        const float4 a = *(const float4*)(d.rowbias + (int64_t)drb(m32) * d.ld_rb + o);
         v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
       }
       if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU)
@@ -1957,6 +2010,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
 // automatic plan never takes it (g_g2_mf 0); -1 = the short-K level-1 convs only, 1 = every conv,
 // 2 = convs and dense GEMMs (vd_gemm_select_path 17 / 18, A/B).  Not for GEGLU.
 int g_g2_mf = 0;
+int g_g2_fd = 1;  // 0: v2's conv row setup with int64 divisions (round 2's form; vd_gemm_select_path(20), A/B)
 inline bool mf32_ok(const vd_gemm_desc& d) {
   if (d.act == VD_ACT_GEGLU || d.N % 32 || d.ldc % 8 || ((uintptr_t)d.out & 15)) return false;
   if (g_g2_mf < 0) return d.a_mode == VD_A_CONV3X3 && d.K <= 2880 && d.M >= 65536;
@@ -1983,7 +2037,10 @@ int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
       goto launched;
     }
   }
-  if (d.a_mode == VD_A_CONV3X3) {
+  if (d.a_mode == VD_A_CONV3X3 && !g_g2_fd && pf == 2) {  // A/B: round 2's conv row setup
+    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3, 2, 0, false>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b,
+                       a1b, wb, split);
+  } else if (d.a_mode == VD_A_CONV3X3) {
     if (pf == 0) G2_LAUNCH(VD_A_CONV3X3, 0);
     else if (pf == 1) G2_LAUNCH(VD_A_CONV3X3, 1);
     else G2_LAUNCH(VD_A_CONV3X3, 2);
@@ -2285,7 +2342,9 @@ extern "C" int vd_gemm_force_v1(int32_t on) {
   return VD_OK;
 }
 extern "C" int vd_gemm_select_path(int32_t path) {
-  if (path < 0 || path > 19 || path == 4) return VD_EINVAL;
+  if (path < 0 || path > 20 || path == 4) return VD_EINVAL;
+  g_g2_fd = path != 20;
+  if (path == 20) path = 0;  // auto plan, v2 conv rows set up with round 2's divisions (A/B)
   g_g2_mf = path == 17 ? 1 : path == 18 ? 2 : path == 19 ? -1 : 0;
   if (path >= 17) path = 0;  // auto plan, v2 in the 32x32x16 form for convs / convs + dense / short-K L1 convs (A/B)
   g_g4_roll = path != 16;
