@@ -1000,8 +1000,8 @@ __global__ __launch_bounds__(G3_NT, 1) void gemm3_kernel(const vd_gemm_desc d, u
     c.t = 0;
     if (u < units) {
       const int tile = u / split, sp = u % split;
-      c.kt0 = (int)((int64_t)nk_all * sp / split);
-      c.nk = (int)((int64_t)nk_all * (sp + 1) / split) - c.kt0;
+      c.kt0 = split == 1 ? 0 : nk_all * sp / split;  // 32-bit: nk_all * split < 2^31
+      c.nk = (split == 1 ? nk_all : nk_all * (sp + 1) / split) - c.kt0;
       c.m0 = (tile / tiles_n) * G3_BM;
       c.n0 = (tile % tiles_n) * G3_BN;
     }
@@ -1705,7 +1705,7 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
   const int tile = lid / split, sp = lid % split;
   const int64_t m0 = (int64_t)(tile / tiles_n) * G6_BM, n0 = (int64_t)(tile % tiles_n) * G6_BN;
   const int nk_all = (int)(K / BK);
-  const int kt0 = (int)((int64_t)nk_all * sp / split), kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
+  const int kt0 = split == 1 ? 0 : nk_all * sp / split, kt1 = split == 1 ? nk_all : nk_all * (sp + 1) / split;
   const int nk = kt1 - kt0;
 
   const int rb = lane >> 3;

@@ -227,9 +227,11 @@ __global__ __launch_bounds__(NT) void gn_apply_kernel(const bf16_t* x0, int64_t 
                                                       int64_t ldy) {
   const int64_t nch = C / 8;
   const int64_t total = rows * nch;
+  // 32-bit row / chunk split (the common case; an int64 division per chunk otherwise)
+  const bool narrow = total + (int64_t)gridDim.x * NT < 0x7fffffff;
   for (int64_t idx = (int64_t)blockIdx.x * NT + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * NT) {
-    const int64_t row = idx / nch;
+    const int64_t row = narrow ? (int64_t)((uint32_t)idx / (uint32_t)nch) : idx / nch;
     const int64_t c = (idx - row * nch) * 8;
     const uint4 u = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row, c);
     const float4* sp = (const float4*)(ss + (row / pix_per_inst) * C + c);
@@ -293,24 +295,38 @@ __global__ __launch_bounds__(NT) void gn_apply_g_kernel(const bf16_t* x0, int64_
     ab[c] = make_float2(a, beta[c] - st.x * a);
   }
   __syncthreads();
-  const int64_t nch = C / 8;
+  // block-local index math in 32 bits (round 3: an int64 idx / nch and idx % nch per chunk were
+  // two 64-bit divisions per 16 bytes moved); the quotient by one fp32 reciprocal multiply and a
+  // one-step fix-up (exact: idx < 2^24, nch <= 320)
+  const int nch = (int)(C / 8);
   const int64_t r0 = (int64_t)inst * pix_per_inst + (int64_t)blk * rows_per_blk;
   const int64_t r1 = min((int64_t)inst * pix_per_inst + pix_per_inst, r0 + rows_per_blk);
-  const int64_t total = (r1 - r0) * nch;
+  const int total = (int)((r1 - r0) * nch);
+  const float rnch = 1.0f / (float)nch;
+  auto qr = [&](int idx, int& q, int& r) {
+    q = (int)((float)idx * rnch);
+    r = idx - q * nch;
+    if (r < 0) { --q; r += nch; }
+    if (r >= nch) { ++q; r -= nch; }
+  };
   constexpr int U = 4;  // 16-byte loads in flight per thread before the first store
-  for (int64_t base = threadIdx.x; base < total; base += U * NT) {
+  for (int base = threadIdx.x; base < total; base += U * NT) {
     uint4 u[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-      const int64_t idx = base + k * NT;
-      if (idx < total) u[k] = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, r0 + idx / nch, (idx % nch) * 8);
+      const int idx = base + k * NT;
+      int q, r;
+      qr(idx, q, r);
+      if (idx < total) u[k] = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, r0 + q, (int64_t)r * 8);
     }
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-      const int64_t idx = base + k * NT;
+      const int idx = base + k * NT;
       if (idx >= total) break;
-      const int64_t row = r0 + idx / nch;
-      const int64_t c = (idx % nch) * 8;
+      int q, r;
+      qr(idx, q, r);
+      const int64_t row = r0 + q;
+      const int64_t c = (int64_t)r * 8;
       float f[8];
       unpack8(u[k], f);
 #pragma unroll
