@@ -232,14 +232,15 @@ def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, ga
     return gn_apply(x, ss, pix, silu, x1=x1)
 
 
-def group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, out=None):
+def group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, out=None, n_split=None):
     """vd_gn_partial_g + vd_gn_apply_g.  Splits: <= 32 per instance (the apply prologue reads
     splits x groups records); the split count is a function of the image size alone (the same
     records whatever the instance count: frame-sharded ranks match the unsharded run bit for bit);
-    ~1024 apply blocks in all (tools/gn_bench.py)."""
+    ~1024 apply blocks in all (tools/gn_bench.py).  n_split: override (the motion norm's splits
+    per frame x frames)."""
     _dev(x, x1, gamma, beta, out)
     C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
-    n_split = max(1, min(pix // 16, 32))
+    n_split = n_split or max(1, min(pix // 16, 32))
     ws = torch.empty(n_inst, n_split, groups, 4, device=x.device, dtype=torch.float32)
     x1p, ld1 = (_p(x1), _rows(x1)) if x1 is not None else (None, 0)
     check(lib().vd_gn_partial_g(_p(x), _rows(x), x.shape[1], x1p, ld1, C, n_inst, pix, n_split, groups, _p(ws),
