@@ -911,12 +911,14 @@ def test_temporal_attention_kv(cuda, frames, qf, f0, d):
     close_bf16(got, want.reshape(batch, pos, qf, C).permute(0, 2, 1, 3).reshape(-1, C))
 
 
-@pytest.mark.parametrize("batch,positions,unit", [(2, 4096, True), (1, 4100, False), (3, 1373, True)])
+@pytest.mark.parametrize("batch,positions,unit", [(2, 4096, True), (1, 4100, False), (3, 1373, True),
+                                                   (1, 2048, False)])
 def test_motion_qkv_attention(cuda, batch, positions, unit):
     """vd_motion_qkv_attention (the level-1 motion module's Q/K/V projection fused into its
     temporal attention) equals vd_gemm + vd_temporal_attention bit for bit — ragged position
     counts (the last workgroup's idle waves), both softmax-scale forms — and fp64 SDPA of the
-    bf16 projection to bf16 rounding."""
+    bf16 projection to bf16 rounding.  The first three shapes take two positions per wave, the
+    last (256 workgroups at one, 128 at two) one."""
     C, d, heads, F = 320, 40, 8, 16
     x = rnd(batch * F * positions, C)
     w = rnd(3 * C, C, std=C ** -0.5 * 2.0)

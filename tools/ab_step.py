@@ -11,7 +11,9 @@ variance is ~3 %): python tools/ab_step.py MODE [frames] — alternates two capt
   roll v5 GEMM with the rolling W-fragment window vs round 1's halves (vd_gemm_select_path 0 vs 16)
   mf   v2 in the 32x32x16 form on the short-K level-1 convs vs the automatic plan (16x16x32)
        (vd_gemm_select_path 19 vs 0)
-  fd   v2 conv row setup with 32-bit shifts (the default) vs round 2's int64 divisions (0 vs 20)"""
+  fd   v2 conv row setup with 32-bit shifts (the default) vs round 2's int64 divisions (0 vs 20)
+  mqpw the fused motion kernel with two positions per wave (the default) vs one
+       (vd_attention_select 42 vs 40)"""
 import sys
 import time
 from pathlib import Path
@@ -54,6 +56,12 @@ elif mode == "ln":
         ops.gemm_ln = fn
         loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
     ops.gemm_ln = orig
+elif mode == "mqpw":
+    from vdiff._lib import lib
+    for name, sel in (("motion-pw2", 42), ("motion-pw1", 40)):
+        lib().vd_attention_select(sel)  # the kernel choice is fixed at capture
+        loops[name] = DenoiseLoop(unet, sched, lat, ehs, 7.5).prime()
+    lib().vd_attention_select(42)
 elif mode == "fd":
     from vdiff._lib import lib
     for name, path in (("div-shift", 0), ("div-int64", 20)):

@@ -43,18 +43,30 @@ from vdiff._lib import lib  # noqa: E402
 lib().vd_attention_select(33)  # the fused kernels at any grid size (the A/B below)
 
 flop = 2.0 * B * F * P * 3 * C * C
+# forms: round 2's kernel (31), round 3's with one position per wave (32 + 40), two per wave (32 + 41)
+forms = {"v1": (31, 42), "v2 pw1": (32, 40), "v2 pw2": (32, 41)}
+
+
+def use(f):
+    for sel in forms[f]:
+        lib().vd_attention_select(sel)
+
+
 outs = {}
-for ver in (1, 2):  # vd_attention_select(30 + ver): round 2's / round 3's fused kernel
-    lib().vd_attention_select(30 + ver)
-    outs[ver] = ops.motion_qkv_attention(x, w, B, F, P, heads, d, scale=sc).clone()
-res = {1: [], 2: []}
+for f in forms:
+    use(f)
+    outs[f] = ops.motion_qkv_attention(x, w, B, F, P, heads, d, scale=sc).clone()
+res = {f: [] for f in forms}
 for _ in range(5):
-    for ver in (1, 2):
-        lib().vd_attention_select(30 + ver)
-        res[ver].append(timeit(lambda: ops.motion_qkv_attention(x, w, B, F, P, heads, d, scale=sc, out=out)))
+    for f in forms:
+        use(f)
+        res[f].append(timeit(lambda: ops.motion_qkv_attention(x, w, B, F, P, heads, d, scale=sc, out=out)))
 lib().vd_attention_select(32)
+lib().vd_attention_select(42)
+lib().vd_attention_select(34)
 t_u = timeit(unfused)
-for ver in (1, 2):
-    t_f = sorted(res[ver])[2]
-    print(f"rows {B * F * P}: fused v{ver} {t_f:.1f} us ({flop / t_f / 1e6:.0f} TF/s on the projection)", flush=True)
-print(f"gemm + temporal attention {t_u:.1f} us; v1 == v2 bitwise: {torch.equal(outs[1], outs[2])}", flush=True)
+for f in forms:
+    t_f = sorted(res[f])[2]
+    print(f"rows {B * F * P}: fused {f} {t_f:.1f} us ({flop / t_f / 1e6:.0f} TF/s on the projection)", flush=True)
+same = all(torch.equal(outs["v1"], outs[f]) for f in forms)
+print(f"gemm + temporal attention {t_u:.1f} us; all fused forms bitwise equal: {same}", flush=True)

@@ -2368,12 +2368,16 @@ extern "C" int vd_attention_force_v1(int32_t on) {
 // flash32 only (round 2's default; automatic = flash40 from 4 key tiles, flash32 below), 9 =
 // flash40's diagnostic build (barrier stamps of workgroup 0, vd_attention_stamps).
 extern int g_a5_var;  // attention_d512.hip
-extern int g_mq_ver, g_mq_any;  // motion.hip
+extern int g_mq_ver, g_mq_any, g_mq_pw;  // motion.hip
 extern int g_fp8_ver;  // attention_fp8.hip
 
 extern "C" int vd_attention_select(int32_t kernel) {
   if (kernel >= 35 && kernel <= 39) {  // fp8 attention: round 1's kernel (35) / round 3's (36; 37-39 its A/B forms)
     g_fp8_ver = kernel - 34;
+    return VD_OK;
+  }
+  if (kernel >= 40 && kernel <= 42) {  // fused motion QKV-attention v2: positions per wave automatic (42) / 1 / 2
+    g_mq_pw = kernel == 42 ? 0 : kernel - 39;
     return VD_OK;
   }
   if (kernel == 33 || kernel == 34) {  // fused motion QKV-attention at any grid size (33) / from 2 WGs per CU (34)

@@ -285,12 +285,19 @@ struct Mq2Cfg {
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
-template <int D>
+// PW (round 3, second pass): positions per wave.  Every wave reads the whole 16 KiB weight chunk
+// from LDS per chunk (8 waves: 128 KiB per chunk) for 16 MFMAs per position: at PW = 1 that is
+// ~250 B/clk per CU, the LDS read port's limit, so the kernel was LDS-bound.  PW = 2 gives each
+// weight fragment two positions' MFMAs (half the LDS bytes per MFMA, half the weight stream per
+// token) for 40 more VGPRs of token fragments and 32 of accumulators; the heads' attention runs
+// position by position through the same per-wave scratch.
+template <int D, int PW = 1>
 __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw, bf16_t* __restrict__ o,
     int64_t ldo, int64_t batch, int64_t positions, float c) {
   using Cf = MqCfg<D>;
   using C2 = Mq2Cfg<D>;
+  constexpr int PWG = Cf::P * PW;  // positions per workgroup
   extern __shared__ __attribute__((aligned(1024))) char lds2[];
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds2;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -301,11 +308,10 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
   bf16_t* k_s = s_l + MF * Cf::DPAD;                     // [16][DPAD]
   bf16_t* v_s = s_l + 2 * MF * Cf::DPAD;                 // V image [16][VS]
 
-  const int64_t nblk_p = (positions + Cf::P - 1) / Cf::P;
+  const int64_t nblk_p = (positions + PWG - 1) / PWG;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t b = lid / nblk_p;
-  const int64_t p0 = (lid - b * nblk_p) * Cf::P;
-  const bool pok = p0 + wave < positions;
+  const int64_t p0 = (lid - b * nblk_p) * PWG;  // this wave's positions: p0 + PW * wave + pw
 
   // ---- weight-chunk DMA: chunk t = (head h, k-chunk kc) -> slot t % S; wave w moves pieces 2w,
   // 2w + 1 = ring rows 8g .. 8g + 7; ring row n < 3D is W row (n / D) * C + h * D + n % D
@@ -334,21 +340,24 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane < MF) v_s[lane * Cf::VS + D] = (bf16_t)0x3F80;
 
-  // ---- this wave's A fragments: token (frame fr, position p0 + wave), k = 32 kk + 8 fq .. +7
-  bf16x8 xf[Cf::C / 32];
-  {
-    int64_t p = p0 + wave;
+  // ---- this wave's A fragments: token (frame fr, position p0 + PW wave + pw), k = 32 kk + 8 fq .. +7
+  bf16x8 xf[PW][Cf::C / 32];
+#pragma unroll
+  for (int pw = 0; pw < PW; ++pw) {
+    int64_t p = p0 + PW * wave + pw;
     p = p < positions ? p : positions - 1;
     const bf16_t* xr = x + ((b * MF + fr) * positions + p) * ldx + 8 * fq;
 #pragma unroll
-    for (int kk = 0; kk < Cf::C / 32; ++kk) xf[kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(xr + 32 * kk));
+    for (int kk = 0; kk < Cf::C / 32; ++kk) xf[pw][kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(xr + 32 * kk));
   }
 
   const bool unitc = c == 1.0f;
   const int vtr = (4 * fq + (fr >> 2)) * Cf::VS + 4 * (fr & 3);  // tr-read lane offset (temporal_mfma_kernel)
-  f32x4 acc[Cf::NBLK];
+  f32x4 acc[PW][Cf::NBLK];
 #pragma unroll
-  for (int a = 0; a < Cf::NBLK; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int pw = 0; pw < PW; ++pw)
+#pragma unroll
+    for (int a = 0; a < Cf::NBLK; ++a) acc[pw][a] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int h = 0; h < 8; ++h) {
 #pragma unroll
    for (int kc = 0; kc < Cf::NCH; ++kc) {  // unrolled: the A fragment index 2 kc + ks is static
@@ -365,21 +374,39 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
     asm volatile("" ::: "memory");
     if (t + MQ2_S - 1 < T) issue(t + MQ2_S - 1);
     const bf16_t* ws = (const bf16_t*)(lds2 + (t % MQ2_S) * C2::W_BYTES);
-    // all 16 weight fragments of the chunk read ahead of its 16 MFMAs (counted lgkmcnt waits)
-    bf16x8 wf[2][Cf::NBLK];
+    if constexpr (PW == 1) {
+      // all 16 weight fragments of the chunk read ahead of its 16 MFMAs (counted lgkmcnt waits)
+      bf16x8 wf[2][Cf::NBLK];
 #pragma unroll
-    for (int ks = 0; ks < Cf::KC / 32; ++ks)
+      for (int ks = 0; ks < Cf::KC / 32; ++ks)
 #pragma unroll
-      for (int a = 0; a < Cf::NBLK; ++a) wf[ks][a] = *(const bf16x8*)(ws + sw64(a * 16 + fr, ks * 4 + fq));
-    __builtin_amdgcn_sched_barrier(0);
+        for (int a = 0; a < Cf::NBLK; ++a) wf[ks][a] = *(const bf16x8*)(ws + sw64(a * 16 + fr, ks * 4 + fq));
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int ks = 0; ks < Cf::KC / 32; ++ks)
+      for (int ks = 0; ks < Cf::KC / 32; ++ks)
 #pragma unroll
-      for (int a = 0; a < Cf::NBLK; ++a)
-        acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][a], xf[2 * kc + ks], acc[a], 0, 0, 0);
+        for (int a = 0; a < Cf::NBLK; ++a)
+          acc[0][a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][a], xf[0][2 * kc + ks], acc[0][a], 0, 0, 0);
+    } else {
+      // one k-step's 8 fragments at a time (32 VGPRs: the second position's tokens and
+      // accumulators take the rest), each feeding PW MFMAs
+#pragma unroll
+      for (int ks = 0; ks < Cf::KC / 32; ++ks) {
+        bf16x8 wf[Cf::NBLK];
+#pragma unroll
+        for (int a = 0; a < Cf::NBLK; ++a) wf[a] = *(const bf16x8*)(ws + sw64(a * 16 + fr, ks * 4 + fq));
+#pragma unroll
+        for (int a = 0; a < Cf::NBLK; ++a)
+#pragma unroll
+          for (int pw = 0; pw < PW; ++pw)
+            acc[pw][a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[pw][2 * kc + ks], acc[pw][a], 0, 0, 0);
+      }
+    }
    }
-    {  // ---- head h done: attention of (position p0 + wave, head h)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous head's scratch reads
+#pragma unroll
+    for (int pw = 0; pw < PW; ++pw) {  // ---- head h done: attention of (position p0 + PW wave + pw, head h)
+      const bool pok = p0 + PW * wave + pw < positions;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous head's / position's scratch reads
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int a = 0; a < Cf::NBLK; ++a) {
@@ -387,9 +414,9 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
         if (ch < 3 * D) {
           const int part = ch / D, cd = ch - part * D;
           bf16_t* dst = part == 0 ? q_s + fr * Cf::DPAD + cd : (part == 1 ? k_s + fr * Cf::DPAD + cd : v_s + fr * Cf::VS + cd);
-          *(uint2*)dst = make_uint2(pack2(acc[a][0], acc[a][1]), pack2(acc[a][2], acc[a][3]));
+          *(uint2*)dst = make_uint2(pack2(acc[pw][a][0], acc[pw][a][1]), pack2(acc[pw][a][2], acc[pw][a][3]));
         }
-        acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc[pw][a] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
@@ -425,7 +452,7 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
       const float l = __shfl(ot[D / 16][(D % 16) % 4], ((D % 16) / 4) * 16 + fr, 64);
       const float inv = __builtin_amdgcn_rcpf(l);
       if (pok) {
-        bf16_t* orow = o + ((b * MF + fr) * positions + p0 + wave) * ldo + (int64_t)h * D;
+        bf16_t* orow = o + ((b * MF + fr) * positions + p0 + PW * wave + pw) * ldo + (int64_t)h * D;
 #pragma unroll
         for (int a = 0; a < Cf::DB; ++a) {
           const int dd = 16 * a + 4 * fq;
@@ -444,6 +471,7 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 int g_mq_any = 0;  // 1: take the fused kernel at any grid size (A/B hook, vd_attention_select(33 / 34))
 int g_mq_ver = 2;  // 1: round 2's kernel (LDS token tile, register-staged weight chunks); vd_attention_select(31 / 32)
+int g_mq_pw = 0;   // v2 positions per wave: 0 automatic (2 when that fills the chip), 1 / 2 forced (vd_attention_select 40 / 41)
 
 extern "C" int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* wqkv, int64_t ldw, void* o,
                                        int64_t ldo, int64_t batch, int32_t frames, int64_t positions,
@@ -467,12 +495,22 @@ extern "C" int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* w
     using C2 = Mq2Cfg<40>;
     static bool attr2_set = false;
     if (!attr2_set) {
-      if (hipFuncSetAttribute((const void*)motion_qkv_attn2_kernel<40>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      if (hipFuncSetAttribute((const void*)motion_qkv_attn2_kernel<40, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              C2::LDS_BYTES) != hipSuccess ||
+          hipFuncSetAttribute((const void*)motion_qkv_attn2_kernel<40, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               C2::LDS_BYTES) != hipSuccess)
         return vd_launch_status();
       attr2_set = true;
     }
-    hipLaunchKernelGGL(motion_qkv_attn2_kernel<40>, dim3((unsigned)nwg), dim3(Cf::NT), C2::LDS_BYTES,
+    // two positions per wave where that still gives one round of the chip (g_mq_pw: A/B hook)
+    const int64_t nwg2 = batch * ((positions + 2 * Cf::P - 1) / (2 * Cf::P));
+    if (g_mq_pw != 1 && (nwg2 >= (int64_t)cus || g_mq_pw == 2)) {
+      hipLaunchKernelGGL((motion_qkv_attn2_kernel<40, 2>), dim3((unsigned)nwg2), dim3(Cf::NT), C2::LDS_BYTES,
+                         (hipStream_t)stream, (const bf16_t*)x, ldx, (const bf16_t*)wqkv, ldw, (bf16_t*)o, ldo, batch,
+                         positions, scale * 1.4426950408889634f);
+      return vd_launch_status();
+    }
+    hipLaunchKernelGGL((motion_qkv_attn2_kernel<40, 1>), dim3((unsigned)nwg), dim3(Cf::NT), C2::LDS_BYTES,
                        (hipStream_t)stream, (const bf16_t*)x, ldx, (const bf16_t*)wqkv, ldw, (bf16_t*)o, ldo, batch,
                        positions, scale * 1.4426950408889634f);
     return vd_launch_status();
