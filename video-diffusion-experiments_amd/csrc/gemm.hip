@@ -552,15 +552,12 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
   int poh[C::NA], pow_[C::NA], pimg[C::NA], pfr[C::NA];
   int c_tap = 0, c_ci = 0;
   bool c_new = true;
+  // (an early-out for split == 1 here measured 15 % slower on the dense v2 GEMMs, same box,
+  // profiles/r03t_unit_kr_bisect.txt: it changes how hipcc lays out the persistent unit loop)
   auto unit_kr = [&](int u, int& kt0, int& kt1) {
-    if (split == 1) {  // (the unsplit common case: no division)
-      kt0 = 0;
-      kt1 = nk_all;
-      return;
-    }
     const int sp = u % split;
-    kt0 = nk_all * sp / split;  // nk_all * split < 2^31
-    kt1 = nk_all * (sp + 1) / split;
+    kt0 = (int)((int64_t)nk_all * sp / split);
+    kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
   };
   auto setup_unit = [&](int u) {  // per-unit row offsets for the issue cursor
     const int tile = u / split;
@@ -1424,15 +1421,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
   int pimg[C::NAMAX], pohw[C::NAMAX];
   int c_tap = 0, c_ci = 0;
   bool c_new = true;
+  // (an early-out for split == 1 here measured 15 % slower on the dense v2 GEMMs, same box,
+  // profiles/r03t_unit_kr_bisect.txt: it changes how hipcc lays out the persistent unit loop)
   auto unit_kr = [&](int u, int& kt0, int& kt1) {
-    if (split == 1) {  // (the unsplit common case: no division)
-      kt0 = 0;
-      kt1 = nk_all;
-      return;
-    }
     const int sp = u % split;
-    kt0 = nk_all * sp / split;  // nk_all * split < 2^31
-    kt1 = nk_all * (sp + 1) / split;
+    kt0 = (int)((int64_t)nk_all * sp / split);
+    kt1 = (int)((int64_t)nk_all * (sp + 1) / split);
   };
   auto setup_unit = [&](int u) {
     const int tile = u / split;
