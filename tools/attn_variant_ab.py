@@ -1,6 +1,6 @@
 """A/B of flash40 schedule variants in one process (interleaved rounds), L1 shape (S 4096,
 8 heads, 32 images, d 40), the model's inputs (softmax scale * log2 e folded into q):
-    python tools/attn_variant_ab.py [rounds] [--pairs=25:26] [--imgs=32]
+    python tools/attn_variant_ab.py [rounds] [--pairs=25:26] [--imgs=32] [--S=4096] [--d=40]
 each pair "a:b" = vd_attention_select(a) vs vd_attention_select(b) on top of the automatic d = 40
 choice (flash40); results must be bitwise equal (the variants only move work between phases).
 """
@@ -19,7 +19,9 @@ rounds = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 7
 pairs = next((a.split("=")[1] for a in sys.argv if a.startswith("--pairs=")), "25:26")
 sels = sorted({int(x) for p in pairs.split(",") for x in p.split(":")})
 n_img = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--imgs=")), "32"))
-S, heads, d = 4096, 8, 40
+S = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--S=")), "4096"))
+d = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--d=")), "40"))
+heads = 8
 C = heads * d
 g = torch.Generator(device="cuda").manual_seed(7)
 qkv = (torch.randn(n_img * S, 3 * C, device="cuda", generator=g) * 1.5)
