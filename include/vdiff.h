@@ -223,9 +223,7 @@ int vd_attention_force_v1(int32_t on);
  * 36-39 = round 3's LDS-DMA-ring kernel with lazy offset + MFMA row sum / eager offset + MFMA
  * row sum / lazy offset + fp32 row sum (the default, 38) / eager + fp32 row sum; 40 / 41 / 42 =
  * the round-3 motion kernel with one / two positions per wave / two where that still fills the
- * chip (the default); 43 / 44 = the d >= 160 self-attention at S <= 256 with 64-query
- * workgroups where the 128-query grid has fewer workgroups than CUs (the default) / never (A/B
- * hooks; the d = 40 choice is left as it was). */
+ * chip (the default) (A/B hooks; the d = 40 choice is left as it was). */
 int vd_attention_select(int32_t kernel);
 /* Diagnostic hook: copy the barrier stamps (s_memtime, 8 waves x 512, wave-major) that the last
  * flash40 launch made under vd_attention_select(9) to dst (device memory, n <= 4096 uint64). */

@@ -32,7 +32,6 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int KT = 64;   // keys per tile
-int g_fa_qb1 = 1;        // d >= 160, S <= 256, small grids: 64-query workgroups (0: never; vd_attention_select 43 / 44)
 int g_f4_g1 = 0;         // flash40 LDS-DMA issuer placement (A/B, vd_attention_select 25-30; 26 = 0 the default)
 int g_flash32 = 1;       // d = 40: 1 = automatic (flash40 for >= 4 key tiles, else flash32), 7 = flash32 only,
                          // 6 = flash40 wherever it applies, 8 = flash40 stamped (diagnostic),
@@ -1893,15 +1892,6 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
     hipLaunchKernelGGL((flash_attn_kernel<D, 4>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                        (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv,
                        kv_div, c, out_f32);
-  } else if (D >= 160 && sq <= 256 && g_fa_qb1 && ((sq + 127) / 128) * heads * batch < 256) {
-    // d 160 at S <= 256 on a grid of fewer 128-query workgroups than CUs (a 2-4-frame rank's
-    // level 3): 64 queries per workgroup, twice the workgroups (4 images at S 256: 14.4 -> 10.8
-    // us); on a full grid the 128-query form stays faster (32 images: 36.1 vs 48.9 us;
-    // profiles/r03v_attn_qb.txt; vd_attention_select 43 / 44 A/B)
-    const dim3 grid((unsigned)((sq + 63) / 64), (unsigned)heads, (unsigned)batch);
-    hipLaunchKernelGGL((flash_attn_kernel<D, 1>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                       (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv,
-                       kv_div, c, out_f32);
   } else {
     const dim3 grid((unsigned)((sq + 127) / 128), (unsigned)heads, (unsigned)batch);
     hipLaunchKernelGGL((flash_attn_kernel<D, 2>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
@@ -2384,10 +2374,6 @@ extern int g_fp8_ver;  // attention_fp8.hip
 extern "C" int vd_attention_select(int32_t kernel) {
   if (kernel >= 35 && kernel <= 39) {  // fp8 attention: round 1's kernel (35) / round 3's (36; 37-39 its A/B forms)
     g_fp8_ver = kernel - 34;
-    return VD_OK;
-  }
-  if (kernel == 43 || kernel == 44) {  // d >= 160 self-attention at S <= 256: 64-query (43) / 128-query (44) workgroups
-    g_fa_qb1 = kernel == 43;
     return VD_OK;
   }
   if (kernel >= 40 && kernel <= 42) {  // fused motion QKV-attention v2: positions per wave automatic (42) / 1 / 2
