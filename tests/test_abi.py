@@ -129,3 +129,18 @@ def test_loader_refuses_a_library_built_from_other_sources(monkeypatch):
     monkeypatch.setattr(sh, "source_hash", lambda flags=(): "0000000000000000")
     with pytest.raises(L.VdiffError, match="built from other sources"):
         L._check_build_hash(h)
+
+
+def test_loader_refuses_a_library_built_for_another_arch(monkeypatch):
+    """the content hash is arch-free, so the arch is checked on its own — a VDIFF_ARCH
+    that differs from the library's vd_build_arch() raises at load, and build() rebuilds when the
+    arch in its stamp changes."""
+    import build_ext
+    h = L.lib()
+    monkeypatch.setenv("VDIFF_ARCH", "gfx942")
+    with pytest.raises(L.VdiffError, match="built for gfx950"):
+        L._check_build_hash(h)
+    monkeypatch.setenv("VDIFF_ARCH", "gfx950")
+    L._check_build_hash(h)
+    if (build_ext.BUILD / "src.hash").exists():  # the build directory is not shipped to GPU boxes
+        assert (build_ext.BUILD / "src.hash").read_text().split()[1] == build_ext.ARCH

@@ -88,3 +88,24 @@ def test_prepare_latents_follows_randn_tensor_cpu_fp16():
     x = pipe.prepare_latents(1, 16, 64, 64, generator=torch.manual_seed(42))
     want = torch.randn((1, 4, 16, 64, 64), generator=torch.manual_seed(42), dtype=torch.float16)
     assert x.dtype == torch.float32 and torch.equal(x, want.float())
+
+
+def test_randn_tensor_generator_devices():
+    """diffusers randn_tensor semantics (AnimateDiffPipeline.prepare_latents): draw on the
+    generator's device, a list of generators draws one batch row each, and a CUDA generator
+    cannot feed a CPU target."""
+    import torch
+    from vdiff.utils import randn_tensor
+    x = randn_tensor((2, 4, 3, 8, 8), generator=torch.Generator().manual_seed(7), device="cpu",
+                     dtype=torch.float16)
+    assert torch.equal(x, torch.randn((2, 4, 3, 8, 8), generator=torch.Generator().manual_seed(7),
+                                      dtype=torch.float16))
+    gens = [torch.Generator().manual_seed(s) for s in (1, 2)]
+    y = randn_tensor((2, 4, 3, 8, 8), generator=gens, device="cpu", dtype=torch.float32)
+    assert torch.equal(y[1:], torch.randn((1, 4, 3, 8, 8), generator=torch.Generator().manual_seed(2)))
+
+    class FakeCudaGen:  # a CUDA generator object needs a GPU; only its .device is read first
+        device = torch.device("cuda")
+    import pytest
+    with pytest.raises(ValueError, match="Cannot generate"):
+        randn_tensor((1, 4), generator=FakeCudaGen(), device="cpu")

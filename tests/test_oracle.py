@@ -208,3 +208,20 @@ def test_bf16_realisation_floor():
     floor, fp32 = rel(d1, d0), rel(f1, f0)
     print(f"bf16 realisation floor {floor:.4f}; fp32 sensitivity {fp32:.2e}")
     assert 0.005 < floor < 0.03 and fp32 < 1e-4
+
+
+def test_euler_sigma_table_within_one_ulp_of_diffusers_pow_form():
+    """ADVICE r3: the product tables take correctly rounded square roots (host-independent);
+    diffusers computes ((1 - a) / a) ** 0.5 in torch fp32 on the host, which some hosts round
+    one ulp off.  Bound the divergence from that form at 1 ulp on every training sigma."""
+    import numpy as np
+    import torch
+    from vdiff.sched.euler import EulerDiscreteScheduler
+    s = EulerDiscreteScheduler(beta_schedule="linear")
+    ac = s.alphas_cumprod
+    pow_form = (((1 - ac) / ac) ** 0.5).numpy().astype(np.float32)
+    ours = s._sigmas_train.astype(np.float32)
+    ulp = np.abs(ours.view(np.int32).astype(np.int64) - pow_form.view(np.int32).astype(np.int64))
+    assert ulp.max() <= 1
+    q32 = ((1 - ac) / ac).double().numpy()
+    assert np.array_equal(ours, np.sqrt(q32).astype(np.float32))  # correctly rounded sqrt of the fp32 quotient

@@ -135,3 +135,46 @@ def test_load_diffusers_state_dict_into_existing_model(checkpoint):
     _bit_identical(m, unet.to(torch.bfloat16))
     with pytest.raises(KeyError, match="mismatch"):
         vdiff.load_diffusers_state_dict(m, root / "adapter" / "diffusion_pytorch_model.safetensors")
+
+
+@pytest.mark.gpu
+def test_baseline_generation_caller_sequence(checkpoint, tmp_path):
+    """experiments/01_baseline_generation.py:55-123 unchanged except for the hub names: MotionAdapter /
+    AnimateDiffPipeline.from_pretrained with torch_dtype=float16, the Euler swap
+    (timestep_spacing="linspace", beta_schedule="linear"), pipe.to("cuda"), enable_vae_slicing(), then
+    pipe(prompt=, negative_prompt=, generator=torch.Generator("cuda").manual_seed(42), **DEFAULT_CONFIG)
+    -> .frames[0] = 16 PIL frames saved as GIF + PNGs.  The initial noise is drawn on the CUDA
+    generator in float16, as diffusers' randn_tensor does (01:103)."""
+    from vdiff import EulerDiscreteScheduler
+    from vdiff.utils import export_to_gif
+    root, _, _ = checkpoint
+    adapter = MotionAdapter.from_pretrained(root / "adapter", torch_dtype=torch.float16)
+    pipe = AnimateDiffPipeline.from_pretrained(root / "sd", motion_adapter=adapter, torch_dtype=torch.float16)
+    pipe.scheduler = EulerDiscreteScheduler.from_config(pipe.scheduler.config, timestep_spacing="linspace",
+                                                        beta_schedule="linear")
+    pipe.to("cuda")
+    pipe.enable_vae_slicing()
+    # the draw: exactly torch.randn on the CUDA generator, float16, scaled by init_noise_sigma
+    pipe.scheduler.set_timesteps(25)
+    x = pipe.prepare_latents(1, 16, 64, 64, generator=torch.Generator("cuda").manual_seed(42))
+    want = torch.randn((1, 4, 16, 64, 64), generator=torch.Generator("cuda").manual_seed(42), device="cuda",
+                       dtype=torch.float16)
+    assert x.is_cuda and torch.equal(x, want.float() * pipe.scheduler.init_noise_sigma)
+    config = {"num_frames": 16, "num_inference_steps": 25, "guidance_scale": 7.5, "width": 512, "height": 512}
+    out = pipe(prompt="a corgi walking on the beach, sunset lighting, high quality",
+               negative_prompt="bad quality, blurry, distorted, ugly, deformed",
+               generator=torch.Generator("cuda").manual_seed(42), **config)
+    frames = out.frames[0]
+    assert len(frames) == 16 and frames[0].mode == "RGB"
+    export_to_gif(frames, str(tmp_path / "corgi_beach.gif"))
+    for i, frame in enumerate(frames):
+        frame.save(tmp_path / f"frame_{i:03d}.png")
+    assert (tmp_path / "corgi_beach.gif").stat().st_size > 0 and (tmp_path / "frame_015.png").exists()
+    # same seed, same generator device -> the same video
+    again = pipe(prompt="a corgi walking on the beach, sunset lighting, high quality",
+                 negative_prompt="bad quality, blurry, distorted, ugly, deformed",
+                 generator=torch.Generator("cuda").manual_seed(42), output_type="latent", **config).frames
+    first = pipe(prompt="a corgi walking on the beach, sunset lighting, high quality",
+                 negative_prompt="bad quality, blurry, distorted, ugly, deformed",
+                 generator=torch.Generator("cuda").manual_seed(42), output_type="latent", **config).frames
+    assert torch.equal(again, first) and torch.isfinite(first).all()

@@ -53,7 +53,10 @@ def _compile(src: Path, defs, verbose: bool) -> Path:
 def build(verbose: bool = True, jobs: int = 8, clean: bool = False) -> Path:
     h = source_hash(HASH_FLAGS)
     stamp = BUILD / "src.hash"
-    if not clean and LIB.exists() and stamp.exists() and stamp.read_text().strip() == h:
+    # the stamp carries the arch too: a VDIFF_ARCH change rebuilds even though the content
+    # hash (arch-free, see HASH_FLAGS) is unchanged
+    want = f"{h} {ARCH}"
+    if not clean and LIB.exists() and stamp.exists() and stamp.read_text().strip() == want:
         if verbose:
             print(f"[vdiff build] {LIB.name} is current (source hash {h})", flush=True)
         return LIB
@@ -70,7 +73,7 @@ def build(verbose: bool = True, jobs: int = 8, clean: bool = False) -> Path:
         print("[vdiff build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
-    stamp.write_text(h + "\n")
+    stamp.write_text(want + "\n")
     return LIB
 
 

@@ -137,6 +137,20 @@ def _check_build_hash(h) -> None:
     if got != want:
         raise VdiffError(f"{LIB_PATH.name} was built from other sources (hash {got}, tree {want}): "
                          "rebuild with python video-diffusion-experiments_amd/build_ext.py")
+    _check_build_arch(h.vd_build_arch().decode())
+
+
+def _check_build_arch(built: str) -> None:
+    """The code objects must be for the requested arch (VDIFF_ARCH, when set) and for the GPU
+    this process sees: a library built for another arch would otherwise load and only fail at
+    the first kernel launch ("no binary for the GPU")."""
+    req = os.environ.get("VDIFF_ARCH")
+    if req and req != built:
+        raise VdiffError(f"{LIB_PATH.name} was built for {built}, VDIFF_ARCH={req}: rebuild")
+    if torch.cuda.device_count() > 0 and torch.cuda.is_available():
+        dev = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.split(":")[0]
+        if dev and dev != built:
+            raise VdiffError(f"{LIB_PATH.name} was built for {built}, the GPU is {dev}: rebuild with VDIFF_ARCH={dev}")
 
 
 def check(rc: int, what: str = "") -> None:

@@ -27,10 +27,11 @@ list of PIL images, which 05_grid_search_ablation.py:169-182 saves as PNG / GIF)
 "pt" / "np" (diffusers' postprocessed video, (B, F, 3, H, W) tensor / (B, F, H, W, 3)
 array in [0, 1]) or "latent" (the final latents).
 
-prepare_latents follows diffusers' randn_tensor for the reference's CPU generator
-(05:156 `torch.manual_seed(seed)`): x_T = torch.randn(shape, generator, dtype) drawn on
-the CPU in the pipeline's torch_dtype — float16 in the reference (05:35, 05:130-134) —
-then moved to the GPU (kept in fp32 from there on).
+prepare_latents follows diffusers' randn_tensor: x_T = torch.randn(shape, generator, dtype)
+drawn on the generator's device — the CPU for 05:156's `torch.manual_seed(seed)`, the GPU
+for 01:103's `torch.Generator("cuda").manual_seed(seed)` — in the pipeline's torch_dtype
+(float16 in the reference, 05:35, 05:130-134), then moved to the GPU (kept in fp32 from
+there on).
 """
 from __future__ import annotations
 
@@ -170,6 +171,31 @@ class DenoiseLoop:
         return self.lat
 
 
+def randn_tensor(shape, generator=None, device=None, dtype=None):
+    """diffusers.utils.torch_utils.randn_tensor: N(0, 1) drawn on the generator's device (the
+    target device when there is no generator), in `dtype`, then moved to `device`.  A list of
+    generators draws one batch row each.  A CUDA generator for a CPU target is refused."""
+    device = torch.device(device or "cpu")
+    gens = generator if isinstance(generator, (list, tuple)) else None
+    if gens is not None and len(gens) == 1:
+        generator, gens = gens[0], None
+    rand_device = device
+    if generator is not None:
+        gtype = (gens[0] if gens is not None else generator).device.type
+        if gtype != device.type:
+            if gtype != "cpu":
+                raise ValueError(f"Cannot generate a {device} tensor from a generator of type {gtype}.")
+            rand_device = torch.device("cpu")
+    if gens is not None:
+        if len(gens) != shape[0]:
+            raise ValueError(f"{len(gens)} generators for a batch of {shape[0]}")
+        one = (1,) + tuple(shape[1:])
+        x = torch.cat([torch.randn(one, generator=gen, device=rand_device, dtype=dtype) for gen in gens])
+    else:
+        x = torch.randn(shape, generator=generator, device=rand_device, dtype=dtype)
+    return x.to(device)
+
+
 def numpy_to_pil(images):
     """diffusers' numpy_to_pil: (F, H, W, 3) floats in [0, 1] -> list of RGB PIL images."""
     from PIL import Image
@@ -278,10 +304,14 @@ class AnimateDiffPipeline:
         return [numpy_to_pil(a) for a in arr]
 
     def prepare_latents(self, batch, num_frames, h, w, generator=None, latents=None):
-        """diffusers AnimateDiffPipeline.prepare_latents -> fp32 on the GPU, x init_noise_sigma."""
+        """diffusers AnimateDiffPipeline.prepare_latents -> fp32 on the GPU, x init_noise_sigma.
+        The draw follows randn_tensor: on the generator's device (a CPU generator from 05:156's
+        torch.manual_seed, a CUDA one from 01:103's torch.Generator("cuda")), in the pipeline's
+        torch_dtype (float16 in the reference, 01:21 / 05:35), then moved."""
         if latents is None:
             shape = (batch, self.unet.config["in_channels"], num_frames, h, w)
-            latents = torch.randn(shape, generator=generator, dtype=self.latent_draw_dtype)
+            dtype = getattr(self, "torch_dtype", None) or self.latent_draw_dtype
+            latents = randn_tensor(shape, generator=generator, device=self.unet.device, dtype=dtype)
         return latents.to(self.unet.device, torch.float32) * self.scheduler.init_noise_sigma
 
     @torch.no_grad()
