@@ -41,7 +41,7 @@ enum vd_status {
 };
 
 const char* vd_strerror(int code);
-int vd_version(void);  /* 3 */
+int vd_version(void);  /* 4 */
 /* Content hash (16 hex digits) of the sources and compile flags the library was built from
  * (video-diffusion-experiments_amd/build_ext.py); the Python loader compares it with the tree. */
 const char* vd_build_hash(void);
@@ -106,6 +106,17 @@ typedef struct vd_gemm_desc {
   const float* ln_gamma; const float* ln_beta; float ln_eps;
   const float* ln_pe; int64_t ln_pe_div; int64_t ln_pe_period;
   void* ln_out; int64_t ld_ln;
+  /* Per-call plan controls (the library keeps no mutable selector state; zero = the product
+   * plan).  path: 0 = automatic; 1 = v1 (register-staged, any shape), 2 = v2 (256 x {128,160}
+   * persistent LDS-DMA), 3 = v3 (256 x 256 ping-pong, dense A), 5 = v5 (256 x 320, BK 32),
+   * 6 = v6 (64 x 64, split K toward 2 workgroups per CU) — forced wherever that kernel takes
+   * the shape, else the automatic choice; every path computes the same arithmetic for an
+   * unsplit K (the K order of each output is fixed), the parity tests run each one.
+   * plan_m > 0: choose kernel, split-K and LayerNorm fusion as if M were plan_m, launch over
+   * all M rows — an unsharded run planned with a frame shard's M reproduces the shard's
+   * summation order bit for bit (tests/test_gpu_dist2.py). */
+  int32_t path;
+  int64_t plan_m;
 } vd_gemm_desc;
 
 int vd_gemm(const vd_gemm_desc* d, vd_stream_t stream);
@@ -113,25 +124,6 @@ int vd_gemm(const vd_gemm_desc* d, vd_stream_t stream);
  * few output tiles to fill 256 CUs are split along K into fp32 slabs that a
  * second kernel reduces (deterministic, no atomics) while applying the epilogue. */
 int64_t vd_gemm_ws_bytes(const vd_gemm_desc* d);
-/* Test/benchmark hook: on != 0 forces the register-staged v1 GEMM path for every
- * shape (default: the LDS-DMA v2 path wherever it applies). */
-int vd_gemm_force_v1(int32_t on);
-/* Test/benchmark hook: 0 = automatic (default), 1 = v1 (register-staged, any shape),
- * 2 = v2 (256 x {128,160} persistent LDS-DMA), 3 = v3 (256 x 256 8-phase, dense A only;
- * shapes it cannot take fall back to the automatic choice), 5 = v5 (256 x 320, BK 32,
- * 4-stage ring, load-free epilogue), 6 = v6 (64 x 64, in-kernel split-K reduction), 7 = the
- * automatic choice without v6, 8 = v6 unsplit, 9 = automatic with split-K cap 8, 10 = v3 one
- * unit per workgroup, 11 = automatic with that v3; A/B hooks of round-2 kernel changes, each the
- * automatic plan with one change undone: 12 = v2 / v6 fragment reads in round 1's order,
- * 13 / 14 = v2 fragment reads pipelined (the default) / all ahead, 15 = v3 with gemm_epilogue
- * instead of the LDS-bias epilogue, 16 = v5 W fragments in halves instead of the rolling window;
- * round 3: 17 / 18 / 19 = the automatic plan with v2's 256 x 160 tiles in the 32x32x16 MFMA form
- * (8 waves of 32 rows) for every conv / for convs and dense GEMMs (not GEGLU) / for convs with
- * K <= 2880 at M >= 65536 (the automatic plan itself never takes it: measured slower); 20 = v2's
- * conv rows set up with round 2's int64 divisions instead of 32-bit shifts.
- * Every path computes the same arithmetic (the K order of each output is fixed). */
-int vd_gemm_select_path(int32_t path);
-
 /* ---------------------------------------------------------------- GroupNorm
  * torch GroupNorm over NHWC rows, for ResnetBlock2D.norm1/2 (eps 1e-5, +SiLU),
  * Transformer2DModel.norm (eps 1e-6) and the motion-module norm whose
@@ -177,9 +169,6 @@ int vd_gn_apply_g(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int6
 int vd_layernorm(const void* x, int64_t ldx, int64_t rows, int64_t C, const float* gamma,
                  const float* beta, float eps, const float* pe, int64_t pe_div,
                  int64_t pe_period, void* y, int64_t ldy, vd_stream_t stream);
-/* Test/benchmark hook: multi_row = 0 forces the one-row-per-wave LayerNorm kernel (default 1:
- * several rows per wave for C in {320, 640, 1280}). */
-int vd_layernorm_select(int32_t multi_row);
 
 /* ---------------------------------------------------------------- attention
  * softmax(q k^T * scale) v per (batch b, head h): replaces
@@ -201,33 +190,16 @@ int vd_attention(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
 int vd_attention_f32(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                      int64_t ldv, float* o, int64_t ldo, int64_t batch, int32_t heads,
                      int64_t sq, int64_t skv, int32_t d, int64_t kv_div, float scale, vd_stream_t stream);
-/* Test/benchmark hook: on != 0 routes d = 40 to the 16x16x32 flash kernel instead of
- * the 32x32x16 one (default). */
-int vd_attention_force_v1(int32_t on);
-/* Test/benchmark hook: the d = 40 kernel — 0 = automatic (flash40 from 4 key tiles, flash32
- * below), 1 = the 16x16x32 flash kernel, 2 = flash32 (4 waves, 32x32x16), 3 = flash32pp (8
- * waves: two staggered groups software-pipelined PV(t-1)+QK(t) | softmax(t); bitwise equal to
- * flash32, measured slower — tools/attn_ab.py), 4 = flash32 with the intra-wave interleaved
- * steady state, 5 = flash32 at one workgroup per CU (occupancy probe), 6 = flash32 with one
- * 32-query block per wave, 7 = flash40 (round 3: two-group ping-pong over an LDS-DMA ring,
- * bit-identical to flash32) wherever it applies (>= 2 key tiles), 8 = flash32 only, 9 = flash40's
- * stamped diagnostic build; 20 / 21 = the d = 512 kernel (flash512, the VAE mid-block
- * attention) with K two tiles ahead in a 3-slot LDS ring and V one ahead / K and V one tile
- * ahead (the default), 22 = DMA ablation (tile 0 only: WRONG results, timing only); 25 / 26 /
- * 27 = flash40's K/V LDS-DMA issued by waves 4-7 only, in their softmax phase / by waves 0-5
- * (the default) / by waves 0-3 only, in their MFMA phase, 28 = by all eight waves, 29 = as 26
- * with waves 4-5 issuing in their MFMA phase, 30 = all eight waves (2, 2, 1, 1 pieces per
- * group) each in its MFMA phase (half the pieces in each barrier interval); 31 / 32 = vd_motion_qkv_attention's
- * round-2 kernel / round-3 kernel (the default); 33 / 34 = the fused motion kernel at any grid
- * size / only from one round of the chip (the default); 35 = vd_attention_fp8's round-1 kernel,
- * 36-39 = round 3's LDS-DMA-ring kernel with lazy offset + MFMA row sum / eager offset + MFMA
- * row sum / lazy offset + fp32 row sum (the default, 38) / eager + fp32 row sum; 40 / 41 / 42 =
- * the round-3 motion kernel with one / two positions per wave / two where that still fills the
- * chip (the default) (A/B hooks; the d = 40 choice is left as it was). */
-int vd_attention_select(int32_t kernel);
-/* Diagnostic hook: copy the barrier stamps (s_memtime, 8 waves x 512, wave-major) that the last
- * flash40 launch made under vd_attention_select(9) to dst (device memory, n <= 4096 uint64). */
-int vd_attention_stamps(void* dst, int64_t n, vd_stream_t stream);
+/* vd_attention / vd_attention_f32 with an explicit kernel choice per call (the library keeps no
+ * selector state): kernel 0 = the automatic choice (what vd_attention runs: d = 40 -> flash40
+ * from 4 key tiles, flash32 below; other d -> the 16x16x32 flash kernel), 1 = the 16x16x32 flash
+ * kernel for any d, 2 = flash32 (d = 40), 3 = flash40 wherever it applies (d = 40, >= 2 key
+ * tiles); a kernel that does not take the shape falls through to the next one down.  All of
+ * them compute softmax(q k^T * scale) v; flash40 is bit-identical to flash32 (the parity tests
+ * run each).  out_f32 as vd_attention_f32. */
+int vd_attention_ex(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                    void* o, int64_t ldo, int64_t batch, int32_t heads, int64_t sq, int64_t skv, int32_t d,
+                    int64_t kv_div, float scale, int32_t out_f32, int32_t kernel, vd_stream_t stream);
 
 /* Temporal (motion-module) self-attention over frames (a9): token (b, f, p) is
  * row (b*frames + f)*positions + p of q/k/v/o (the NHWC layout, no permute);
@@ -262,15 +234,17 @@ int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* wqkv, int64_
                             float scale, vd_stream_t stream);
 /* vd_temporal_attention for the DiT's temporal blocks (d = 64, 17..32 frames) with the 1-D
  * temporal RoPE (vd_rope_qk mode 1, angle by frame) applied to q/k inside the kernel as they
- * are loaded; q and k are read un-rotated and left unchanged.  Returns VD_EUNSUPPORTED while
- * vd_temporal_force_valu is on (the fused form exists only on the MFMA kernel). */
+ * are loaded; q and k are read un-rotated and left unchanged. */
 int vd_temporal_attention_rope(const void* q, const void* k, const void* v, int64_t ld, void* o,
                                int64_t ldo, int64_t batch, int32_t frames, int64_t positions,
                                int32_t heads, int32_t d, float scale, float theta,
                                vd_stream_t stream);
-/* Test/benchmark hook: on != 0 forces the VALU temporal kernel (default: the MFMA kernel
- * for frames <= 16 and d in {32, 40, 64, 80, 160}, frames 17..32 and d in {40, 64, 80, 160}). */
-int vd_temporal_force_valu(int32_t on);
+/* vd_temporal_attention on the VALU kernel for every shape (vd_temporal_attention takes the
+ * MFMA kernel for frames <= 16 and d in {32, 40, 64, 80, 160}, frames 17..32 and d in {40, 64, 80,
+ * 160}, and this one otherwise): the same arguments and result; the parity tests run both. */
+int vd_temporal_attention_valu(const void* q, const void* k, const void* v, int64_t ld, void* o,
+                               int64_t ldo, int64_t batch, int32_t frames, int64_t positions,
+                               int32_t heads, int32_t d, float scale, vd_stream_t stream);
 
 /* Row softmax over fp32 scores in log2 units (p = exp2(s - max) / sum, bf16 out): round 2's
  * materialised-score form of the VAE mid-block attention (now vd_attention with d = 512;

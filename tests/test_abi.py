@@ -27,7 +27,7 @@ def test_library_loads_and_exports_every_symbol():
     h = L.lib()
     for name in header_functions():
         assert hasattr(h, name), name
-    assert h.vd_version() == 3
+    assert h.vd_version() == 4
     from vdiff._srchash import source_hash
     import build_ext
     assert h.vd_build_hash().decode() == source_hash(build_ext.HASH_FLAGS)  # a build of THIS tree
@@ -144,3 +144,19 @@ def test_loader_refuses_a_library_built_for_another_arch(monkeypatch):
     L._check_build_hash(h)
     if (build_ext.BUILD / "src.hash").exists():  # the build directory is not shipped to GPU boxes
         assert (build_ext.BUILD / "src.hash").read_text().split()[1] == build_ext.ARCH
+
+
+def test_product_library_has_no_selector_state():
+    """VERDICT r3 #6 / SURVEY §8b "stateless and reentrant": the product library exports no
+    mutable selector — no vd_*select* / *force* entry points, no exported data symbols beyond
+    the HIP runtime's per-module ids — and every variant choice a test needs is a per-call
+    argument (vd_gemm_desc.path / plan_m, vd_attention_ex's kernel, vd_temporal_attention_valu)."""
+    out = subprocess.run(["nm", "-D", "--defined-only", str(L.LIB_PATH)], capture_output=True, text=True).stdout
+    syms = [line.split() for line in out.splitlines() if len(line.split()) == 3]
+    exported_fns = {name for _, kind, name in syms if kind == "T" and name.startswith("vd_")}
+    assert exported_fns == header_functions()
+    assert not any(("select" in n or "force" in n or "stamps" in n) for n in exported_fns)
+    data = [name for _, kind, name in syms if kind in "BDGRSV" and not name.startswith("__hip_cuid_")]
+    assert data == [], data
+    fields = [f for f, _ in L.GemmDesc._fields_]
+    assert fields[-2:] == ["path", "plan_m"]

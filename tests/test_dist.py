@@ -131,7 +131,7 @@ def _worker(rank, world, port, errq):
         want = ref.reshape(B, F, C, HW).permute(0, 1, 3, 2)[:, rank * Fl:(rank + 1) * Fl].reshape(-1, C)
         err = (got - want).abs().max().item()
         assert err < 1e-4, f"sharded motion module max err {err}"
-        # ---- 3. kt = 3 temporal conv under frame sharding: one-frame halo (P2P) + a conv
+        # ---- 3. kt = 3 temporal conv under frame sharding: one-frame halo (all-gather) + a conv
         # over the halo'd frames with no temporal padding == the unsharded 3-D conv's frames
         Cc, Co = 8, 16
         vid = torch.randn(B, Cc, F, H, W)
@@ -178,3 +178,49 @@ def test_frames_must_divide():
 
     with pytest.raises(ValueError):
         Fake().frames_local(16)
+
+
+def _halo_worker(rank, world, port, errq):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        fs = FrameShard()
+        B, F, H, W, Cc, Co = 2, 6, 4, 3, 8, 16
+        Fl, HW = F // world, H * W
+        g = torch.Generator().manual_seed(7)
+        vid = torch.randn(B, Cc, F, H, W, generator=g)
+        wt = torch.randn(Co, Cc, 3, 3, 3, generator=g) * 0.2
+        full = torch.nn.functional.conv3d(vid, wt, padding=1)
+        rows = vid.permute(0, 2, 3, 4, 1)[:, rank * Fl:(rank + 1) * Fl].reshape(-1, Cc).contiguous()
+        halo = fs.halo_frames(rows, B, Fl, HW)
+        hv = halo.reshape(B, Fl + 2, H, W, Cc).permute(0, 4, 1, 2, 3)
+        # the halo frames are exactly the neighbours' boundary frames (zeros at the ends)
+        for side, f in ((0, rank * Fl - 1), (Fl + 1, (rank + 1) * Fl)):
+            want = vid[:, :, f] if 0 <= f < F else torch.zeros_like(vid[:, :, 0])
+            assert torch.equal(hv[:, :, side], want), (rank, side)
+        got = torch.nn.functional.conv3d(hv, wt, padding=(0, 1, 1))
+        err = (got - full[:, :, rank * Fl:(rank + 1) * Fl]).abs().max().item()
+        assert err < 1e-4, f"rank {rank}: halo'd temporal conv max err {err}"
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        errq.put(f"rank {rank}: {e}\n{traceback.format_exc()}")
+        raise
+
+
+def test_halo_frames_world3_gloo():
+    """FrameShard.halo_frames' all-gather form with a middle rank (both neighbours present)
+    and both video ends (zero halo): the halo'd per-rank temporal conv equals the full 3-D conv."""
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_halo_worker, args=(r, 3, port, errq)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]

@@ -96,3 +96,34 @@ def test_dit_sharded_loop_world1_matches_unsharded(pg):
     loop = DiTDenoiseLoop(m, s, lat, ehs, 7.5, use_graph=True, dist=FrameShard()).prime()
     assert loop.graph is not None
     assert torch.equal(loop.run(2), ref)
+
+
+def test_halo_conv3d_world1_rccl_graph(pg):
+    """The kt = 3 temporal conv's frame halo (FrameShard.halo_frames: one RCCL all-gather of the
+    boundary frames, no point-to-point request, no host wait) captured into a hipGraph with the
+    halo'd conv (frames_in = F + 2, t_off = 1) and replayed: at world size 1 the halo is the
+    video's zero padding, so the graph's output equals the unsharded 3-D conv bit for bit."""
+    from vdiff import ops
+    from vdiff.models.layers import pack_conv3d
+    fs = FrameShard()
+    B, F, h, w, ci, co = 2, 4, 16, 16, 64, 64
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = (torch.randn(B * F * h * w, ci, device="cuda", generator=g)).to(torch.bfloat16)
+    wt = (torch.randn(co, ci, 3, 3, 3, device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    wp = pack_conv3d(wt)
+    full, _, _ = ops.conv3d(x, B, F, h, w, wp, kt=3, ks=3)
+    out = torch.empty_like(full)
+
+    def step():
+        halo = fs.halo_frames(x, B, F, h * w)
+        ops.conv3d(halo, B, F + 2, h, w, wp, kt=3, ks=3, frames_out=F, t_off=1, out=out)
+
+    step()  # eager: communicator set-up
+    torch.cuda.synchronize()
+    out.zero_()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, full)

@@ -7,8 +7,12 @@ test closes the gap between them: 2/4/8 processes share cuda:0, each holds 8/wor
 of both CFG halves (one frame per rank at world 8, the driver's 8-GPU layout) and runs the product path (HIP kernels, GroupNorm partials merged across
 ranks, vd_block_transpose re-shards around every motion module) with the collectives staged
 through gloo on the host (RCCL refuses two ranks on one device); the gathered latents must
-match the unsharded single-process loop.  Tolerance: rel-L2 1e-2 over 2 DDIM steps (the
-cross-rank GroupNorm combine reorders fp32 sums; bf16 activations amplify that slightly).
+match the unsharded single-process loop BIT FOR BIT under the product GEMM plan: the unsharded
+reference is planned as one of `world` shards (ops.gemm_plan(plan_div=world) -> vd_gemm_desc.plan_m:
+the same kernels, split-K counts and LayerNorm fusion as a rank's smaller M, so the same fp32
+summation order), GroupNorm records are frame-aligned and all-gathered in frame order, and every
+collective only moves bytes.  The chunked-overlap cases run the motion blocks at a further 1/c of
+the rows, a plan no single plan_div reproduces: those stay bounded at rel-L2 1e-2.
 """
 import os
 import socket
@@ -62,9 +66,7 @@ def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2, ov
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from vdiff import DenoiseLoop
-    from vdiff._lib import check, lib
-    check(lib().vd_gemm_select_path(gemm_path), "vd_gemm_select_path")
+    from vdiff import DenoiseLoop, ops
     from vdiff.dist import CfgShard, FrameShard, NodeLayout
 
     class HostStagedShard(FrameShard):
@@ -87,6 +89,8 @@ def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2, ov
         def gather_eps(self, eps):
             return super().gather_eps(eps.cpu()).to(eps.device)
 
+    plan = ops.gemm_plan(path=gemm_path)
+    plan.__enter__()  # for the whole worker process
     try:
         unet = _model(cfg)
         lay = NodeLayout(layout, FRAMES if cfg == "tiny" else FULL_FRAMES, world=world, rank=rank)
@@ -109,11 +113,25 @@ def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2, ov
         dist.destroy_process_group()
 
 
-@pytest.fixture(scope="module")
-def unsharded_ref(cuda):
-    from vdiff import DenoiseLoop
-    lat, ehs = _inputs()
-    return DenoiseLoop(_model(), _sched(), lat.cuda(), ehs.cuda(), 7.5, use_graph=False).prime().run(2).cpu()
+_REFS = {}
+
+
+def _unsharded(world, cfg="tiny", steps=2):
+    """The unsharded loop under the product plan, each GEMM planned as one of `world` frame shards."""
+    from vdiff import DenoiseLoop, ops
+    key = (world, cfg, steps)
+    if key not in _REFS:
+        lat, ehs = _inputs(cfg)
+        with ops.gemm_plan(plan_div=world):
+            _REFS[key] = DenoiseLoop(_model(cfg), _sched(), lat.cuda(), ehs.cuda(), 7.5,
+                                     use_graph=False).prime().run(steps).cpu()
+    return _REFS[key]
+
+
+def _report(tag, got, ref):
+    err = ((got.double() - ref.double()).norm() / ref.double().norm()).item()
+    print(f"{tag}: rel-L2 {err:.2e}, max|diff| {(got - ref).abs().max().item():.2e}")
+    return err
 
 
 @pytest.mark.parametrize("world,layout,overlap,window",
@@ -121,51 +139,47 @@ def unsharded_ref(cuda):
                           (2, "cfg-frame", 1, "a2a"), (4, "cfg-frame", 1, "a2a"), (8, "cfg-frame", 1, "a2a"),
                           (2, "frame", 2, "a2a"), (4, "cfg-frame", 4, "a2a"),
                           (2, "frame", 1, "kv-gather"), (4, "frame", 1, "kv-gather"), (8, "cfg-frame", 1, "kv-gather")])
-def test_ranks_on_one_gpu_match_unsharded(unsharded_ref, world, layout, overlap, window):
+def test_ranks_on_one_gpu_match_unsharded(cuda, world, layout, overlap, window):
     """layout "cfg-frame" (SURVEY §8e (ii)): the two CFG halves on two rank groups, eps
     swapped between CFG pairs before the update; at world 2 no motion-module collective.
     overlap > 1: the motion modules' all-to-alls chunked over positions on a side stream.
-    window "kv-gather": rows stay frame-sharded, every temporal attention's K/V all-gathered."""
-    ref = unsharded_ref
+    window "kv-gather": rows stay frame-sharded, every temporal attention's K/V all-gathered.
+    Both layouts give a rank 1/world of the rows, so the reference is planned with plan_div = world."""
+    ref = _unsharded(world)
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "out.pt")
         mp.start_processes(_worker, args=(world, _port(), path, layout, "tiny", 2, overlap, window), nprocs=world,
                            join=True, start_method="spawn")
         got = torch.load(path, weights_only=True)
     assert got.shape == ref.shape
-    err = ((got.double() - ref.double()).norm() / ref.double().norm()).item()
-    assert err < 1e-2, err
+    err = _report(f"tiny {world} ranks {layout} overlap {overlap} {window}", got, ref)
+    if overlap == 1:
+        assert torch.equal(got, ref), err
+    else:
+        assert err < 1e-2, err
 
 
 def test_full_model_eight_ranks_two_frames_match_unsharded(cuda):
     """BASELINE config 4 at its real shapes: the FULL 1.31B model, 16
     frames sharded 2 per rank over 8 ranks sharing cuda:0 (collectives staged through gloo),
-    one CFG DDIM step after prime(), against the unsharded 16-frame loop.  Both sides run one
-    GEMM path (vd_gemm_select_path(1): the register-staged kernel, unsplit, for every shape), so
-    the ranks' smaller M cannot change a GEMM plan or a split-K summation order; GroupNorm
+    one CFG DDIM step after prime(), against the unsharded 16-frame loop.  Both sides run the
+    PRODUCT GEMM plan (v2 / v3 / v5 / v6 with split-K where the rank's M asks for it); the
+    unsharded side plans every GEMM as a rank would (ops.gemm_plan(plan_div=8) ->
+    vd_gemm_desc.plan_m), so the same kernels, split counts and fusions run; GroupNorm
     splits are frame-aligned (a rank's records are the unsharded run's records of its frames,
     all-gathered in frame order) and image norms split by image size alone.  What is left is the
     collective decomposition itself — all-gathers and all-to-all re-shards that move bytes — so
     the sharded loop must equal the unsharded one BIT FOR BIT (printed: max |diff|, rel-L2).
     (Round 2 bounded this at 2e-2: any fp32 reordering anywhere decorrelates a bf16 network to
     its ~1 % realisation floor, so only exactness is a meaningful check.)"""
-    from vdiff import DenoiseLoop
-    from vdiff._lib import check, lib
-    lat, ehs = _inputs("full")
-    check(lib().vd_gemm_select_path(1), "vd_gemm_select_path")
-    try:
-        ref = DenoiseLoop(_model("full"), _sched(), lat.cuda(), ehs.cuda(), 7.5,
-                          use_graph=False).prime().run(1).cpu()
-    finally:
-        check(lib().vd_gemm_select_path(0), "vd_gemm_select_path")
+    ref = _unsharded(8, "full", 1)
     torch.cuda.empty_cache()
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "out.pt")
-        mp.start_processes(_worker, args=(8, _port(), path, "frame", "full", 1, 1, "a2a", 1), nprocs=8,
+        mp.start_processes(_worker, args=(8, _port(), path, "frame", "full", 1, 1, "a2a", 0), nprocs=8,
                            join=True, start_method="spawn")
         got = torch.load(path, weights_only=True)
+    _REFS.clear()
     assert got.shape == ref.shape == (1, 4, FULL_FRAMES, 64, 64)
-    err = ((got.double() - ref.double()).norm() / ref.double().norm()).item()
-    print(f"full model 8 ranks x 2 frames vs unsharded (one GEMM path): rel-L2 {err:.2e}, "
-          f"max|diff| {(got - ref).abs().max().item():.2e}")
+    err = _report("full model 8 ranks x 2 frames vs unsharded (product plan)", got, ref)
     assert torch.equal(got, ref), err

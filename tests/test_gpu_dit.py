@@ -376,20 +376,21 @@ def test_dit_20_frames_fused_rope_matches_unfused_and_oracle(dit_f20):
     assert e_fu < 0.03 and e_un < 0.03, (e_fu, e_un)
 
 
-def test_dit_20_frames_force_valu_falls_back(dit_f20):
-    """Under the force-VALU hook vd_temporal_attention_rope returns VD_EUNSUPPORTED and
-    ops.temporal_attention falls back to rope_qk + the VALU kernel: the model
-    still matches the fused MFMA path."""
-    from vdiff._lib import lib
-    m, _ = dit_f20
-    x, ehs = _f20_inputs()
-    ref = m(x.cuda(), 500, encoder_hidden_states=ehs.cuda()).sample.cpu()
-    lib().vd_temporal_force_valu(1)
-    try:
-        got = m(x.cuda(), 500, encoder_hidden_states=ehs.cuda()).sample.cpu()
-    finally:
-        lib().vd_temporal_force_valu(0)
-    assert rel_l2(got, ref) < 0.01
+def test_temporal_rope_valu_path_matches_fused(cuda):
+    """The DiT's temporal RoPE attention (20 frames, d 64): the VALU kernel, which has no fused
+    RoPE (ops.temporal_attention(valu=True) rotates a copy of q|k with vd_rope_qk first), equals
+    the fused MFMA kernel to bf16 rounding, and leaves the caller's q|k un-rotated."""
+    from vdiff import ops
+    batch, frames, pos, heads, d = 2, 20, 36, 3, 64
+    C = heads * d
+    g = torch.Generator(device="cuda").manual_seed(4)
+    qkv = (torch.randn(batch * frames * pos, 3 * C, device="cuda", generator=g) * 1.5).to(torch.bfloat16)
+    keep = qkv.clone()
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    fused = ops.temporal_attention(q, k, v, batch, frames, pos, heads, d, rope_theta=10000.0)
+    valu = ops.temporal_attention(q, k, v, batch, frames, pos, heads, d, rope_theta=10000.0, valu=True)
+    assert torch.equal(qkv, keep)
+    assert rel_l2(valu.float().cpu(), fused.float().cpu()) < 0.01
 
 
 def test_full_config_dit_fp8_forward(cuda):

@@ -98,14 +98,12 @@ def test_gemm_geglu(cuda):
 
 
 # ---------------------------------------------------------------- v2 (LDS-DMA) paths
-@pytest.fixture(params=["v6", "v5", "v3", "v2", "v1", "v2mf"])
+@pytest.fixture(params=["v6", "v5", "v3", "v2", "v1"])
 def gemm_path(request, cuda):
-    """Force one GEMM kernel (v3 only takes dense A; other shapes fall back to auto; v2mf = the
-    automatic plan with v2's 256 x 160 tiles in the 32x32x16 form for convs and dense GEMMs)."""
-    from vdiff._lib import lib
-    lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6, "v2mf": 18}[request.param])
-    yield request.param
-    lib().vd_gemm_select_path(0)
+    """Force one GEMM kernel per call (vd_gemm_desc.path; v3 only takes dense A, other shapes
+    fall back to the automatic plan)."""
+    with ops.gemm_plan(path={"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6}[request.param]):
+        yield request.param
 
 
 def test_gemm_large_dense(gemm_path):
@@ -129,9 +127,7 @@ def test_gemm_large_dense(gemm_path):
 def test_gemm_v3_shapes(cuda, M, N, K, k0):
     """v3 pipeline edges: 1-3 K-tiles (prologue / drain), ragged M and N, the a0|a1 channel
     concat split at k0, few tiles (split-K), bias + residual epilogue."""
-    from vdiff._lib import lib
-    lib().vd_gemm_select_path(3)
-    try:
+    with ops.gemm_plan(path=3):
         a = rnd(M, k0)
         a1 = rnd(M, K - k0) if K > k0 else None
         w = rnd(N, K, std=K ** -0.5)
@@ -140,8 +136,6 @@ def test_gemm_v3_shapes(cuda, M, N, K, k0):
         got = ops.gemm(a, w, a1=a1, bias=b, res=res)
         x = a if a1 is None else torch.cat([a, a1], 1)
         close_bf16(got, x.float() @ w.float().T + b + res.float())
-    finally:
-        lib().vd_gemm_select_path(0)
 
 
 @pytest.mark.parametrize("M,N,K,k0", [(256, 160, 32, 32), (300, 128, 96, 64), (513, 1000, 192, 160),
@@ -152,9 +146,7 @@ def test_gemm_v5_shapes(cuda, path, M, N, K, k0):
     """v5 (BK 32 ring; path 0 = automatic, which takes v5 for k0 % 64 != 0) pipeline edges: 1-3 k-steps (shorter than the ring), ragged M and
     N, the a0|a1 concat split at k0 (a multiple of 32, not of 64), few tiles (split-K), and
     the L1 shape whose units wrap the persistent grid several times."""
-    from vdiff._lib import lib
-    lib().vd_gemm_select_path(path)
-    try:
+    with ops.gemm_plan(path=path):
         a = rnd(M, k0)
         a1 = rnd(M, K - k0) if K > k0 else None
         w = rnd(N, K, std=K ** -0.5)
@@ -163,8 +155,6 @@ def test_gemm_v5_shapes(cuda, path, M, N, K, k0):
         got = ops.gemm(a, w, a1=a1, bias=b, res=res)
         x = a if a1 is None else torch.cat([a, a1], 1)
         close_bf16(got, x.float() @ w.float().T + b + res.float())
-    finally:
-        lib().vd_gemm_select_path(0)
 
 
 @pytest.mark.parametrize("M,N,K", [(131072, 960, 320), (1000, 328, 96), (4096, 640, 32), (300, 2560, 640)])
@@ -174,9 +164,7 @@ def test_gemm_v5_load_free_epilogue(cuda, path, M, N, K, epi):
     """v5's load-free epilogue (bias DMA'd into an LDS slot per unit, unconditional buffer
     stores with out-of-range lanes dropped, the stores left in flight across the next
     k-steps' counted waits): ragged M and N, one-k-step units, every activation."""
-    from vdiff._lib import lib
-    lib().vd_gemm_select_path(path)
-    try:
+    with ops.gemm_plan(path=path):
         a = rnd(M, K)
         if epi == "geglu":
             N = N // 32 * 32
@@ -190,8 +178,6 @@ def test_gemm_v5_load_free_epilogue(cuda, path, M, N, K, epi):
             got = ops.gemm(a, w, bias=b, act=ops.ACT_SILU if epi == "silu" else ops.ACT_NONE)
             want = a.float() @ w.float().T + (b if b is not None else 0)
             close_bf16(got, F.silu(want) if epi == "silu" else want)
-    finally:
-        lib().vd_gemm_select_path(0)
 
 
 @pytest.mark.parametrize("M,N,K,kind", [(256, 1280, 1280, "res"), (1024, 1280, 5120, "rowbias"), (100, 320, 2560, "silu"),
@@ -200,9 +186,7 @@ def test_gemm_v6_small_m_splitk(cuda, M, N, K, kind):
     """v6 (64 x 64 tiles, split K reduced in-kernel by the last-arriving K-slice): small M
     with long K (the split path), every epilogue flavour, and a second launch on the
     same workspace (the counters were reset)."""
-    from vdiff._lib import lib
-    lib().vd_gemm_select_path(6)
-    try:
+    with ops.gemm_plan(path=6):
         a = rnd(M, K)
         w = rnd(N, K, std=K ** -0.5)
         b = torch.randn(N, device=cuda)
@@ -224,17 +208,13 @@ def test_gemm_v6_small_m_splitk(cuda, M, N, K, kind):
             else:
                 close_f32(ops.gemm(a, w, bias=b, out_f32=True), x.double() @ w.double().T + b.double(),
                           rtol=1e-3, atol=1e-3)
-    finally:
-        lib().vd_gemm_select_path(0)
 
 
 @pytest.mark.parametrize("case", ["l3", "l4cat"])
 def test_conv3x3_v6_splitk(cuda, case):
     """Small-M implicit-GEMM conv on v6 with split K (L3/L4 shapes at 2 frames per GPU),
     including the up-block channel concat."""
-    from vdiff._lib import lib
-    lib().vd_gemm_select_path(6)
-    try:
+    with ops.gemm_plan(path=6):
         n, hw, c0, c1, co = (4, 16, 640, 0, 640) if case == "l3" else (4, 8, 1280, 1280, 1280)
         x0 = rnd(n * hw * hw, c0)
         x1 = rnd(n * hw * hw, c1) if c1 else None
@@ -246,8 +226,6 @@ def test_conv3x3_v6_splitk(cuda, case):
         img = xin.float().reshape(n, hw, hw, -1).permute(0, 3, 1, 2)
         want = F.conv2d(img, wt.float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, co) + res.float()
         close_bf16(out, want)
-    finally:
-        lib().vd_gemm_select_path(0)
 
 
 def test_gemm_large_geglu(gemm_path):
@@ -332,11 +310,8 @@ def test_gemm_ln(cuda, M, N, res, pe):
     if pe:
         ref = ref + pet.double()[(torch.arange(M, device=cuda) // pos) % frames]
     close_bf16(ln, ref)
-    lib().vd_gemm_select_path(2)  # unfused reference path: GEMM + vd_layernorm
-    try:
+    with ops.gemm_plan(path=2):  # unfused reference path: GEMM + vd_layernorm
         out2, ln2 = ops.gemm_ln(a, w, g, be, bias=b, res=r, **kw)
-    finally:
-        lib().vd_gemm_select_path(0)
     assert torch.equal(ln2, want)
     assert (ln.float() - ln2.float()).abs().max().item() <= 2 ** -6 * (ln2.float().abs().max().item() + 1)
 
@@ -375,44 +350,6 @@ def test_conv3x3_splitk(cuda):
     img = x.float().reshape(n, h, w, ci).permute(0, 3, 1, 2)
     want = F.conv2d(img, wt.float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, co) + res.float()
     close_bf16(out, want)
-
-
-@pytest.mark.parametrize("kind", ["conv", "conv_splitk", "dense_res", "dense_silu_f32", "dense_splitk"])
-def test_gemm_v2_mfma32(cuda, kind):
-    """v2 in the 32x32x16 form (vd_gemm_select_path(18)): one output row per lane, the
-    permlane32-paired 16-B epilogue (bias, row bias, SiLU, residual, fp32 out) and the split-K
-    slab in that layout, against fp32 / fp64 references."""
-    from vdiff._lib import lib
-    lib().vd_gemm_select_path(18)
-    try:
-        if kind.startswith("conv"):
-            n, h, w, ci, co = (8, 64, 64, 128, 320) if kind == "conv" else (32, 8, 8, 256, 1280)
-            x0, x1 = rnd(n * h * w, ci // 2), rnd(n * h * w, ci - ci // 2)
-            wt = bf(torch.randn(co, ci, 3, 3, device=cuda) * 0.03)
-            b = torch.randn(co, device=cuda)
-            temb = torch.randn(n, co, device=cuda)
-            res = rnd(n * h * w, co)
-            out, _, _ = ops.conv3x3(x0, n, h, w, pack_conv3x3(wt), x1=x1, bias=b, rowbias=temb, rb_div=h * w,
-                                    res=res)
-            img = torch.cat([x0, x1], 1).float().reshape(n, h, w, ci).permute(0, 3, 1, 2)
-            want = (F.conv2d(img, wt.float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, co) +
-                    temb.repeat_interleave(h * w, 0) + res.float())
-            close_bf16(out, want)
-            return
-        M, N, K = (32768, 640, 640) if kind != "dense_splitk" else (2048, 1280, 2560)
-        a, w = rnd(M, K), rnd(N, K, std=K ** -0.5)
-        b = torch.randn(N, device=cuda)
-        if kind == "dense_silu_f32":
-            got = ops.gemm(a, w, bias=b, act=ops.ACT_SILU, out_f32=True)
-            close_f32(got, F.silu(a.double() @ w.double().T + b.double()), rtol=1e-3, atol=1e-3)
-            return
-        temb = torch.randn(2, N, device=cuda)
-        res = rnd(M, N)
-        got = ops.gemm(a, w, bias=b, rowbias=temb, rb_div=M // 2, res=res)
-        want = a.float() @ w.float().T + b + temb.repeat_interleave(M // 2, 0) + res.float()
-        close_bf16(got, want)
-    finally:
-        lib().vd_gemm_select_path(0)
 
 
 # ---------------------------------------------------------------- conv
@@ -465,11 +402,8 @@ def test_conv3d_temporal_taps(cuda, kt, ks, stride, path):
     x = rnd(B * T * h * w, ci)
     wt = bf(torch.randn(co, ci, kt, ks, ks, device=cuda) * 0.05)
     b = torch.randn(co, device=cuda)
-    lib().vd_gemm_select_path({0: 0, 1: 1, 2: 2}[path])
-    try:
+    with ops.gemm_plan(path=path):
         out, ho, wo = ops.conv3d(x, B, T, h, w, pack_conv3d(wt), kt=kt, ks=ks, stride=stride, bias=b, out_f32=True)
-    finally:
-        lib().vd_gemm_select_path(0)
     vid = x.double().reshape(B, T, h, w, ci).permute(0, 4, 1, 2, 3).cpu()
     want = F.conv3d(vid, wt.double().cpu(), b.double().cpu(), stride=(1, stride, stride),
                     padding=(kt // 2, ks // 2, ks // 2))
@@ -559,21 +493,17 @@ def test_group_norm_paths(cuda, n_inst, pix, C, c0, silu, path):
     close_bf16(got, want)
 
 
-@pytest.mark.parametrize("C,rows", [(320, 4 * 16 * 24 + 5), (640, 1000), (1280, 333), (64, 77)])
-@pytest.mark.parametrize("multi_row", [1, 0])
-def test_layer_norm_kernels(cuda, C, rows, multi_row):
+@pytest.mark.parametrize("C,rows", [(320, 4 * 16 * 24 + 5), (640, 1000), (1280, 333), (64, 77), (128, 301),
+                                    (1152, 129), (2048, 65)])
+def test_layer_norm_kernels(cuda, C, rows):
     """Both LayerNorm kernels (several rows per wave for C in 320/640/1280, one row per wave
-    otherwise) with ragged row counts and the motion block's sinusoidal PE."""
-    from vdiff._lib import lib
+    otherwise: 64 / 128 the tiny config, 1152 the DiT, 2048 the widest row) with ragged row counts
+    and the motion block's sinusoidal PE."""
     x = rnd(rows, C) * 2 + 0.3
     g, b = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda)
     pe = torch.randn(16, C, device=cuda)
-    lib().vd_layernorm_select(multi_row)
-    try:
-        got = ops.layer_norm(x, g, b, pe=pe, pe_div=24, pe_period=16)
-        plain = ops.layer_norm(x, g, b)
-    finally:
-        lib().vd_layernorm_select(1)
+    got = ops.layer_norm(x, g, b, pe=pe, pe_div=24, pe_period=16)
+    plain = ops.layer_norm(x, g, b)
     f = (torch.arange(rows, device=cuda) // 24) % 16
     ref = F.layer_norm(x.double(), (C,), g.double(), b.double(), 1e-5)
     close_bf16(got, ref + pe.double()[f])
@@ -602,15 +532,13 @@ def sdpa_ref(q, k, v, batch, heads, sq, skv, d, kv_div=1, scale=None):
     return (w @ vb).transpose(1, 2).reshape(batch * sq, heads * d)
 
 
-@pytest.fixture(params=["flash40", "flash32", "v1", "flash32-qb1"])
+@pytest.fixture(params=["flash40", "flash32", "v1"])
 def attn_path(request, cuda):
-    """d = 40: "flash40" (round 3's two-group ping-pong over an LDS-DMA ring, wherever it applies:
-    >= 2 key tiles; the automatic choice from 4), "flash32" (the 4-wave 32x32x16 kernel), "v1"
-    (the 16x16x32 one), "flash32-qb1" (32x32x16 with one 32-query block per wave)."""
-    from vdiff._lib import lib
-    lib().vd_attention_select({"flash40": 7, "flash32": 8, "v1": 1, "flash32-qb1": 6}[request.param])
-    yield request.param
-    lib().vd_attention_select(0)
+    """d = 40, per call (vd_attention_ex's kernel): "flash40" (round 3's two-group ping-pong over
+    an LDS-DMA ring, wherever it applies: >= 2 key tiles; the automatic choice from 4), "flash32"
+    (the 4-wave 32x32x16 kernel), "v1" (the 16x16x32 one).  Other head widths take their one
+    kernel whatever is asked."""
+    return request.param
 
 
 @pytest.mark.parametrize("d", [32, 40, 64, 80, 128, 160])
@@ -656,7 +584,7 @@ def test_flash_attention_d40_paths(attn_path, sq, skv):
     C = heads * d
     q = rnd(batch * sq, 3 * C, std=1.5)[:, :C]
     kv = rnd(batch * skv, 2 * C, std=1.5)
-    got = ops.attention(q, kv[:, :C], kv[:, C:], batch, heads, sq, skv, d)
+    got = ops.attention(q, kv[:, :C], kv[:, C:], batch, heads, sq, skv, d, kernel=attn_path)
     close_bf16(got, sdpa_ref(q, kv[:, :C], kv[:, C:], batch, heads, sq, skv, d))
 
 
@@ -693,7 +621,7 @@ def _deferred_max_case(kind, sq=256, skv=640, d=40):
 def test_flash_attention_deferred_max(attn_path, kind):
     q, k, v = _deferred_max_case(kind)
     sq, skv, d = q.shape[0], k.shape[0], q.shape[1]
-    got = ops.attention(q, k, v, 1, 1, sq, skv, d)
+    got = ops.attention(q, k, v, 1, 1, sq, skv, d, kernel=attn_path)
     assert torch.isfinite(got.float()).all()
     # O is a convex combination of V rows and P is rounded to bf16 (relative 2^-9) before
     # PV, so the absolute error scales with |V|, not |O| (these cases concentrate the
@@ -709,7 +637,7 @@ def test_flash_attention_deferred_max_unit_scale(attn_path, kind):
     q, k, v = _deferred_max_case(kind)
     sq, skv, d = q.shape[0], k.shape[0], q.shape[1]
     q = bf(q.float() * d ** -0.5 * math.log2(math.e))  # scores in log2 units
-    got = ops.attention(q, k, v, 1, 1, sq, skv, d, scale=1.0 / math.log2(math.e))
+    got = ops.attention(q, k, v, 1, 1, sq, skv, d, scale=1.0 / math.log2(math.e), kernel=attn_path)
     assert torch.isfinite(got.float()).all()
     want = sdpa_ref(q, k, v, 1, 1, sq, skv, d, scale=1.0 / math.log2(math.e))
     close_bf16(got, want, abs_frac=2e-3 * v.float().abs().max().item() / want.abs().max().item())
@@ -743,7 +671,8 @@ def test_attention_fp32_out_north_star_tolerance(attn_path, d, sq, skv, batch, k
     q = bf(torch.randint(-1, 2, (batch * sq, C), device="cuda").float())
     k = bf(torch.randint(-1, 2, (batch // kv_div * skv, C), device="cuda").float())
     v = rnd(batch // kv_div * skv, C)
-    got = ops.attention(q, k, v, batch, heads, sq, skv, d, kv_div=kv_div, scale=1.0 / math.log2(math.e), out_f32=True)
+    got = ops.attention(q, k, v, batch, heads, sq, skv, d, kv_div=kv_div, scale=1.0 / math.log2(math.e), out_f32=True,
+                        kernel=attn_path)
     assert got.dtype == torch.float32
     qd = q.double().reshape(batch, sq, heads, d).transpose(1, 2)
     kd = k.double().reshape(batch // kv_div, skv, heads, d).transpose(1, 2).repeat_interleave(kv_div, 0)
@@ -757,14 +686,8 @@ def test_attention_fp32_out_north_star_tolerance(attn_path, d, sq, skv, batch, k
 
 
 def _flash40_vs_flash32(q, k, v, batch, heads, sq, skv, d, kv_div=1, scale=None, out_f32=False):
-    from vdiff._lib import lib
-    try:
-        lib().vd_attention_select(7)
-        a = ops.attention(q, k, v, batch, heads, sq, skv, d, kv_div=kv_div, scale=scale, out_f32=out_f32)
-        lib().vd_attention_select(8)
-        b = ops.attention(q, k, v, batch, heads, sq, skv, d, kv_div=kv_div, scale=scale, out_f32=out_f32)
-    finally:
-        lib().vd_attention_select(0)
+    a = ops.attention(q, k, v, batch, heads, sq, skv, d, kv_div=kv_div, scale=scale, out_f32=out_f32, kernel="flash40")
+    b = ops.attention(q, k, v, batch, heads, sq, skv, d, kv_div=kv_div, scale=scale, out_f32=out_f32, kernel="flash32")
     return a, b
 
 
@@ -826,7 +749,8 @@ def test_attention_d40_real_valued_north_star_tolerance(attn_path, sq, skv, batc
     q = bf(torch.randn(batch * sq, C, device="cuda") * 1.5 * d ** -0.5 * math.log2(math.e))
     k = bf(torch.randn(batch * skv, C, device="cuda") * 1.5)
     v = bf(torch.randn(batch * skv, C, device="cuda") * 1.5)
-    got = ops.attention(q, k, v, batch, heads, sq, skv, d, scale=1.0 / math.log2(math.e), out_f32=True)
+    got = ops.attention(q, k, v, batch, heads, sq, skv, d, scale=1.0 / math.log2(math.e), out_f32=True,
+                        kernel=attn_path)
     qd = q.double().reshape(batch, sq, heads, d).transpose(1, 2)
     kd = k.double().reshape(batch, skv, heads, d).transpose(1, 2)
     vd = v.double().reshape(batch, skv, heads, d).transpose(1, 2)
@@ -860,11 +784,9 @@ def test_attention_d40_real_valued_north_star_tolerance(attn_path, sq, skv, batc
 
 @pytest.fixture(params=["mfma", "valu"])
 def temporal_path(request, cuda):
-    """frames <= 16 with d in {40, 80, 160} run on the MFMA kernel unless forced to VALU."""
-    from vdiff._lib import lib
-    lib().vd_temporal_force_valu(int(request.param == "valu"))
-    yield request.param
-    lib().vd_temporal_force_valu(0)
+    """frames <= 16 with d in {40, 80, 160} run on the MFMA kernel; "valu" runs every shape on the
+    VALU kernel (vd_temporal_attention_valu)."""
+    return request.param
 
 
 @pytest.mark.parametrize("frames,d,scale", [(16, 40, None), (16, 80, None), (16, 160, None), (5, 40, None),
@@ -876,7 +798,7 @@ def test_temporal_attention(temporal_path, frames, d, scale):
     qkv = rnd(batch * frames * pos, 3 * C, std=1.5)
     q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
     sc = 1.0 / math.log2(math.e) if scale == "unit" else None   # the model's call (scale folded into to_q)
-    got = ops.temporal_attention(q, k, v, batch, frames, pos, heads, d, scale=sc)
+    got = ops.temporal_attention(q, k, v, batch, frames, pos, heads, d, scale=sc, valu=temporal_path == "valu")
     if sc is not None:
         q = q.double() * (sc * math.sqrt(d))   # sdpa_ref applies d^-0.5
 

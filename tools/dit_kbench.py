@@ -1,6 +1,6 @@
 """GEMM path sweep over the DiT's (BASELINE config 5) projection shapes, 1x MI355X.
 
-python tools/dit_kbench.py  -> per shape and path (vd_gemm_select_path): us, TFLOP/s
+python tools/dit_kbench.py  -> per shape and path (vd_gemm_desc.path): us, TFLOP/s
 """
 import sys
 from pathlib import Path
@@ -42,7 +42,7 @@ for name, K, N, epi in SHAPES:
     line = f"{name:10s} M={M} N={N} K={K}"
     ref = None
     for path in (0, 2, 3, 5, 6):
-        lib().vd_gemm_select_path(path)
+        ops._PLAN.path = path  # per-call vd_gemm_desc.path
         try:
             fn = lambda: ops.gemm(a, w, bias=bias, res=res, act=act, out=out)  # noqa: E731
             us = timeit(fn)
@@ -53,6 +53,6 @@ for name, K, N, epi in SHAPES:
             line += f" | p{path} {us:8.1f} us {2 * M * N * K / us / 1e6:6.0f} TF/s{'' if ok else ' MISMATCH'}"
         except Exception as e:  # noqa: BLE001
             line += f" | p{path} err {str(e)[:30]}"
-    lib().vd_gemm_select_path(0)
+    ops._PLAN.path = 0  # per-call vd_gemm_desc.path
     print(line, flush=True)
     del a, w, res, out

@@ -35,7 +35,7 @@ for M, N, K in [(256, 64, 64), (256, 64, 320), (256, 64, 1280), (256, 1280, 1280
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     row = []
     for path, code in (("auto", 0), ("v1", 1), ("v2", 2), ("v6", 8)):
-        lib().vd_gemm_select_path(code)
+        ops._PLAN.path = code  # per-call vd_gemm_desc.path
         row.append(f"{path} {graph_us(lambda: ops.gemm(a, w, out=out)):6.1f}")
-    lib().vd_gemm_select_path(0)
+    ops._PLAN.path = 0  # per-call vd_gemm_desc.path
     print(f"gemm M={M:5d} N={N:5d} K={K:5d}: " + "  ".join(row) + " us", flush=True)

@@ -49,10 +49,10 @@ for name, M, N, K, act in SHAPES:
     out = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
     res = []
     for path, code in (("auto", 0), ("v2", 2), ("v3", 3)):
-        lib().vd_gemm_select_path(code)
+        ops._PLAN.path = code  # per-call vd_gemm_desc.path
         us = timeit(lambda: ops.gemm(a, w, bias=b, act=act, out=out))
         res.append(f"{path} {us:7.1f}us {2.0 * M * N * K / us / 1e6:6.0f}TF")
-    lib().vd_gemm_select_path(0)
+    ops._PLAN.path = 0  # per-call vd_gemm_desc.path
     us = timeit(lambda: torch.nn.functional.linear(a, w))
     res.append(f"hipblaslt {us:7.1f}us {2.0 * M * N * K / us / 1e6:6.0f}TF")
     print(f"{name:22s} M={M:6d} N={N:5d} K={K:5d} | " + " | ".join(res), flush=True)

@@ -67,14 +67,14 @@ for name, kind, M, N, K, res in cases:
             us = timeit(lambda: torch.nn.functional.linear(a, w))
             report(f"{name} [hipblaslt]", us, 2.0 * M * N * K, 2 * (M * K + N * K + M * N))
             continue
-        lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6, "pre6": 7, "v6ns": 8, "cap8": 9, "v3np": 10, "autonp": 11, "old": 12, "pf2": 13, "pf1": 14, "v3slow": 15, "v5half": 16, "v2mfc": 17, "v2mf": 18, "mfl1": 19, "div64": 20}[path])
+        ops._PLAN.path = {"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6}[path]  # per-call vd_gemm_desc.path
         act = ops.ACT_GEGLU if kind == "geglu" else ops.ACT_NONE
         nout = N // 2 if kind == "geglu" else N
         out = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
         us = timeit(lambda: ops.gemm(a, w, bias=b, res=r, act=act, out=out))
         byts = 2 * (M * K + N * K + M * nout + (M * N if res else 0))
         report(f"{name} [{path}]", us, 2.0 * M * N * K, byts)
-    lib().vd_gemm_select_path(0)
+    ops._PLAN.path = 0  # per-call vd_gemm_desc.path
 
 for name, n, hw, ci, co in convs:
     if flt not in name:
@@ -90,11 +90,11 @@ for name, n, hw, ci, co in convs:
             report(f"{name} M={n*hw*hw} K={9*ci} [miopen]", us, 2.0 * n * hw * hw * co * 9 * ci,
                    2 * (n * hw * hw * (ci + co) + co * 9 * ci))
             continue
-        lib().vd_gemm_select_path({"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6, "pre6": 7, "v6ns": 8, "cap8": 9, "v3np": 10, "autonp": 11, "old": 12, "pf2": 13, "pf1": 14, "v3slow": 15, "v5half": 16, "v2mfc": 17, "v2mf": 18, "mfl1": 19, "div64": 20}[path])
+        ops._PLAN.path = {"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6}[path]  # per-call vd_gemm_desc.path
         us = timeit(lambda: ops.conv3x3(x, n, hw, hw, w, out=out))
         report(f"{name} M={n*hw*hw} K={9*ci} [{path}]", us, 2.0 * n * hw * hw * co * 9 * ci,
                2 * (n * hw * hw * (ci + co) + co * 9 * ci))
-    lib().vd_gemm_select_path(0)
+    ops._PLAN.path = 0  # per-call vd_gemm_desc.path
 
 for name, n_img, S, d, skv in [("attn L1 self", 32, 4096, 40, 4096), ("attn L2 self", 32, 1024, 80, 1024),
                                ("attn L3 self", 32, 256, 160, 256), ("attn L1 cross", 32, 4096, 40, 77),

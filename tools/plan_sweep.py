@@ -52,7 +52,7 @@ def run(imgs):
     for rnd_i in range(4):  # round 0 = warm-up, not recorded
         for name, fn in fns:
             for path, code in PATHS.items():
-                lib().vd_gemm_select_path(code)
+                ops._PLAN.path = code  # per-call vd_gemm_desc.path
                 try:
                     for _ in range(2):
                         fn()
@@ -67,7 +67,7 @@ def run(imgs):
                     us = float("nan")
                 if rnd_i:
                     best[(name, path)] = min(best.get((name, path), float("inf")), us)
-        lib().vd_gemm_select_path(0)
+        ops._PLAN.path = 0  # per-call vd_gemm_desc.path
     for name, _ in fns:
         row = "  ".join(f"{p} {best[(name, p)]:7.1f}" for p in PATHS)
         print(f"[{imgs:2d} img] {name:36s} {row}", flush=True)

@@ -32,10 +32,6 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int KT = 64;   // keys per tile
-int g_f4_g1 = 0;         // flash40 LDS-DMA issuer placement (A/B, vd_attention_select 25-30; 26 = 0 the default)
-int g_flash32 = 1;       // d = 40: 1 = automatic (flash40 for >= 4 key tiles, else flash32), 7 = flash32 only,
-                         // 6 = flash40 wherever it applies, 8 = flash40 stamped (diagnostic),
-                         // 2 = flash32pp (8-wave pipeline), 0 = flash_attn 16x16x32
 
 template <int D>
 struct AttnCfg {
@@ -426,7 +422,7 @@ __device__ __forceinline__ float partner32(float x) {
 // >= the running max (l >= 2^(max - mu)), so nothing underflows that matters;
 // a row sum >= 2^100 (or non-finite) means a score jumped past the fp32/bf16
 // range and the pass reports `bad` so the block reruns EXACT.
-template <int D, bool UNITC, bool EXACT, bool IL = false, int QB = 2>
+template <int D, bool UNITC, bool EXACT, int QB = 2>
 __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, const bf16_t* vb_ptr, int ldk32,
                                          int ldv32, int64_t skv, const int (&krow)[F32Cfg<D>::LREG],
                                          const uint32_t (&kcol)[F32Cfg<D>::LREG],
@@ -624,146 +620,7 @@ __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, cons
     }
     __syncthreads();
   };
-  // a steady-state tile of the fast pass (not the first, not a ragged last one),
-  // software-pipelined inside the wave: the exps of key block 0 issue in the shadow of
-  // key block 1's QK^T MFMAs, and key block 1's exps in the shadow of block 0's PV MFMAs
-  // (MI355X_MICROARCH.md: an MFMA leaves 24 of its 32 issue cycles to VALU work).  The
-  // rescale check runs before the tile's QK^T instead of after it: the new -mu is in Q'
-  // before the MFMAs, so the scores come out already shifted.  Kept out of the general
-  // tile's loop: the two bodies in one loop spill (the register allocator merges them).
-  auto tile_il = [&](int t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, t + 1, skv, krow, kcol);
-    const bf16_t* kl = lds + buf * C::STAGE;
-    const bf16_t* vl = kl + C::K_ELEMS;
-    if (t > 1) {
-      float lq[QB];
-      bool resc = false, over = false;
-#pragma unroll
-      for (int qb = 0; qb < QB; ++qb) {
-        const float lown = oacc[C::L_DB][qb][C::L_I];
-        const float lp = partner32(lown);
-        lq[qb] = hh == C::L_H ? lown : lp;
-        resc |= lq[qb] > RESCALE;
-        over |= !(lq[qb] < BAD);
-      }
-      if (__any(over)) {
-        bad = true;
-      } else if (__any(resc)) {
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
-          const float step = lq[qb] > RESCALE ? __builtin_amdgcn_logf(lq[qb]) : 0.f;
-          const float nmu = (float)(__bf16)(mu[qb] + (UNITC ? step : step / c));
-          const float alpha = __builtin_amdgcn_exp2f(UNITC ? mu[qb] - nmu : (mu[qb] - nmu) * c);
-          mu[qb] = nmu;
-#pragma unroll
-          for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
-          if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
-        }
-      }
-    }
-    bf16x8 kfr[2][C::KSTEPS];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int ks = 0; ks < C::KSTEPS; ++ks)
-        kfr[kb][ks] = *(const bf16x8*)(kl + (kb * 32 + r32) * C::KS + ks * 16 + 8 * hh);
-    __builtin_amdgcn_sched_barrier(0);
-    f32x16 s[2][QB];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int ks = 0; ks < C::KSTEPS; ++ks)
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
-          if (ks == 0) {
-            f32x16 z;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) z[i] = 0.f;
-            s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], z, 0, 0, 0);
-          } else {
-            s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], s[kb][qb], 0, 0, 0);
-          }
-        }
-    bf16x8 vfr[C::NDB][2][2];
-#pragma unroll
-    for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16_t* p0 = vl + (db * KT + kb * 32 + 16 * s2) * 32 + vtr;
-          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-              (bf16x4 __attribute__((address_space(3)))*)(p0));
-          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-              (bf16x4 __attribute__((address_space(3)))*)(p0 + 8 * 32));
-          vfr[db][kb][s2] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      bf16x8 pf[2][QB];
-#pragma unroll
-      for (int qb = 0; qb < QB; ++qb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 f;
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            f[j] = (__bf16)__builtin_amdgcn_exp2f(UNITC ? s[kb][qb][8 * s2 + j] : s[kb][qb][8 * s2 + j] * c);
-          pf[s2][qb] = f;
-        }
-#pragma unroll
-      for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int qb = 0; qb < QB; ++qb)
-            oacc[db][qb] =
-                __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[db][kb][s2], pf[s2][qb], oacc[db][qb], 0, 0, 0);
-    }
-    // issue order: QK^T(kb 0); QK^T(kb 1) | exp(kb 0); rest of exp(kb 0); PV(kb 0) | exp(kb 1); PV(kb 1)
-    constexpr int NQK = 2 * C::KSTEPS * QB / 2;       // MFMAs per key block
-    constexpr int NPV = C::NDB * 2 * QB;              // MFMAs per key block
-    constexpr int NV = 16 * QB + 8 * QB;              // exps + packs per key block
-    constexpr int V1 = NV / 2 / NQK;                  // per QK^T(kb 1) MFMA
-    constexpr int V2 = NV / NPV;                      // per PV(kb 0) MFMA
-#pragma unroll
-    for (int i = 0; i < NQK; ++i) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-#pragma unroll
-    for (int i = 0; i < NQK; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, V1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x002, NV - V1 * NQK, 0);
-#pragma unroll
-    for (int i = 0; i < NPV; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, V2, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < NPV; ++i) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < ntiles) {
-      bf16_t* nb = lds + (buf ^ 1) * C::STAGE;
-#pragma unroll
-      for (int i = 0; i < C::LREG; ++i) {
-        *(uint4*)(nb + ldsk[i]) = make_uint4(kvst[4 * i], kvst[4 * i + 1], kvst[4 * i + 2], kvst[4 * i + 3]);
-        *(uint4*)(nb + ldsv[i]) = make_uint4(kvst[4 * C::LREG + 4 * i], kvst[4 * C::LREG + 4 * i + 1],
-                                             kvst[4 * C::LREG + 4 * i + 2], kvst[4 * C::LREG + 4 * i + 3]);
-      }
-    }
-    __syncthreads();
-  };
-  if constexpr (IL && !EXACT) {
-    tile_generic(0);
-    const int tend = ragged ? ntiles - 1 : ntiles;
-    for (int t = 1; t < tend; ++t) tile_il(t);
-    if (ragged && ntiles > 1) tile_generic(ntiles - 1);
-  } else {
-    for (int t = 0; t < ntiles; ++t) tile_generic(t);
-  }
+  for (int t = 0; t < ntiles; ++t) tile_generic(t);
   if (!EXACT) {  // the last tiles' row sums were not checked in the loop
     bool over = false;
 #pragma unroll
@@ -777,13 +634,13 @@ __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, cons
   return bad;
 }
 
-// QB = 32-query blocks per wave: 2 (default: 256 VGPRs, two waves per SIMD) or 1 (half the
-// registers, three waves per SIMD — round 2's occupancy variant, vd_attention_select(6)).
+// QB = 32-query blocks per wave: 2 (256 VGPRs, two waves per SIMD; one block per wave with three
+// waves per SIMD measured slower, 1010 vs 878 us: profiles/r02_attn_occupancy_ab.txt).
 // FIX: flash40's exact fix-up pass — a block whose first output element is a NaN flag (flash40
 // found a score jump past its fast pass's range there) recomputes its 256 queries with the exact
 // pass; every other block returns at once.
-template <int D, bool UNITC, bool IL = false, int QB = 2, bool FIX = false>
-__global__ __launch_bounds__(NT, QB == 1 ? 3 : 2) void flash32_kernel(
+template <int D, bool UNITC, bool FIX = false, int QB = 2>
+__global__ __launch_bounds__(NT, 2) void flash32_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
     int64_t sq, int64_t skv, int64_t kv_div, float c, int out_f32 = 0) {
@@ -857,13 +714,13 @@ __global__ __launch_bounds__(NT, QB == 1 ? 3 : 2) void flash32_kernel(
   // V^T tr-read lane offset inside a [32 d] image row block (elements)
   const int vtr = ((4 * hh + (i16 >> 2)) * 32) + 16 * (g16 & 1) + 4 * (i16 & 3);
   f32x16 oacc[C::NDB][QB];
-  const bool bad = FIX || f32_loop<D, UNITC, false, IL, QB>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk,
+  const bool bad = FIX || f32_loop<D, UNITC, false, QB>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk,
                                                            ldsv, qf, oacc, r32, hh, vtr, c);
   if (__syncthreads_or(bad)) {  // a score jumped > ~100 (log2) past mu somewhere: exact pass
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb)
       if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)0.0f;
-    f32_loop<D, UNITC, true, false, QB>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv, qf, oacc, r32, hh,
+    f32_loop<D, UNITC, true, QB>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv, qf, oacc, r32, hh,
                              vtr, c);
   }
 
@@ -901,352 +758,6 @@ __global__ __launch_bounds__(NT, QB == 1 ? 3 : 2) void flash32_kernel(
         auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
         auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
         // lanes < 32: (x, y) = channels 16m + 0..7; lanes >= 32: channels 16m + 8..15
-        const int dd = 32 * db + 16 * m + 8 * hh;
-        if (qi < sq && dd + 8 <= D) *(uint4*)(orow + dd) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-      }
-    }
-  }
-}
-
-// ============================================================ flash32pp
-// flash32 as a software pipeline over two staggered wave groups (FA3-style ping-pong;
-// MI355X_MICROARCH.md "Two waves per SIMD" items 1-3 and 9).  Each wave's tile work is
-// split into
-//     M(t) = PV(t-1) + QK^T(t)        — MFMA only (16 + 12 x 32x32x16)
-//     V(t) = the softmax of tile t    — VALU only (tile max / rescale, exp2, bf16 pack)
-// with tile t's P fragments kept in registers from V(t) to M(t+1), and group 1 (waves
-// 4-7) runs one barrier behind group 0: on every SIMD one wave issues MFMAs while its
-// partner does its VALU.  (In the 4-wave flash32 both waves of a SIMD reached the same
-// phase together: a 64x64 tile cost ~1800 cycles per wave against 896 of MFMA.)
-// Barriers: every interval ends with one; the group leaving M waits for its LDS traffic
-// first (__syncthreads), the group leaving V passes a raw s_barrier (the next tile's
-// global loads stay in flight).  LDS: three K/V buffers, tile t in buffer t % 3; group 0
-// issues the global loads of tile t+2 at the start of V(t) and writes them in M(t+1)
-// (interval 2t+2), when buffer (t+2) % 3 = (t-1) % 3 was last read by group 1's M(t)
-// (V of tile t-1) in interval 2t+1.  512 queries per workgroup share each K/V tile.
-__device__ __forceinline__ void bar_raw() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int D>
-__device__ __forceinline__ void f32_qk(const bf16_t* kl, int r32, int hh, const bf16x8 (&kfr)[2][F32Cfg<D>::KSTEPS],
-                                       const bf16x8 (&qf)[2][F32Cfg<D>::KSTEPS], f32x16 (&s)[2][2]) {
-  using C = F32Cfg<D>;
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-    for (int ks = 0; ks < C::KSTEPS; ++ks) {
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        if (ks == 0) {
-          f32x16 z;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) z[i] = 0.f;
-          s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], z, 0, 0, 0);
-        } else {
-          s[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[qb][ks], s[kb][qb], 0, 0, 0);
-        }
-      }
-    }
-  }
-}
-
-template <int D>
-__device__ __forceinline__ void f32_read_k(const bf16_t* kl, int r32, int hh, bf16x8 (&kfr)[2][F32Cfg<D>::KSTEPS]) {
-  using C = F32Cfg<D>;
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int ks = 0; ks < C::KSTEPS; ++ks)
-      kfr[kb][ks] = *(const bf16x8*)(kl + (kb * 32 + r32) * C::KS + ks * 16 + 8 * hh);
-}
-
-template <int D, bool UNITC, bool EXACT>
-__device__ __forceinline__ bool f32pp_loop(bf16_t* lds, const bf16_t* kb_ptr, const bf16_t* vb_ptr, int ldk32,
-                                           int ldv32, int64_t skv, const int (&krow)[F32Cfg<D>::LREG],
-                                           const uint32_t (&kcol)[F32Cfg<D>::LREG],
-                                           const uint32_t (&ldsk)[F32Cfg<D>::LREG],
-                                           const uint32_t (&ldsv)[F32Cfg<D>::LREG],
-                                           bf16x8 (&qf)[2][F32Cfg<D>::KSTEPS], f32x16 (&oacc)[F32Cfg<D>::NDB][2],
-                                           int r32, int hh, int vtr, float c, bool g0) {
-  using C = F32Cfg<D>;
-  constexpr int QB = 2;
-  constexpr float RESCALE = 4294967296.0f;        // 2^32
-  constexpr float BAD = 1.2676506002282294e30f;   // 2^100
-#pragma unroll
-  for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[db][qb][i] = 0.f;
-  float mu[QB];
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb) mu[qb] = 0.f;
-  bool bad = false;
-
-  const int ntiles = (int)((skv + KT - 1) / KT);
-  const bool ragged = (skv % KT) != 0;
-  stage_t<C::LREG> kvst;
-  if (g0) {  // tiles 0 and 1 before the loop
-    kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, 0, skv, krow, kcol);
-    kv_store<C::LREG>(kvst, lds, lds, ldsk, ldsv);
-    if (ntiles > 1) {
-      kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, 1, skv, krow, kcol);
-      kv_store<C::LREG>(kvst, lds + C::STAGE, lds + C::STAGE, ldsk, ldsv);
-    }
-  }
-  __syncthreads();
-  if (!g0) bar_raw();  // the stagger: group 1 runs one barrier behind
-
-  // ---- M(0): QK^T of tile 0
-  f32x16 s[2][QB];
-  {
-    bf16x8 kfr[2][C::KSTEPS];
-    f32_read_k<D>(lds, r32, hh, kfr);
-    f32_qk<D>(lds, r32, hh, kfr, qf, s);
-  }
-  __syncthreads();
-
-  for (int t = 0; t < ntiles; ++t) {
-    // ================= V(t): softmax of tile t -> pf (group 0 also issues tile t+2's loads)
-    if (g0 && t + 2 < ntiles) kvst = kv_load<C::LREG>(kb_ptr, vb_ptr, ldk32, ldv32, t + 2, skv, krow, kcol);
-    if (ragged && t == ntiles - 1) {
-      const int kvalid = (int)(skv - (int64_t)t * KT);
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (key >= kvalid) {
-#pragma unroll
-            for (int qb = 0; qb < QB; ++qb) s[kb][qb][i] = -INFINITY;
-          }
-        }
-    }
-    if (EXACT || t == 0) {
-      float tm[QB];
-      bool need = t == 0;
-#pragma unroll
-      for (int qb = 0; qb < QB; ++qb) {
-        const float m = tile_max(s[0][qb], s[1][qb]);
-        tm[qb] = vmax2(m, partner32(m));
-        need |= (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
-      }
-      if (__any(need)) {
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
-          const bool up = t == 0 || (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
-          const float nmu = up ? (float)(__bf16)(mu[qb] + tm[qb]) : mu[qb];
-          const float delta = nmu - mu[qb];
-          const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
-          mu[qb] = nmu;
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) s[kb][qb][i] -= delta;
-#pragma unroll
-          for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
-          if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
-        }
-      }
-    }
-    if (!EXACT && t > 1) {  // fast pass: rescale from the row sum of tiles 0..t-1 past 2^32
-      float lq[QB];
-      bool resc = false, over = false;
-#pragma unroll
-      for (int qb = 0; qb < QB; ++qb) {
-        const float lown = oacc[C::L_DB][qb][C::L_I];
-        const float lp = partner32(lown);
-        lq[qb] = hh == C::L_H ? lown : lp;
-        resc |= lq[qb] > RESCALE;
-        over |= !(lq[qb] < BAD);
-      }
-      if (__any(over)) {
-        bad = true;
-      } else if (__any(resc)) {
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
-          const float step = lq[qb] > RESCALE ? __builtin_amdgcn_logf(lq[qb]) : 0.f;
-          const float nmu = (float)(__bf16)(mu[qb] + (UNITC ? step : step / c));
-          const float delta = nmu - mu[qb];
-          const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
-          mu[qb] = nmu;
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) s[kb][qb][i] -= delta;
-#pragma unroll
-          for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
-          if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
-        }
-      }
-    }
-    bf16x8 pf[2][2][QB];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int qb = 0; qb < QB; ++qb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 f;
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            f[j] = (__bf16)__builtin_amdgcn_exp2f(UNITC ? s[kb][qb][8 * s2 + j] : s[kb][qb][8 * s2 + j] * c);
-          pf[kb][s2][qb] = f;
-        }
-    bar_raw();  // end of V(t)
-
-    // ================= M(t+1): PV(t) + QK^T(t+1); group 0 writes tile t+2
-    {
-      const bf16_t* vl = lds + (t % 3) * C::STAGE + C::K_ELEMS;
-      bf16x8 vfr[C::NDB][2][2];
-#pragma unroll
-      for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const bf16_t* p0 = vl + (db * KT + kb * 32 + 16 * s2) * 32 + vtr;
-            const bf16x4 lo =
-                __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(p0));
-            const bf16x4 hi =
-                __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(p0 + 8 * 32));
-            vfr[db][kb][s2] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          }
-#pragma unroll
-      for (int db = 0; db < C::NDB; ++db)
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-            for (int qb = 0; qb < QB; ++qb)
-              oacc[db][qb] =
-                  __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[db][kb][s2], pf[kb][s2][qb], oacc[db][qb], 0, 0, 0);
-      // P and the V fragments die here; keep QK^T's accumulators from overlapping them
-      __builtin_amdgcn_sched_barrier(0);
-      if (t + 1 < ntiles) {
-        bf16x8 kfr[2][C::KSTEPS];
-        f32_read_k<D>(lds + ((t + 1) % 3) * C::STAGE, r32, hh, kfr);
-        f32_qk<D>(lds, r32, hh, kfr, qf, s);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (g0 && t + 2 < ntiles) {
-        bf16_t* nb = lds + ((t + 2) % 3) * C::STAGE;
-        kv_store<C::LREG>(kvst, nb, nb, ldsk, ldsv);
-      }
-    }
-    __syncthreads();  // end of M(t+1): tile t+2's LDS writes (group 0) complete
-  }
-  if (g0) bar_raw();  // balance the stagger
-  if (!EXACT) {
-    bool over = false;
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-      const float lown = oacc[C::L_DB][qb][C::L_I];
-      const float lp = partner32(lown);
-      over |= !((hh == C::L_H ? lown : lp) < BAD);
-    }
-    bad |= __any(over);
-  }
-  return bad;
-}
-
-template <int D, bool UNITC>
-__global__ __launch_bounds__(2 * NT, 1) void flash32pp_kernel(
-    const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
-    const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
-    int64_t sq, int64_t skv, int64_t kv_div, float c) {
-  using C = F32Cfg<D>;
-  constexpr int QB = 2;
-  constexpr int QWG = 8 * 32 * QB;  // queries per workgroup
-  __shared__ __attribute__((aligned(16))) bf16_t lds[3 * C::STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool g0 = wave < 4;
-  const int r32 = lane & 31, hh = lane >> 5;
-  const int nqb = (int)((sq + QWG - 1) / QWG);
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int qblk = lid % nqb;
-  const int h = (lid / nqb) % heads;
-  const int64_t b = (lid / nqb) / heads;
-  const int64_t q0 = (int64_t)qblk * QWG + wave * (32 * QB);
-  const int64_t bkv = b / kv_div;
-  const bf16_t* qb_ptr = q + b * sq * ldq + (int64_t)h * D;
-  const bf16_t* kb_ptr = k + bkv * skv * ldk + (int64_t)h * D;
-  const bf16_t* vb_ptr = v + bkv * skv * ldv + (int64_t)h * D;
-
-  bf16x8 qf[QB][C::KSTEPS];
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb) {
-    const int64_t qi = q0 + qb * 32 + r32;
-#pragma unroll
-    for (int ks = 0; ks < C::KSTEPS; ++ks) {
-      const int dd = ks * 16 + 8 * hh;
-      uint4 u = make_uint4(0, 0, 0, 0);
-      if (qi < sq && dd < D) u = *(const uint4*)(qb_ptr + qi * ldq + dd);
-      qf[qb][ks] = __builtin_bit_cast(bf16x8, u);
-    }
-  }
-  for (int idx = tid; idx < 3 * KT; idx += 2 * NT) {
-    const int buf = idx / KT, r = idx % KT;
-    bf16_t* kl = lds + buf * C::STAGE;
-    bf16_t* vl = kl + C::K_ELEMS;
-    for (int cc = C::DCH; cc < C::DK / 8; ++cc)
-      *(uint4*)(kl + r * C::KS + cc * 8) = make_uint4(cc == C::DCH ? 0x3F80u : 0u, 0, 0, 0);
-    for (int cc = C::DCH; cc < C::DVP / 8; ++cc)
-      *(uint4*)(vl + ((cc >> 2) * KT + r) * 32 + (cc & 3) * 8) = make_uint4(cc == C::DCH ? 0x3F80u : 0u, 0, 0, 0);
-  }
-  // staging slots of group 0's 256 threads (group 1 never stages)
-  const int st = tid & (NT - 1);
-  int krow[C::LREG];
-  uint32_t kcol[C::LREG], ldsk[C::LREG], ldsv[C::LREG];
-#pragma unroll
-  for (int i = 0; i < C::LREG; ++i) {
-    const int idx = (st + i * NT) % (KT * C::DCH);
-    const int r = idx / C::DCH, cc = idx % C::DCH;
-    krow[i] = r;
-    kcol[i] = (uint32_t)(cc * 8);
-    ldsk[i] = (uint32_t)(r * C::KS + cc * 8);
-    ldsv[i] = (uint32_t)(C::K_ELEMS + ((cc >> 2) * KT + r) * 32 + (cc & 3) * 8);
-  }
-  const int ldk32 = (int)ldk, ldv32 = (int)ldv;
-  const int g16 = lane >> 4, i16 = lane & 15;
-  const int vtr = ((4 * hh + (i16 >> 2)) * 32) + 16 * (g16 & 1) + 4 * (i16 & 3);
-  f32x16 oacc[C::NDB][QB];
-  const bool bad = f32pp_loop<D, UNITC, false>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv,
-                                               qf, oacc, r32, hh, vtr, c, g0);
-  if (__syncthreads_or(bad)) {
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb)
-      if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)0.0f;
-    f32pp_loop<D, UNITC, true>(lds, kb_ptr, vb_ptr, ldk32, ldv32, skv, krow, kcol, ldsk, ldsv, qf, oacc, r32, hh,
-                               vtr, c, g0);
-  }
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb) {
-    const float lown = oacc[C::L_DB][qb][C::L_I];
-    const float lp = partner32(lown);
-    const float l = hh == C::L_H ? lown : lp;
-    const float inv = __builtin_amdgcn_rcpf(l);
-    const int64_t qi = q0 + qb * 32 + r32;
-    bf16_t* orow = o + (b * sq + (qi < sq ? qi : 0)) * ldo + (int64_t)h * D;
-#pragma unroll
-    for (int db = 0; db < C::NDB; ++db) {
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        const f32x16& a = oacc[db][qb];
-        uint32_t x0 = pack2(a[8 * m + 0] * inv, a[8 * m + 1] * inv), x1 = pack2(a[8 * m + 2] * inv, a[8 * m + 3] * inv);
-        uint32_t y0 = pack2(a[8 * m + 4] * inv, a[8 * m + 5] * inv), y1 = pack2(a[8 * m + 6] * inv, a[8 * m + 7] * inv);
-        auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
-        auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
         const int dd = 32 * db + 16 * m + 8 * hh;
         if (qi < sq && dd + 8 <= D) *(uint4*)(orow + dd) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
       }
@@ -1313,12 +824,13 @@ __device__ __forceinline__ void f4_dma(u32x4 rs, uint32_t lds, uint32_t voff) {
 // This wave's two pieces of every tile (waves 0-5; piece p = 2 wave + i): 0-4 = K chunk p of
 // the 64 keys (lane = key), 5 = the K' ones chunk, 6-9 = V d 0..31 of keys 16 (p-6) + lane/4
 // (lane % 4 = chunk), 10 = V d 32..39, 11 = the V ones chunk.
-struct F4Dma {  // up to 3 pieces per issuing wave (G1: waves 4-7 issue all 12)
-  u32x4 rs[3];
-  uint32_t voff[3];   // lane part of the byte offset (row r, column chunk), or 0 for a ones chunk
-  uint32_t step[3];   // bytes per key (0 for a ones chunk)
-  uint32_t row[3];    // the lane's key inside the tile
-  uint32_t lds[3];    // byte offset of the piece inside a slot
+struct F4Dma {  // the issuing wave's two pieces (placements over other waves / phases measured
+                // slower, profiles/r03h_flash40_dma_issuers_ab.txt, r03p_flash40_dma_interval_ab.txt)
+  u32x4 rs[2];
+  uint32_t voff[2];   // lane part of the byte offset (row r, column chunk), or 0 for a ones chunk
+  uint32_t step[2];   // bytes per key (0 for a ones chunk)
+  uint32_t row[2];    // the lane's key inside the tile
+  uint32_t lds[2];    // byte offset of the piece inside a slot
 };
 
 template <int NP>
@@ -1357,35 +869,11 @@ __device__ __forceinline__ void f4_bar() {  // this wave's LDS reads drained, DM
   asm volatile("" ::: "memory");
 }
 
-// Diagnostic build (ST, vd_attention_select(9)): workgroup 0's waves record s_memtime on both
-// sides of every barrier into LDS and copy them to f4_stamps at the end (vd_attention_stamps):
-// per phase, the work time (release -> arrival) and the barrier wait (arrival -> release).
-constexpr int F4_NST = 1024;  // stamps per wave: (tag << 56) | s_memtime
-__device__ uint64_t f4_stamps[F4_NW * F4_NST];
-
-template <bool UNITC, bool ST = false, int G1 = 0>
+template <bool UNITC>
 __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F4Dma& dma, bool issuer,
-                                        bool g0, bool one, int64_t skv, bf16x8 (&qf)[F4_QB][3], f32x16 (&oacc)[2][F4_QB],
+                                        bool g0, int64_t skv, bf16x8 (&qf)[F4_QB][3], f32x16 (&oacc)[2][F4_QB],
                                         uint32_t kl0, uint32_t v0l, uint32_t v1l, int hh, float c) {
-  int nst = 0;
-  const bool stw = ST && blockIdx.x == 0;
-  // tags: 1 barrier arrival, 2 release, 3 exps done, 4 V reads issued, 5 DMA issued, 6 PV(db 0)
-  // issued, 7 PV(db 1) issued, 8 QK^T issued, 9 decisions done
-  auto stamp = [&](uint64_t tag) {
-    if constexpr (ST) {
-      __builtin_amdgcn_sched_barrier(0);
-      const uint64_t tt = __builtin_amdgcn_s_memtime();
-      if (stw && (threadIdx.x & 63) == 0 && nst < F4_NST)
-        *(uint64_t*)(smem + F4_LDS + ((threadIdx.x >> 6) * F4_NST + nst) * 8) = (tag << 56) | (tt & ((1ull << 56) - 1));
-      ++nst;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  auto bar = [&]() {
-    stamp(1);
-    f4_bar();
-    stamp(2);
-  };
+  auto bar = [&]() { f4_bar(); };
   using C = F32Cfg<40>;
   constexpr int QB = F4_QB;
   constexpr float RESCALE = 4294967296.0f;        // 2^32
@@ -1472,22 +960,21 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   // ran earlier in this phase) — the same values at the same point of the tile order as flash32
   auto decide = [&](int t) {
     if (t == 0) {
-      // tile_max reads the QK^T accumulators through inline asm (v_max3), and hipcc pads no
-      // MFMA -> asm-reader wait states: wait out the last MFMA (8-pass XDL: 12 states) in one
-      // statement that takes EVERY accumulator as an operand, so no v_max3 can be scheduled
-      // ahead of it (a pin on one accumulator let the others' reads race their MFMAs: mu off
-      // by a bf16 step on ~half the rows, run to run)
-      static_assert(QB == 2, "the pin below names the four accumulators");
-      asm volatile("s_nop 7\n\ts_nop 7" : "+v"(s[0][0]), "+v"(s[0][1]), "+v"(s[1][0]), "+v"(s[1][1]));
+      // the tile-0 max with compiler-visible maxes (once per workgroup, so their canonicalising
+      // cost does not matter): hipcc sees the MFMA results being read and inserts the hazard
+      // wait states itself.  (The inline-asm v_max3 of tile_max hides that read from it; a
+      // hand-counted s_nop pad before it raced the MFMAs when the schedule moved, round 3.)
       float tm[QB];
-      bool need = true;
 #pragma unroll
       for (int qb = 0; qb < QB; ++qb) {
-        const float m = tile_max(s[0][qb], s[1][qb]);
-        tm[qb] = vmax2(m, partner32(m));
-        need |= (UNITC ? tm[qb] : tm[qb] * c) > F32_THR;
+        float m = s[0][qb][0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) m = __builtin_fmaxf(m, s[0][qb][i]);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m = __builtin_fmaxf(m, s[1][qb][i]);
+        tm[qb] = __builtin_fmaxf(m, partner32(m));
       }
-      if (__any(need)) {
+      {  // tile 0 always sets mu (flash32's t == 0 branch)
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb) {
           rescale(qb, (float)(__bf16)(mu[qb] + tm[qb]));
@@ -1543,43 +1030,27 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
     __builtin_amdgcn_sched_barrier(0);
     pv(0);
     __builtin_amdgcn_sched_barrier(0);
-    stamp(6);
     if (more) read_k(t + 1, 1);
     __builtin_amdgcn_sched_barrier(0);
     pv(1);
     __builtin_amdgcn_sched_barrier(0);
-    stamp(7);
     if (more) {
       qk(0);
       qk(1);
     }
-    stamp(8);
     __builtin_amdgcn_s_setprio(0);
     if (more) decide(t + 1);
-    stamp(9);
   };
   // tile u's DMA: issued at phase 2u-4 (u >= 2), waited for at the end of phase 2u-1
   auto issue = [&](int u) {
-    if (issuer && u < T) {
-      if (one) f4_issue<1>(dma, lds0, u, skv);
-      else f4_issue<G1 == 1 || G1 == 2 ? 3 : 2>(dma, lds0, u, skv);
-    }
-    stamp(5);
+    if (issuer && u < T) f4_issue<2>(dma, lds0, u, skv);
   };
   auto wait_tile = [&](int u) {
     if (issuer && u < T) {
-      if (u + 1 < T) {
-        if (one) f4_wait_vm<1>();
-        else f4_wait_vm<G1 == 1 || G1 == 2 ? 3 : 2>();
-      }
+      if (u + 1 < T) f4_wait_vm<2>();
       else f4_wait_vm<0>();
     }
   };
-  // G1 = 4 / 5: the second group issues at the start of its M phase instead of its V phase, so
-  // half the pieces go out in each of the two barrier intervals (the other group's M phase runs
-  // in the other interval) instead of all twelve in one
-  constexpr bool G1M = G1 == 4 || G1 == 5;
-
   // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere
   issue(0);
   issue(1);
@@ -1598,10 +1069,9 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   if (!g0) wait_tile(1);
   bar();
   for (int t = 0; t < T; ++t) {
-    if (!g0 && !G1M) issue(t + 3);
+    if (!g0) issue(t + 3);
     softmax();
     __builtin_amdgcn_sched_barrier(0);
-    stamp(3);
     read_v(t, 0);
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -1611,10 +1081,9 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb) f4_pin(pf[kb][s2][qb]);
       }
-    stamp(4);
     if (g0) wait_tile(t + 1);
     bar();
-    if (g0 || G1M) issue(t + 3);
+    if (g0) issue(t + 3);
     mphase(t);
     if (!g0) wait_tile(t + 2);
     bar();
@@ -1630,11 +1099,6 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
     }
     bad |= __any(over);
   }
-  if constexpr (ST) {
-    if (stw && (threadIdx.x & 63) == 0)
-      for (int i = 0; i < nst && i < F4_NST; ++i)
-        f4_stamps[(threadIdx.x >> 6) * F4_NST + i] = *(const uint64_t*)(smem + F4_LDS + ((threadIdx.x >> 6) * F4_NST + i) * 8);
-  }
   return bad;
 }
 
@@ -1642,7 +1106,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
 // jumped > ~100 (log2) past mu somewhere in the block it stores NaN flags instead, and flash32's
 // exact pass (flash32_kernel<..., FIX>, launched right after) recomputes the flagged quarters —
 // the exact loop inlined here as well would double the kernel's register pressure.
-template <bool UNITC, bool ST = false, int G1 = 0>
+template <bool UNITC>
 __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ q, int64_t ldq,
                                          const bf16_t* __restrict__ k, int64_t ldk, const bf16_t* __restrict__ v,
                                          int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads, int64_t sq,
@@ -1681,24 +1145,16 @@ __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ 
 
   // LDS-DMA pieces (waves 0-5)
   F4Dma dma;
-  // LDS-DMA issuers: waves 0-5 with two pieces each (G1 = 0), or one group's four waves with
-  // three each: G1 = 1 the second group (waves 4-7, in its softmax phase: measured 930 vs 805 us),
-  // G1 = 2 the first group (waves 0-3, in its PV / QK^T phase: 912 us), G1 = 3 all eight waves
-  // (waves 0-3 two pieces each in their M phase, waves 4-7 one each in their V phase)
-  // G1 = 5: all eight waves, group g's pieces 6g..6g+5 as 2, 2, 1, 1 over its waves
-  const bool issuer = G1 == 1 ? wave >= 4 : (G1 == 2 ? wave < 4 : (G1 == 3 || G1 == 5 ? true : wave < 6));
-  const bool one = (G1 == 3 && wave >= 4) || (G1 == 5 && (wave & 3) >= 2);
+  // LDS-DMA issuers: waves 0-5, two pieces each
+  const bool issuer = wave < 6;
   {
     const uint32_t ldkb = (uint32_t)ldk * 2, ldvb = (uint32_t)ldv * 2;
     const u32x4 rk = f4_rsrc(kb_ptr, (uint32_t)(skv - 1) * ldkb + 2 * D);
     const u32x4 rv = f4_rsrc(vb_ptr, (uint32_t)(skv - 1) * ldvb + 2 * D);
     const u32x4 r1 = f4_rsrc(f4_ones, 16);
 #pragma unroll
-    for (int i = 0; i < (G1 == 1 || G1 == 2 ? 3 : 2); ++i) {
-      const int p = G1 == 1 ? 3 * (wave - 4) + i
-                    : G1 == 2 ? 3 * wave + i
-                    : G1 == 5 ? 6 * (wave >> 2) + ((wave & 3) < 2 ? 2 * (wave & 3) + i : 2 + (wave & 3))
-                    : (G1 == 3 && wave >= 4 ? 8 + (wave - 4) : 2 * wave + i);
+    for (int i = 0; i < 2; ++i) {
+      const int p = 2 * wave + i;
       uint32_t row = lane, col = 0, step = 0, lds = 0;
       u32x4 rs = r1;
       if (p < 5) {
@@ -1726,7 +1182,7 @@ __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ 
                        (uint32_t)((4 * hh + qq) * 16);
 
   f32x16 oacc[2][QB];
-  if (__syncthreads_or(f4_loop<UNITC, ST, G1>(smem, lds0, dma, issuer, g0, one, skv, qf, oacc, kl0, v0l, v1l, hh, c))) {
+  if (__syncthreads_or(f4_loop<UNITC>(smem, lds0, dma, issuer, g0, skv, qf, oacc, kl0, v0l, v1l, hh, c))) {
     // a score jumped > ~100 (log2) past mu somewhere in the block: no output here; a NaN in
     // element (first query, d 0) of each 256-query quarter tells flash32's exact fix-up pass,
     // launched right after, to recompute that quarter
@@ -1777,109 +1233,52 @@ __device__ __forceinline__ bool f4_block(char* smem, const bf16_t* __restrict__ 
   return false;
 }
 
-template <bool UNITC, bool ST = false, int G1 = 0>
+template <bool UNITC>
 __global__ __launch_bounds__(F4_NT, 1) void flash40_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
     int64_t sq, int64_t skv, int64_t kv_div, float c, int out_f32) {
-  __shared__ __attribute__((aligned(1024))) char smem[F4_LDS + (ST ? F4_NW * F4_NST * 8 : 0)];
-  f4_block<UNITC, ST, G1>(smem, q, ldq, k, ldk, v, ldv, o, ldo, heads, sq, skv, kv_div, c, out_f32);
+  __shared__ __attribute__((aligned(1024))) char smem[F4_LDS];
+  f4_block<UNITC>(smem, q, ldq, k, ldk, v, ldv, o, ldo, heads, sq, skv, kv_div, c, out_f32);
 }
 
+// kernel (per call, test hook; 0 everywhere in the product): 0 = automatic — d = 40: flash40 from
+// 4 key tiles, flash32 below (and for its text cross-attention), other d: flash_attn_kernel;
+// 1 = flash_attn_kernel (16x16x32) for any d; 2 = flash32 (d = 40); 3 = flash40 wherever it
+// applies (d = 40, >= 2 key tiles).  A kernel that does not take the shape falls through to
+// the next one down.
 template <int D>
 int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                  void* o, int64_t ldo, int64_t batch, int heads, int64_t sq, int64_t skv,
-                 int64_t kv_div, float scale, hipStream_t s, int out_f32 = 0) {
+                 int64_t kv_div, float scale, hipStream_t s, int out_f32, int kernel) {
   const float c = scale * 1.4426950408889634f;
   if constexpr (D == 40) {
-    // flash40 (ping-pong, LDS-DMA ring): the default for the long self-attention (>= 2 key tiles)
-    if ((g_flash32 == 6 || g_flash32 == 8 || (g_flash32 == 1 && skv >= 256)) && skv >= 2 * KT &&
-        ((uintptr_t)o & 15) == 0 && ldo % (out_f32 ? 4 : 8) == 0) {
+    const bool oal = ((uintptr_t)o & 15) == 0 && ldo % (out_f32 ? 4 : 8) == 0;
+    // flash40 (ping-pong, LDS-DMA ring): the default for the long self-attention
+    if ((kernel == 3 || (kernel == 0 && skv >= 256)) && skv >= 2 * KT && oal) {
       const int64_t nblk = (sq + F4_QWG - 1) / F4_QWG * heads * batch;
       if (nblk > 0x7fffffff) return VD_EINVAL;
       const dim3 grid((unsigned)nblk);
       const dim3 fix((unsigned)((sq + 255) / 256 * heads * batch));
-      if (g_flash32 == 8) {  // diagnostic: stamped flash40 (unit c only)
-        if (c != 1.0f) return VD_EUNSUPPORTED;
-        hipLaunchKernelGGL((flash40_kernel<true, true>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,
-                           ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-      } else if (c == 1.0f && (g_f4_g1 == 4 || g_f4_g1 == 5)) {
-        if (g_f4_g1 == 4)
-          hipLaunchKernelGGL((flash40_kernel<true, false, 4>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
-                             (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
-                             out_f32);
-        else
-          hipLaunchKernelGGL((flash40_kernel<true, false, 5>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
-                             (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
-                             out_f32);
-        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-      } else if (c == 1.0f && g_f4_g1 == 3) {
-        hipLaunchKernelGGL((flash40_kernel<true, false, 3>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
-                           out_f32);
-        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-      } else if (c == 1.0f && g_f4_g1 == 2) {
-        hipLaunchKernelGGL((flash40_kernel<true, false, 2>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
-                           out_f32);
-        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-      } else if (c == 1.0f && g_f4_g1 == 1) {
-        hipLaunchKernelGGL((flash40_kernel<true, false, 1>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
-                           out_f32);
-        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-      } else if (c == 1.0f) {
+      if (c == 1.0f) {
         hipLaunchKernelGGL((flash40_kernel<true>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,
                            ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-        hipLaunchKernelGGL((flash32_kernel<D, true, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+        hipLaunchKernelGGL((flash32_kernel<D, true, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                            (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
       } else {
         hipLaunchKernelGGL((flash40_kernel<false>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,
                            ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-        hipLaunchKernelGGL((flash32_kernel<D, false, false, 2, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+        hipLaunchKernelGGL((flash32_kernel<D, false, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                            (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
       }
       return vd_launch_status();
     }
-    if (g_flash32 == 2 && !out_f32 && ((uintptr_t)o & 15) == 0 && ldo % 8 == 0) {  // ping-pong 8-wave kernel
-      const int64_t nblk = (sq + 511) / 512 * heads * batch;
-      if (nblk > 0x7fffffff) return VD_EINVAL;
-      const dim3 grid((unsigned)nblk);
-      if (c == 1.0f)
-        hipLaunchKernelGGL((flash32pp_kernel<D, true>), grid, dim3(2 * NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
-      else
-        hipLaunchKernelGGL((flash32pp_kernel<D, false>), grid, dim3(2 * NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c);
-      return vd_launch_status();
-    }
-    if (g_flash32 == 5 && ((uintptr_t)o & 15) == 0 && ldo % (out_f32 ? 4 : 8) == 0) {  // QB = 1, 4 waves/SIMD
-      const int64_t nblk = (sq + 127) / 128 * heads * batch;
-      if (nblk > 0x7fffffff) return VD_EINVAL;
-      const dim3 grid((unsigned)nblk);
-      if (c == 1.0f)
-        hipLaunchKernelGGL((flash32_kernel<D, true, false, 1>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-      else
-        hipLaunchKernelGGL((flash32_kernel<D, false, false, 1>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-      return vd_launch_status();
-    }
-    if (g_flash32 && ((uintptr_t)o & 15) == 0 && ldo % (out_f32 ? 4 : 8) == 0) {
+    if (kernel != 1 && oal) {  // flash32
       const int64_t nblk = (sq + 255) / 256 * heads * batch;
       if (nblk > 0x7fffffff) return VD_EINVAL;
       const dim3 grid((unsigned)nblk);
-      if (c == 1.0f && g_flash32 == 3)
-        hipLaunchKernelGGL((flash32_kernel<D, true, true>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-      else if (c == 1.0f)
-        hipLaunchKernelGGL((flash32_kernel<D, true>), grid, dim3(NT), g_flash32 == 4 ? 96 * 1024 : 0, s, (const bf16_t*)q, ldq,
+      if (c == 1.0f)
+        hipLaunchKernelGGL((flash32_kernel<D, true>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                            (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
       else
         hipLaunchKernelGGL((flash32_kernel<D, false>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
@@ -2349,69 +1748,8 @@ __global__ __launch_bounds__(NT) void softmax_rows_kernel(const float* __restric
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
-int g_temporal_valu = 0;  // vd_temporal_force_valu
 
 }  // namespace
-
-// Test/benchmark hook: route d = 40 to the 16x16x32 kernel instead of flash32.
-extern "C" int vd_attention_force_v1(int32_t on) {
-  g_flash32 = on ? 0 : 1;
-  return VD_OK;
-}
-
-// Test/benchmark hook: the d = 40 kernel — 0 = automatic, 1 = flash_attn (16x16x32),
-// 2 = flash32 (4-wave 32x32x16), 3 = flash32pp (8-wave pipeline), 4 = flash32 with the
-// intra-wave interleaved steady state (unit c only), 5 = flash32 held to one workgroup per
-// CU (96 KiB of dynamic LDS: one wave per SIMD — the occupancy probe of DESIGN.md §5), 6 =
-// flash32 with one 32-query block per wave (128 VGPRs, four waves per SIMD), 7 = flash40 (the
-// two-group ping-pong over an LDS-DMA ring, round 3) wherever it applies (>= 2 key tiles), 8 =
-// flash32 only (round 2's default; automatic = flash40 from 4 key tiles, flash32 below), 9 =
-// flash40's diagnostic build (barrier stamps of workgroup 0, vd_attention_stamps).
-extern int g_a5_var;  // attention_d512.hip
-extern int g_mq_ver, g_mq_any, g_mq_pw;  // motion.hip
-extern int g_fp8_ver;  // attention_fp8.hip
-
-extern "C" int vd_attention_select(int32_t kernel) {
-  if (kernel >= 35 && kernel <= 39) {  // fp8 attention: round 1's kernel (35) / round 3's (36; 37-39 its A/B forms)
-    g_fp8_ver = kernel - 34;
-    return VD_OK;
-  }
-  if (kernel >= 40 && kernel <= 42) {  // fused motion QKV-attention v2: positions per wave automatic (42) / 1 / 2
-    g_mq_pw = kernel == 42 ? 0 : kernel - 39;
-    return VD_OK;
-  }
-  if (kernel == 33 || kernel == 34) {  // fused motion QKV-attention at any grid size (33) / from 2 WGs per CU (34)
-    g_mq_any = kernel == 33;
-    return VD_OK;
-  }
-  if (kernel == 31 || kernel == 32) {  // fused motion QKV-attention: round 2's kernel (31) / round 3's (32)
-    g_mq_ver = kernel - 30;
-    return VD_OK;
-  }
-  if (kernel >= 25 && kernel <= 30) {  // flash40 DMA issuers: 25 waves 4-7, 26 waves 0-5 (default), 27 waves 0-3,
-    // 28 all eight (2 / 1 pieces); 29 = 26 with the second group issuing in its M phase, 30 = all eight
-    // waves (2, 2, 1, 1 per group), each group in its M phase
-    g_f4_g1 = kernel == 25 ? 1 : kernel == 27 ? 2 : kernel == 28 ? 3 : kernel == 29 ? 4 : kernel == 30 ? 5 : 0;
-    return VD_OK;
-  }
-  if (kernel >= 20 && kernel <= 22) {  // d = 512 (flash512): DMA placement A/B, 22 = ablation
-    g_a5_var = kernel - 20;
-    return VD_OK;
-  }
-  if (kernel < 0 || kernel > 9) return VD_EINVAL;
-  static const int map[10] = {1, 0, 7, 2, 3, 4, 5, 6, 7, 8};
-  g_flash32 = map[kernel];
-  return VD_OK;
-}
-
-// Diagnostic: copy the last stamped flash40 launch's barrier stamps (8 waves x 512 uint64
-// s_memtime values, wave-major) to dst (device memory, n <= 4096 values), stream-ordered.
-extern "C" int vd_attention_stamps(void* dst, int64_t n, vd_stream_t stream) {
-  VD_CHECK_ARG(dst && n > 0 && n <= F4_NW * F4_NST);
-  hipError_t e = hipMemcpyFromSymbolAsync(dst, HIP_SYMBOL(f4_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToDevice,
-                                          (hipStream_t)stream);
-  return e == hipSuccess ? VD_OK : (int)e;
-}
 
 // attention_d512.hip: the VAE mid-block attention (d = 512)
 int launch_flash512(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
@@ -2421,21 +1759,22 @@ int launch_flash512(const void* q, int64_t ldq, const void* k, int64_t ldk, cons
 static int attention_entry(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                             int64_t ldv, void* o, int64_t ldo, int64_t batch, int32_t heads,
                             int64_t sq, int64_t skv, int32_t d, int64_t kv_div, float scale,
-                            vd_stream_t stream, int out_f32) {
+                            vd_stream_t stream, int out_f32, int kernel) {
   VD_CHECK_ARG(q && k && v && o && al16(q) && al16(k) && al16(v) && ((uintptr_t)o & 7) == 0);
   VD_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0);
   if (out_f32) VD_CHECK_ARG(((uintptr_t)o & 15) == 0);
   VD_CHECK_ARG(batch > 0 && heads > 0 && sq > 0 && skv > 0 && kv_div > 0 && batch % kv_div == 0);
   VD_CHECK_ARG(batch <= 65535 && heads <= 65535);
   VD_CHECK_ARG(skv * ldk < 0x7fffffff && skv * ldv < 0x7fffffff);
+  VD_CHECK_ARG(kernel >= 0 && kernel <= 3);
   hipStream_t s = (hipStream_t)stream;
   switch (d) {
-    case 32: return launch_flash<32>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
-    case 40: return launch_flash<40>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
-    case 64: return launch_flash<64>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
-    case 80: return launch_flash<80>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
-    case 128: return launch_flash<128>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
-    case 160: return launch_flash<160>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
+    case 32: return launch_flash<32>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32, kernel);
+    case 40: return launch_flash<40>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32, kernel);
+    case 64: return launch_flash<64>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32, kernel);
+    case 80: return launch_flash<80>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32, kernel);
+    case 128: return launch_flash<128>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32, kernel);
+    case 160: return launch_flash<160>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32, kernel);
     case 512: return launch_flash512(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, kv_div, scale, s, out_f32);
     default: return VD_EUNSUPPORTED;
   }
@@ -2445,26 +1784,27 @@ extern "C" int vd_attention(const void* q, int64_t ldq, const void* k, int64_t l
                             int64_t ldv, void* o, int64_t ldo, int64_t batch, int32_t heads,
                             int64_t sq, int64_t skv, int32_t d, int64_t kv_div, float scale,
                             vd_stream_t stream) {
-  return attention_entry(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, d, kv_div, scale, stream, 0);
+  return attention_entry(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, d, kv_div, scale, stream, 0, 0);
 }
 
 extern "C" int vd_attention_f32(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                                 int64_t ldv, float* o, int64_t ldo, int64_t batch, int32_t heads,
                                 int64_t sq, int64_t skv, int32_t d, int64_t kv_div, float scale,
                                 vd_stream_t stream) {
-  return attention_entry(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, d, kv_div, scale, stream, 1);
+  return attention_entry(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, d, kv_div, scale, stream, 1, 0);
 }
 
-// Test/benchmark hook: on != 0 runs every temporal attention on the VALU kernel.
-extern "C" int vd_temporal_force_valu(int32_t on) {
-  g_temporal_valu = on;
-  return VD_OK;
+extern "C" int vd_attention_ex(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                               int64_t ldv, void* o, int64_t ldo, int64_t batch, int32_t heads, int64_t sq,
+                               int64_t skv, int32_t d, int64_t kv_div, float scale, int32_t out_f32,
+                               int32_t kernel, vd_stream_t stream) {
+  return attention_entry(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, sq, skv, d, kv_div, scale, stream,
+                         out_f32 != 0, kernel);
 }
 
-extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v, int64_t ld,
-                                     void* o, int64_t ldo, int64_t batch, int32_t frames,
-                                     int64_t positions, int32_t heads, int32_t d, float scale,
-                                     vd_stream_t stream) {
+static int temporal_entry(const void* q, const void* k, const void* v, int64_t ld, void* o, int64_t ldo,
+                          int64_t batch, int32_t frames, int64_t positions, int32_t heads, int32_t d, float scale,
+                          bool valu, vd_stream_t stream) {
   VD_CHECK_ARG(q && k && v && o && al16(q) && al16(k) && al16(v) && al16(o));
   VD_CHECK_ARG(ld % 8 == 0 && ldo % 8 == 0 && d % 8 == 0 && d > 0 && d <= 160);
   VD_CHECK_ARG(frames >= 1 && frames <= 32 && batch > 0 && positions > 0 && heads > 0);
@@ -2472,7 +1812,7 @@ extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v
   const unsigned grid = (unsigned)((items + 3) / 4);
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  if (!g_temporal_valu && (d == 40 || d == 64 || d == 80 || d == 160 || (d == 32 && frames <= 16)) && ld % 8 == 0 &&
+  if (!valu && (d == 40 || d == 64 || d == 80 || d == 160 || (d == 32 && frames <= 16)) && ld % 8 == 0 &&
       ldo % 4 == 0) {
     const int64_t g = (items + 3) / 4;
     const unsigned grid2 = (unsigned)(g < 8192 ? g : 8192);
@@ -2514,6 +1854,20 @@ extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v
   return vd_launch_status();
 }
 
+extern "C" int vd_temporal_attention(const void* q, const void* k, const void* v, int64_t ld,
+                                     void* o, int64_t ldo, int64_t batch, int32_t frames,
+                                     int64_t positions, int32_t heads, int32_t d, float scale,
+                                     vd_stream_t stream) {
+  return temporal_entry(q, k, v, ld, o, ldo, batch, frames, positions, heads, d, scale, false, stream);
+}
+
+extern "C" int vd_temporal_attention_valu(const void* q, const void* k, const void* v, int64_t ld,
+                                          void* o, int64_t ldo, int64_t batch, int32_t frames,
+                                          int64_t positions, int32_t heads, int32_t d, float scale,
+                                          vd_stream_t stream) {
+  return temporal_entry(q, k, v, ld, o, ldo, batch, frames, positions, heads, d, scale, true, stream);
+}
+
 extern "C" int vd_temporal_attention_kv(const void* q, int64_t ldq, const void* k, const void* v, int64_t ldkv,
                                         void* o, int64_t ldo, int64_t batch, int32_t qframes, int32_t kframes,
                                         int64_t positions, int32_t heads, int32_t d, float scale,
@@ -2546,9 +1900,6 @@ extern "C" int vd_temporal_attention_rope(const void* q, const void* k, const vo
   VD_CHECK_ARG(q && k && v && o && al16(q) && al16(k) && al16(v) && al16(o));
   VD_CHECK_ARG(ld % 8 == 0 && ldo % 4 == 0 && d == 64 && theta > 1.f);
   VD_CHECK_ARG(frames >= 17 && frames <= 32 && batch > 0 && positions > 0 && heads > 0);
-  // the fused form exists only on the MFMA kernel: under the force-VALU hook the caller
-  // runs vd_rope_qk + vd_temporal_attention (the VALU kernel) instead
-  if (g_temporal_valu) return VD_EUNSUPPORTED;
   const int64_t g = (batch * positions * heads + 3) / 4;
   hipLaunchKernelGGL((temporal_mfma32_kernel<64, true>), dim3((unsigned)(g < 8192 ? g : 8192)), dim3(NT), 0,
                      (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, ld, (bf16_t*)o, ldo,

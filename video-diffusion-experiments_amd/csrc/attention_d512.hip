@@ -75,12 +75,11 @@ __device__ __forceinline__ float a5_partner(float x) {  // the value of lane l ^
   return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
 }
 
-// PD: LDS fragment reads issued PD MFMAs ahead; DV (A/B): 1 = K and V one tile ahead in 2 + 2
-// slots (the default), 0 = K two tiles ahead in a 3-slot ring and V one ahead (measured 15 %
-// SLOWER: 608 vs 529 us at 16 x 4096, tools/vae_attn_dma.py), 2 = no DMA after the first tile
-// (ablation only: wrong results; 439 us — the LDS-DMA issue, ~60 cycles per 1 KiB piece and 16
-// pieces per wave per tile, is the kernel's largest non-MFMA cost)
-template <bool RAGGED, int PD, int DV = 0>
+// PD: LDS fragment reads issued PD MFMAs ahead.  K and V stream one tile ahead in 2 + 2 slots (a
+// 3-slot K ring two tiles ahead measured 15 % slower, 608 vs 529 us at 16 x 4096; a no-DMA
+// ablation ran 439 us — the LDS-DMA issue, ~60 cycles per 1 KiB piece and 16 pieces per wave
+// per tile, is the kernel's largest non-MFMA cost; profiles/r03h_flash512_dma_ab.txt)
+template <bool RAGGED, int PD>
 __global__ __launch_bounds__(A5_NT, 1) void flash512_kernel(const bf16_t* __restrict__ q, int64_t ldq,
                                                             const bf16_t* __restrict__ k, int64_t ldk,
                                                             const bf16_t* __restrict__ v, int64_t ldv,
@@ -108,10 +107,9 @@ __global__ __launch_bounds__(A5_NT, 1) void flash512_kernel(const bf16_t* __rest
   const uint32_t ldkb = (uint32_t)ldk * 2, ldvb = (uint32_t)ldv * 2;
   const u32x4_5 rk = a5_rsrc(kb_ptr, (uint32_t)(skv - 1) * ldkb + A5_ROW);
   const u32x4_5 rv = a5_rsrc(vb_ptr, (uint32_t)(skv - 1) * ldvb + A5_ROW);
-  // LDS slots of 32 KiB: DV 0 (default) K(t) in slot t % 3 (0 / 32 / 64 KiB) and V(t) in slot
-  // 3 + (t & 1) (96 / 128 KiB): K streams two tiles ahead, V one; DV 1 / 2: two slots each
-  auto ks_off = [&](int t) -> uint32_t { return (uint32_t)(DV == 0 ? t % 3 : (t & 1)) * A5_TILE; };
-  auto vs_off = [&](int t) -> uint32_t { return (uint32_t)(DV == 0 ? 3 + (t & 1) : 2 + (t & 1)) * A5_TILE; };
+  // LDS slots of 32 KiB: K(t) in slot t & 1, V(t) in slot 2 + (t & 1)
+  auto ks_off = [&](int t) -> uint32_t { return (uint32_t)(t & 1) * A5_TILE; };
+  auto vs_off = [&](int t) -> uint32_t { return (uint32_t)(2 + (t & 1)) * A5_TILE; };
   auto issue_k = [&](int t) {  // rows past skv: every byte out of the buffer's range -> zeros
     const uint32_t key0 = (uint32_t)t * A5_KT, kl = lds0 + ks_off(t);
 #pragma unroll
@@ -269,34 +267,18 @@ __global__ __launch_bounds__(A5_NT, 1) void flash512_kernel(const bf16_t* __rest
       for (int i = 0; i < 16; ++i) oacc[db][i] = 0.f;
     lsum = 0.f;
     sync();  // (the exact rerun's max sweep may still be reading K slot 0 in other waves)
-    if (DV == 0) {
-      // step t: K(t), V(t) landed (only K(t+1) may still fly); DMA V(t+1), then K(t+2)
-      issue_v(0);
-      issue_k(0);
-      if (T > 1) issue_k(1);
-      for (int t = 0; t < T; ++t) {
-        sync(t + 1 < T);
-        if (t + 1 < T) issue_v(t + 1);
-        if (t + 2 < T) issue_k(t + 2);
-        const f32x16 s = qk(kslot(t), t, -1);
-        bf16x8 pf[2];
-        softmax(s, fast, t == 0, pf);
-        pv(vslot(t), pf);
+    issue_k(0);
+    issue_v(0);
+    for (int t = 0; t < T; ++t) {
+      sync();
+      if (t + 1 < T) {
+        issue_k(t + 1);
+        issue_v(t + 1);
       }
-    } else {
-      issue_k(0);
-      issue_v(0);
-      for (int t = 0; t < T; ++t) {
-        sync();
-        if (t + 1 < T && DV == 1) {
-          issue_k(t + 1);
-          issue_v(t + 1);
-        }
-        const f32x16 s = qk(kslot(t), t, -1);
-        bf16x8 pf[2];
-        softmax(s, fast, t == 0, pf);
-        pv(vslot(t), pf);
-      }
+      const f32x16 s = qk(kslot(t), t, -1);
+      bf16x8 pf[2];
+      softmax(s, fast, t == 0, pf);
+      pv(vslot(t), pf);
     }
   };
 
@@ -354,8 +336,6 @@ __global__ __launch_bounds__(A5_NT, 1) void flash512_kernel(const bf16_t* __rest
 
 }  // namespace
 
-int g_a5_var = 1;  // DMA ring (vd_attention_select(20 + DV): A/B hook, 22 = ablation)
-
 // d = 512 (the VAE mid-block attention) for attention_entry (attention.hip).
 int launch_flash512(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv, void* o,
                     int64_t ldo, int64_t batch, int heads, int64_t sq, int64_t skv, int64_t kv_div, float scale,
@@ -369,17 +349,11 @@ int launch_flash512(const void* q, int64_t ldq, const void* k, int64_t ldk, cons
   if (nblk > 0x7fffffff) return VD_EINVAL;
   const float c = scale * 1.4426950408889634f;
   const dim3 grid((unsigned)nblk);
-#define A5_LAUNCH(R, V)                                                                                       \
-  hipLaunchKernelGGL((flash512_kernel<R, 3, V>), grid, dim3(A5_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,  \
+#define A5_LAUNCH(R)                                                                                          \
+  hipLaunchKernelGGL((flash512_kernel<R, 3>), grid, dim3(A5_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,  \
                      ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32)
-  const bool ragged = skv % A5_KT != 0;
-  if (g_a5_var == 1) {
-    if (ragged) A5_LAUNCH(true, 1); else A5_LAUNCH(false, 1);
-  } else if (g_a5_var == 2) {
-    if (ragged) A5_LAUNCH(true, 2); else A5_LAUNCH(false, 2);
-  } else {
-    if (ragged) A5_LAUNCH(true, 0); else A5_LAUNCH(false, 0);
-  }
+  if (skv % A5_KT != 0) A5_LAUNCH(true);
+  else A5_LAUNCH(false);
 #undef A5_LAUNCH
   return vd_launch_status();
 }

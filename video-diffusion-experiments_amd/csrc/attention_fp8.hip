@@ -326,11 +326,13 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_kernel(
 // K and V^T rows of 64 B XOR-swizzled on the source chunk, conflict-free b128 reads; the 64
 // per-key scale bytes by one buffer_load_ubyte ... lds, one dword each), five tiles in flight behind counted
 // vmcnt waits; the running offset m moves only when a row max passes it by 8 (P <= 2^8 < 448:
-// no clamp; cdna_hip_programming.md T13).  A/B forms (tools/fp8_variants.py, DiT shape, rel-L2 vs
-// fp32 SDPA at S = 2304): v1 1.580 ms / 8.60 %; LAZY + row sum on the MFMA (an all-ones e4m3 A
-// operand against P) 1.389 ms / 8.93 %; LAZY + fp32 VALU row sum (the default, v = 4) 1.426 ms /
-// 8.78 %; eager offset + VALU sum (v1's arithmetic on the ring) 1.520 ms / 8.60 %.  The MFMA row
-// sum is faster but sums the e4m3-rounded P, which costs accuracy.
+// no clamp; cdna_hip_programming.md T13), and the row sum is an fp32 VALU sum of the unrounded P.
+// Measured forms (DiT shape, rel-L2 vs fp32 SDPA at S = 2304, profiles/r03l_fp8_variants.txt):
+// v1 1.580 ms / 8.60 %; lazy + row sum on the MFMA (an all-ones e4m3 A operand against P)
+// 1.389 ms / 8.93 %; lazy + fp32 VALU row sum (this kernel) 1.426 ms / 8.78 %; eager offset +
+// VALU sum 1.520 ms / 8.60 %.  The MFMA row sum is faster but sums the e4m3-rounded P, which
+// costs accuracy.  v1 (flash_fp8_kernel) stays as the path for shapes whose ring offsets do not
+// fit 32 bits.
 constexpr int F8S = 6;  // ring stages
 constexpr int F8_K = 0, F8_V = 4096, F8_KS = 8192, F8_STAGE = 8192 + 256;
 
@@ -375,7 +377,6 @@ __device__ __forceinline__ void f8_wait(int n) {  // s_waitcnt vmcnt(n), n in {0
 // physical 16-byte chunk of logical chunk c in a 64-byte row r of a K / V^T tile image
 __device__ __forceinline__ uint32_t f8_chunk(uint32_t r, uint32_t c) { return c ^ ((r >> 2) & 3); }
 
-template <bool LAZY, bool ONES>  // lazy offset (P <= 2^8) / row sum on the MFMA (A/B: both on by default)
 __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
     const uint8_t* __restrict__ q8, const uint8_t* __restrict__ k8, int64_t ld8,
     const uint8_t* __restrict__ qs, const uint8_t* __restrict__ ks, const uint8_t* __restrict__ vt8,
@@ -417,8 +418,6 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
   // Q^T fragment: d = 32 hh + j of this lane's query, and its scale
   const i32x8 qf = *(const i32x8*)(q8 + qrow * ld8 + h * FD + 32 * hh);
   const int qsc = qs[qrow * heads + h];
-  const i32x8 ones = {0x38383838, 0x38383838, 0x38383838, 0x38383838,
-                      0x38383838, 0x38383838, 0x38383838, 0x38383838};  // e4m3 1.0
   // per-lane LDS read offsets: K row 32 kb + r and V^T row 32 a + r, logical chunks 2 hh, 2 hh + 1
   uint32_t kro[2][2], vro[2][2];
 #pragma unroll
@@ -430,9 +429,9 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
       vro[x][j] = F8_V + row * 64 + 16u * f8_chunk(row, (uint32_t)(2 * hh + j));
     }
 
-  f32x16 ot[2], lacc;
+  f32x16 ot[2];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) { ot[0][i] = 0.f; ot[1][i] = 0.f; lacc[i] = 0.f; }
+  for (int i = 0; i < 16; ++i) { ot[0][i] = 0.f; ot[1][i] = 0.f; }
   float m = -INFINITY, lsum = 0.f;
   for (int t = 0; t < ntiles; ++t) {
     const int ahead = (ntiles - 1 - t) < (F8S - 2) ? (ntiles - 1 - t) : (F8S - 2);
@@ -467,13 +466,13 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
 #pragma unroll
       for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kb][i]);
     mt = fmaxf(mt, partner32f(mt)) * c;
-    if (LAZY ? __any(mt > m + 8.f) : mt > m) {  // lazy: wave-uniform; always on the first tile (m = -inf)
+    if (__any(mt > m + 8.f)) {  // lazy, wave-uniform; always on the first tile (m = -inf)
       const float mn = fmaxf(m, mt);
       const float alpha = __builtin_amdgcn_exp2f(m - mn);
       m = mn;
       lsum *= alpha;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { ot[0][i] *= alpha; ot[1][i] *= alpha; lacc[i] *= alpha; }
+      for (int i = 0; i < 16; ++i) { ot[0][i] *= alpha; ot[1][i] *= alpha; }
     }
     uint32_t pw[8];
 #pragma unroll
@@ -484,7 +483,7 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
         const float p1 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 1], c, -m));
         const float p2 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 2], c, -m));
         const float p3 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 3], c, -m));
-        if (!ONES) lsum += (p0 + p1) + (p2 + p3);
+        lsum += (p0 + p1) + (p2 + p3);
         int w = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, 0, false);
         pw[4 * kb + g] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(p2, p3, w, true);
       }
@@ -492,11 +491,9 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
 #pragma unroll
     for (int a = 0; a < 2; ++a)
       ot[a] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf[a], pf, ot[a], 0, 0, 0, vsc, 0, 127);
-    if (ONES) lacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones, pf, lacc, 0, 0, 0, 127, 0, 127);
   }
-  // ONES: every row of the ones-product is this query's row sum (over the e4m3 P); else the
-  // lane's fp32 partial over its 32 unrounded scores plus its partner's
-  const float inv = 1.0f / (ONES ? lacc[0] : lsum + partner32f(lsum));
+  // the lane's fp32 partial over its 32 unrounded scores plus its partner's
+  const float inv = 1.0f / (lsum + partner32f(lsum));
   if (qvalid) {
     bf16_t* orow = o + (b * sq + q0 + r) * ldo + h * FD;
 #pragma unroll
@@ -547,8 +544,6 @@ int quant_operands(const void* q, int64_t ldq, const void* k, int64_t ldk, const
 
 }  // namespace
 
-int g_fp8_ver = 4;  // 1: round 1's flash_fp8_kernel; 2-5: round 3's forms (vd_attention_select(34 + v): A/B hook)
-
 extern "C" int vd_attention_fp8_quant(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                                       int64_t ldv, int64_t batch, int32_t heads, int64_t sq, int64_t skv,
                                       int32_t d, void* q8, void* k8, int64_t ld8, void* vt8, void* qs,
@@ -577,15 +572,10 @@ extern "C" int vd_attention_fp8(const void* q8, const void* k8, int64_t ld8, con
   VD_CHECK_ARG(nblk < 0x7fffffff);
   const float c = scale * 1.4426950408889634f;
   const bool v2ok = skv * ld8 < 0x7fffffff && skv * FD < 0x7fffffff && skv * heads < 0x7fffffff;
-#define F8V2(L, O)                                                                                               \
-  hipLaunchKernelGGL((flash_fp8_v2_kernel<L, O>), dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream,        \
-                     (const uint8_t*)q8, (const uint8_t*)k8, ld8, (const uint8_t*)qs, (const uint8_t*)ks,        \
-                     (const uint8_t*)vt8, (const uint8_t*)vs, (bf16_t*)o, ldo, (int)heads, sq, skv, c)
-  if (v2ok && g_fp8_ver == 2) F8V2(true, true);
-  else if (v2ok && g_fp8_ver == 3) F8V2(false, true);
-  else if (v2ok && g_fp8_ver == 4) F8V2(true, false);
-  else if (v2ok && g_fp8_ver == 5) F8V2(false, false);
-#undef F8V2
+  if (v2ok)
+    hipLaunchKernelGGL(flash_fp8_v2_kernel, dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream,
+                       (const uint8_t*)q8, (const uint8_t*)k8, ld8, (const uint8_t*)qs, (const uint8_t*)ks,
+                       (const uint8_t*)vt8, (const uint8_t*)vs, (bf16_t*)o, ldo, (int)heads, sq, skv, c);
   else
     hipLaunchKernelGGL(flash_fp8_kernel, dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream, (const uint8_t*)q8,
                        (const uint8_t*)k8, ld8, (const uint8_t*)qs, (const uint8_t*)ks, (const uint8_t*)vt8,

@@ -43,8 +43,9 @@ struct Div {
 
 template <int MB, int NB>
 __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], int mbase,
-                                              int nbase, int lane) {
-  // acc[a][b][j] = C[m = mbase + b*16 + fr][n = nbase + a*16 + 4*fq + j]  (the wave's sub-tile)
+                                              int nbase, int lane, int nodd = -1) {
+  // acc[a][b][j] = C[m = mbase + b*16 + fr][n = nbase + a*16 + 4*fq + j]  (the wave's sub-tile);
+  // nodd >= 0 moves the odd last block (NB odd) to columns nodd .. nodd + 15 instead
   // All offsets fit 32 bits (M*ldc < 2^31 is checked on the host).
   const int M = (int)d.M, N = (int)d.N;
   const int fr = lane & 15, fq = lane >> 4;
@@ -200,7 +201,7 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
 #pragma unroll
   for (int a = 0; a < NB; ++a) {  // narrow path (or, when wide, the odd last block)
     if (wide && a + 1 < NB) continue;
-    const int n = nw + a * 16 + 4 * fq;
+    const int n = (nodd >= 0 && a == NB - 1 ? nodd : nw + a * 16) + 4 * fq;
     if (n >= N) continue;
     float bv[4] = {0, 0, 0, 0};
     if (d.bias) {
@@ -400,13 +401,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
 // outside the image are zero-filled by the buffer range check (voffset beyond
 // num_records returns 0).  Per-tile address work: one integer add per load.
 constexpr int G2_BM = 256, G2_NT = 512, G2_STAGES = 3;
-int g_num_cus = 256;  // MI355X; refreshed from the device on first use
-// v2 fragment-read order (A/B: vd_gemm_select_path 12/13/14 force 0/2/1); -1 = the default, 2:
-// k-step 0's reads ahead, k-step 1's interleaved with k-step 0's MFMAs (tools/ab_step.py pf:
-// 52.79 vs 53.50 ms/step for round 1's order, 53.11 all-ahead; profiles/r02f_fragment_order.txt)
-int g_g2_pf = -1;
-int g_g4_roll = 1;  // v5 W-fragment rolling window (0: round 1's halves, vd_gemm_select_path(16), A/B)
-int g_g2_old = 0;     // 1: v6 with the round-1 fragment-read order (vd_gemm_select_path(12))
+int g_num_cus = 256;  // MI355X; the device's CU count, read once per process (read_num_cus)
 constexpr uint32_t G2_OOB = 0x80000000u;
 
 template <int BN>
@@ -439,70 +434,12 @@ __device__ __forceinline__ void wait_vm() {
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
-// Epilogue of the 32x32x16 form (MF = 1): acc[a][4 g + i] = C[m = mbase + (lane & 31)]
-// [n = nbase + 32 a + 8 g + 4 (lane >> 5) + i] — one output row per lane, its 8-column groups
-// split across the half-waves.  bias / row bias / activation / residual in fp32 in that layout
-// (8-B residual loads), then bf16 packs and one v_permlane32_swap per dword of a group pair
-// (cdna_hip_programming.md T21), so each lane stores 16 contiguous bytes: lanes 0-31 columns
-// 16 h .. 16 h + 7, lanes 32-63 the next 8.  fp32 output: 16-B stores in the MFMA layout.
-// Requires (host plan) N % 32 == 0, ldc % 8 == 0, a 16-B aligned output, no GEGLU.
-template <int NB>
-__device__ __forceinline__ void gemm_epilogue32(const vd_gemm_desc& d, f32x16 (&acc)[NB], int mbase, int nbase,
-                                                int lane) {
-  const int M = (int)d.M, N = (int)d.N;
-  const int m = mbase + (lane & 31), hh = lane >> 5;
-  if (m >= M) return;
-  const float* rbrow = d.rowbias ? d.rowbias + (int64_t)Div((int)d.rb_div)(m) * d.ld_rb : nullptr;
-#pragma unroll
-  for (int a = 0; a < NB; ++a) {
-    const int n0 = nbase + 32 * a;
-    if (n0 >= N) continue;
-    float o[4][4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int n = n0 + 8 * g + 4 * hh;
-      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (d.bias) bv = *(const float4*)(d.bias + n);
-      o[g][0] = acc[a][4 * g] + bv.x; o[g][1] = acc[a][4 * g + 1] + bv.y;
-      o[g][2] = acc[a][4 * g + 2] + bv.z; o[g][3] = acc[a][4 * g + 3] + bv.w;
-      if (rbrow) {
-        const float4 t = *(const float4*)(rbrow + n);
-        o[g][0] += t.x; o[g][1] += t.y; o[g][2] += t.z; o[g][3] += t.w;
-      }
-      if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[g][j] = act_pw(d.act, o[g][j]);
-      }
-      if (d.res) {
-        const uint2 r = *(const uint2*)((const bf16_t*)d.res + (uint32_t)(m * (int)d.ld_res + n));
-        o[g][0] += bf_lo(r.x); o[g][1] += bf_hi(r.x); o[g][2] += bf_lo(r.y); o[g][3] += bf_hi(r.y);
-      }
-    }
-    if (d.out_f32) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *(float4*)((float*)d.out + (uint32_t)(m * (int)d.ldc + n0 + 8 * g + 4 * hh)) =
-            make_float4(o[g][0], o[g][1], o[g][2], o[g][3]);
-      continue;
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      uint32_t x0 = pack2(o[2 * h][0], o[2 * h][1]), x1 = pack2(o[2 * h][2], o[2 * h][3]);
-      uint32_t y0 = pack2(o[2 * h + 1][0], o[2 * h + 1][1]), y1 = pack2(o[2 * h + 1][2], o[2 * h + 1][3]);
-      const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
-      const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
-      *(uint4*)((bf16_t*)d.out + (uint32_t)(m * (int)d.ldc + n0 + 16 * h + 8 * hh)) =
-          make_uint4(s0[0], s1[0], s0[1], s1[1]);
-    }
-  }
-}
-
-// PF (fragment-read order, round 2): without a pin hipcc sinks each X fragment read to its 4
-// MFMAs behind an lgkmcnt(0) — 8 exposed LDS latencies per K-tile (PF = 0, round 1's order).
-// PF = 1 issues all 18 reads of the K-tile right after the barrier (sched_barrier), PF = 2 (the
-// default) issues k-step 0's 9 reads, then interleaves k-step 1's reads one per two of k-step
-// 0's MFMAs (sched_group_barrier), so the MFMA chain waits on counted lgkmcnt only.
-template <int BN, int MODE, int PF = 1, int MF = 0, bool FD = true>
+// Fragment-read order (round 2): without a pin hipcc sinks each X fragment read to its 4 MFMAs
+// behind an lgkmcnt(0) — 8 exposed LDS latencies per K-tile.  k-step 0's 9 reads issue right
+// after the barrier (sched_barrier), then k-step 1's reads interleave one per two of k-step 0's
+// MFMAs (sched_group_barrier), so the MFMA chain waits on counted lgkmcnt only (52.79 vs 53.50
+// ms/step for the unpinned order, 53.11 with all reads ahead; profiles/r02f_fragment_order.txt).
+template <int BN, int MODE>
 __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                          uint32_t a1_bytes, uint32_t w_bytes,
                                                          int split) {
@@ -530,13 +467,6 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
 
   const int rb = lane >> 3;                                  // row within the 8-row DMA block
   const uint32_t lc16 = (uint32_t)(((lane & 7) ^ rb) * 16);  // swizzled source chunk (bytes)
-  // MF = 1: the image's XOR is (row >> 1) & 7 (conflict-free 32-row fragment reads), which for
-  // row = 8 p + rb depends on the piece parity p & 1: A pieces wid * 4 + j (parity j & 1), W
-  // pieces 8 j + wid (parity wid & 1)
-  auto lcs = [&](int par) -> uint32_t {
-    return MF ? (uint32_t)(((lane & 7) ^ ((4 * par + (rb >> 1)) & 7)) * 16) : lc16;
-  };
-  const uint32_t lcb = lcs(wid & 1);
   const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)d.a0, 0, a0_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ra1 =
       __builtin_amdgcn_make_buffer_rsrc((void*)(d.a1 ? d.a1 : d.a0), 0, d.a1 ? a1_bytes : 0, 0x00020000);
@@ -569,17 +499,17 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     for (int j = 0; j < C::NBMAX; ++j) {
       int64_t n = n0 + (j * 8 + wid) * 8 + rb;
       n = n < N ? n : N - 1;
-      boff[j] = (uint32_t)(n * d.ldw * 2) + lcb;
+      boff[j] = (uint32_t)(n * d.ldw * 2) + lc16;
     }
     if constexpr (MODE == VD_A_DENSE) {
 #pragma unroll
       for (int j = 0; j < C::NA; ++j) {
         int64_t m = m0 + (wid * 4 + j) * 8 + rb;
         m = m < M ? m : M - 1;
-        aoff0[j] = (uint32_t)(m * d.lda0 * 2) + lcs(j & 1);
-        aoff1[j] = (uint32_t)(m * d.lda1 * 2) + lcs(j & 1);
+        aoff0[j] = (uint32_t)(m * d.lda0 * 2) + lc16;
+        aoff1[j] = (uint32_t)(m * d.lda1 * 2) + lc16;
       }
-    } else if constexpr (FD) {  // 32-bit rows, shifts for power-of-two sizes (round 3)
+    } else {  // 32-bit rows, shifts for power-of-two sizes (round 3; int64 divisions: -2-3 %)
       const int hw = d.h_out * d.w_out;
       const Div dhw(hw), dfr(d.frames_out), dw(d.w_out);
 #pragma unroll
@@ -592,20 +522,6 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
         pimg[j] = vid * d.frames_in + pfr[j];
         const int p = m - img * hw;
         poh[j] = dw(p);
-        pow_[j] = p - poh[j] * d.w_out;
-      }
-    } else {  // round 2's form (int64 rows, divisions): the A/B arm
-      const int hw = d.h_out * d.w_out;
-#pragma unroll
-      for (int j = 0; j < C::NA; ++j) {
-        int64_t m = m0 + (wid * 4 + j) * 8 + rb;
-        m = m < M ? m : M - 1;
-        const int img = (int)(m / hw);
-        const int vid = img / d.frames_out;
-        pfr[j] = img - vid * d.frames_out + d.t_off - d.kt / 2;
-        pimg[j] = vid * d.frames_in + pfr[j];
-        const int p = (int)(m - (int64_t)img * hw);
-        poh[j] = p / d.w_out;
         pow_[j] = p - poh[j] * d.w_out;
       }
     }
@@ -640,8 +556,8 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
           const bool ok = ((uint32_t)ih < (uint32_t)hgrid) & ((uint32_t)iw < (uint32_t)wgrid) &
                           ((uint32_t)fin < (uint32_t)d.frames_in);
           const uint32_t pix = (uint32_t)(((pimg[j] + dt) * d.h_in + (ih >> d.upsample)) * d.w_in + (iw >> d.upsample));
-          aoff0[j] = ok ? pix * (uint32_t)(d.lda0 * 2) + lcs(j & 1) : G2_OOB;
-          aoff1[j] = ok ? pix * (uint32_t)(d.lda1 * 2) + lcs(j & 1) : G2_OOB;
+          aoff0[j] = ok ? pix * (uint32_t)(d.lda0 * 2) + lc16 : G2_OOB;
+          aoff1[j] = ok ? pix * (uint32_t)(d.lda1 * 2) + lc16 : G2_OOB;
         }
       }
       const bool s0 = c_ci < (int)d.k0;
@@ -660,21 +576,11 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     if (++ikt == ikt1 && (iu += G) < units) setup_unit(iu);
   };
 
-  f32x4 acc[MF ? 1 : C::NB][MF ? 1 : C::MB];
+  f32x4 acc[C::NB][C::MB];
 #pragma unroll
-  for (int a = 0; a < (MF ? 1 : C::NB); ++a)
+  for (int a = 0; a < C::NB; ++a)
 #pragma unroll
-    for (int b = 0; b < (MF ? 1 : C::MB); ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // MF = 1: 8 waves as 8(M) x 1(N), each 32 rows x BN columns in BN / 32 accumulators of
-  // v_mfma_f32_32x32x16_bf16 — half the MFMA instructions of the 16x16x32 form for the same
-  // work (an MFMA holds the SIMD's vector issue for 8 cycles either way), 24 fragment reads
-  // per K-tile instead of 18
-  constexpr int NB32 = BN / 32;
-  f32x16 acc32[MF ? NB32 : 1];
-#pragma unroll
-  for (int a = 0; a < (MF ? NB32 : 1); ++a)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc32[a][i] = 0.f;
+    for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // total k-tiles this workgroup streams
   int n_it = 0;
@@ -690,21 +596,19 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
   // per-lane LDS byte offsets of the first fragment of each operand for k-step
   // ks (rows differ by multiples of 16 between fragments, so the (row & 7) XOR
   // swizzle is the same and fragment a/b adds a constant)
-  uint32_t wlane[BK / 32], xlane[BK / 32];
+  // Column map (BN = 160, 5 blocks per wave): wave wn owns the 64 columns 64 wn .. 64 wn + 63 as
+  // two 16-B-store pairs, and the odd block at 128 + 16 wn, so every bf16 store segment is 64-B
+  // aligned (an 80-column wave tile put wave 1's pairs across 64-B granules and wrote 1.6x,
+  // profiles/r03w_gemm_traffic.txt). Rows stay 16-multiples apart: the LDS XOR is unchanged.
+  constexpr bool ODDMAP = (C::NB % 2) == 1 && C::NB > 1;
+  const int wcb = ODDMAP ? wn * 16 * (C::NB - 1) : wn * (BN / 2);  // the wave's first column
+  const int wodd = ODDMAP ? 32 * (C::NB - 1) + 16 * wn : wcb + 16 * (C::NB - 1);  // odd block's column
+  uint32_t wlane[BK / 32], xlane[BK / 32], wlodd[BK / 32];
 #pragma unroll
   for (int ks = 0; ks < BK / 32; ++ks) {
-    wlane[ks] = C::A_BYTES + 2 * lds_off(wn * (BN / 2) + (lane & 15), ks * 4 + (lane >> 4));
+    wlane[ks] = C::A_BYTES + 2 * lds_off(wcb + (lane & 15), ks * 4 + (lane >> 4));
+    wlodd[ks] = wlane[ks] + (uint32_t)(wodd - wcb) * BK * 2;
     xlane[ks] = 2 * lds_off(wm * 64 + (lane & 15), ks * 4 + (lane >> 4));
-  }
-  // MF = 1 fragment offsets, k-steps of 16: row r, chunk 2 ks + lane / 32, XOR (r >> 1) & 7
-  // (W block a adds 32 a rows = 4096 a bytes, the XOR unchanged)
-  uint32_t w32[BK / 16], x32[BK / 16];
-#pragma unroll
-  for (int ks = 0; ks < BK / 16; ++ks) {
-    const int r = lane & 31, c = 2 * ks + (lane >> 5);
-    w32[ks] = C::A_BYTES + (uint32_t)(r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-    const int rx = 32 * wid + r;
-    x32[ks] = (uint32_t)(rx * 128 + ((c ^ ((rx >> 1) & 7)) << 4));
   }
   // ---- compute cursor
   int cu = u_begin, ckt, ckt1;
@@ -723,28 +627,16 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's DMA for `it` landed; stage (it-1)%3 fully read
     const char* sbase = smem + stage * C::STAGE;
-    if constexpr (MF) {
-      bf16x8 wf[BK / 16][NB32], xf[BK / 16];
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        xf[ks] = *(const bf16x8*)(sbase + x32[ks]);
-#pragma unroll
-        for (int a = 0; a < NB32; ++a) wf[ks][a] = *(const bf16x8*)(sbase + w32[ks] + a * 4096);
-      }
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks)
-#pragma unroll
-        for (int a = 0; a < NB32; ++a)
-          acc32[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks][a], xf[ks], acc32[a], 0, 0, 0);
-    } else if constexpr (PF != 0) {
+    {
       bf16x8 wf[BK / 32][C::NB], xf[BK / 32][C::MB];
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks) {
 #pragma unroll
         for (int b = 0; b < C::MB; ++b) xf[ks][b] = *(const bf16x8*)(sbase + xlane[ks] + b * 16 * BK * 2);
 #pragma unroll
-        for (int a = 0; a < C::NB; ++a) wf[ks][a] = *(const bf16x8*)(sbase + wlane[ks] + a * 16 * BK * 2);
-        if (PF == 1 || ks == 0) __builtin_amdgcn_sched_barrier(0);
+        for (int a = 0; a < C::NB; ++a)
+          wf[ks][a] = *(const bf16x8*)(sbase + (a == C::NB - 1 ? wlodd[ks] : wlane[ks] + a * 16 * BK * 2));
+        if (ks == 0) __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks)
@@ -753,7 +645,7 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
 #pragma unroll
           for (int b = 0; b < C::MB; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][a], xf[ks][b], acc[a][b], 0, 0, 0);
-      if constexpr (PF == 2) {  // k-step 1's reads one per two of k-step 0's MFMAs
+      {  // k-step 1's reads one per two of k-step 0's MFMAs
         constexpr int NR = C::MB + C::NB, NM = 2 * C::MB * C::NB;
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
@@ -762,49 +654,18 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
         }
         __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
       }
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
-        bf16x8 wf[C::NB], xf[C::MB];
-        const char* wp = sbase + wlane[ks];
-        const char* xp = sbase + xlane[ks];
-#pragma unroll
-        for (int a = 0; a < C::NB; ++a) wf[a] = *(const bf16x8*)(wp + a * 16 * BK * 2);
-#pragma unroll
-        for (int b = 0; b < C::MB; ++b) xf[b] = *(const bf16x8*)(xp + b * 16 * BK * 2);
-#pragma unroll
-        for (int a = 0; a < C::NB; ++a)
-#pragma unroll
-          for (int b = 0; b < C::MB; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][b], 0, 0, 0);
-      }
     }
     if (++ckt == ckt1) {  // unit finished: epilogue (its memory ops precede the next DMA)
       const int tile = cu / split, sp = cu % split;
       const int64_t m0 = (int64_t)(tile / tiles_n) * G2_BM, n0 = (int64_t)(tile % tiles_n) * BN;
-      if constexpr (MF) {
-        if (split == 1) {
-          gemm_epilogue32<NB32>(d, acc32, (int)m0 + 32 * wid, (int)n0, lane);
-        } else {  // split-K slab in the 32x32 layout
-          float* slab = (float*)d.ws + (int64_t)sp * M * N;
-          const int64_t m = m0 + 32 * wid + (lane & 31);
-#pragma unroll
-          for (int a = 0; a < NB32; ++a)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const int64_t n = n0 + 32 * a + 8 * g + 4 * (lane >> 5);
-              if (m < M && n < N)
-                *(float4*)(slab + m * N + n) =
-                    make_float4(acc32[a][4 * g], acc32[a][4 * g + 1], acc32[a][4 * g + 2], acc32[a][4 * g + 3]);
-            }
-        }
-      } else if (split == 1) {
-        gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::MB * 16, (int)n0 + wn * (BN / 2), lane);
+      if (split == 1) {
+        gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::MB * 16, (int)n0 + wcb, lane,
+                                    ODDMAP ? (int)n0 + wodd : -1);
       } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
         float* slab = (float*)d.ws + (int64_t)sp * M * N;
 #pragma unroll
         for (int a = 0; a < C::NB; ++a) {
-          const int64_t n = n0 + wn * (BN / 2) + a * 16 + 4 * fq;
+          const int64_t n = n0 + (a == C::NB - 1 ? wodd : wcb + a * 16) + 4 * fq;
           if (n >= N) continue;
 #pragma unroll
           for (int b = 0; b < C::MB; ++b) {
@@ -815,13 +676,9 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
         }
       }
 #pragma unroll
-      for (int a = 0; a < (MF ? 1 : C::NB); ++a)
+      for (int a = 0; a < C::NB; ++a)
 #pragma unroll
-        for (int b = 0; b < (MF ? 1 : C::MB); ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int a = 0; a < (MF ? NB32 : 1); ++a)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc32[a][i] = 0.f;
+        for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
       if ((cu += G) < units) unit_kr(cu, ckt, ckt1);
     }
     if (it + 2 < n_it) issue(stage == 0 ? 2 : stage - 1);
@@ -971,7 +828,6 @@ constexpr int G3_STAGE = 2 * G3_A_BYTES;       // A + W: 64 KiB
 // global bias loads made hipcc wait vmcnt(0) at every unit boundary — draining the next
 // unit's two K-tiles of DMA under the epilogue (20 units per CU at the L1 GEGLU).
 constexpr int G3_BIAS_N = 5120;
-int g_g3_fast = 1;  // 0: gemm_epilogue everywhere (vd_gemm_select_path(15), A/B only)
 
 struct G3Cursor {  // a position (unit, local K-tile) in the workgroup's flat K-tile stream
   int u, t, kt0, nk, m0, n0;
@@ -1376,7 +1232,7 @@ __device__ __forceinline__ void epi_ln(const vd_gemm_desc& d, f32x4 (&acc)[NB][M
   }
 }
 
-template <int BN, int WM, int WN, int STAGES, int MODE, bool LN = false, bool ROLL = true>
+template <int BN, int WM, int WN, int STAGES, int MODE, bool LN = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_waves_per_eu(2))) void gemm4_kernel(
     const vd_gemm_desc d, uint32_t a0_bytes, uint32_t a1_bytes, uint32_t w_bytes, int split) {
   using C = G4<BN, WM, WN, STAGES>;
@@ -1578,7 +1434,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
           for (int a = 0; a < C::NB; ++a)
             acc[a][4 * h + b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][4 * h + b], 0, 0, 0);
       }
-    } else if constexpr (ROLL) {
+    } else {
       // X once; W fragments two ahead in a rolling window (round 2): each W read issues under the
       // MFMAs of the fragment two before it, pinned by sched_group_barrier — the halves below let
       // hipcc wait lgkmcnt on every pair right before its MFMAs
@@ -1601,24 +1457,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
       for (int a = 0; a < C::NB; ++a) {
         if (a + 2 < C::NB) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, C::MB, 0);
-      }
-    } else {
-      // X once, W in two halves
-      constexpr int HN = (C::NB + 1) / 2;
-      bf16x8 xf[C::MB], wf[HN];
-#pragma unroll
-      for (int b = 0; b < C::MB; ++b) xf[b] = *(const bf16x8*)(sbase + xlane + b * 1024);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int a = 0; a < HN; ++a)
-          if (h * HN + a < C::NB) wf[a] = *(const bf16x8*)(sbase + wlane + (h * HN + a) * 1024);
-#pragma unroll
-        for (int a = 0; a < HN; ++a)
-          if (h * HN + a < C::NB)
-#pragma unroll
-            for (int b = 0; b < C::MB; ++b)
-              acc[h * HN + a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[h * HN + a][b], 0, 0, 0);
       }
     }
     if (++ckt == ckt1) {  // unit finished: epilogue
@@ -1685,7 +1523,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
 constexpr int G6_BM = 64, G6_BN = 64, G6_NT = 256;
 constexpr int G6_A = G6_BM * BK * 2, G6_W = G6_BN * BK * 2, G6_STAGE = G6_A + G6_W;  // 8 + 8 KiB
 
-template <int MODE, int G6_S, bool PF = true>  // PF: as gemm2's (all fragment reads ahead of the MFMAs)
+template <int MODE, int G6_S>  // all fragment reads of a K-tile ahead of its MFMAs (as gemm2)
 __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void gemm6_kernel(
     const vd_gemm_desc d, uint32_t a0_bytes, uint32_t a1_bytes, uint32_t w_bytes, int split) {
   constexpr int MB = 2, NB = 2;
@@ -1801,7 +1639,7 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
     __builtin_amdgcn_s_barrier();
     if (it + G6_S - 1 < nk) issue(stage == 0 ? G6_S - 1 : stage - 1);
     const char* sb = smem + stage * G6_STAGE;
-    if constexpr (PF) {
+    {
       bf16x8 wf[BK / 32][NB], xf[BK / 32][MB];
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks) {
@@ -1819,20 +1657,6 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
 #pragma unroll
           for (int b = 0; b < MB; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][a], xf[ks][b], acc[a][b], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
-        bf16x8 wf[NB], xf[MB];
-#pragma unroll
-        for (int a = 0; a < NB; ++a) wf[a] = *(const bf16x8*)(sb + G6_A + 2 * lds_off(wn * 32 + a * 16 + fr, ks * 4 + fq));
-#pragma unroll
-        for (int b = 0; b < MB; ++b) xf[b] = *(const bf16x8*)(sb + 2 * lds_off(wm * 32 + b * 16 + fr, ks * 4 + fq));
-#pragma unroll
-        for (int a = 0; a < NB; ++a)
-#pragma unroll
-          for (int b = 0; b < MB; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], xf[b], acc[a][b], 0, 0, 0);
-      }
     }
     stage = stage == G6_S - 1 ? 0 : stage + 1;
   }
@@ -1996,55 +1820,16 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
   }
 }
 
-// v2 in the 32x32x16 form (gemm2_kernel<160, *, 1, 1>; round 3): half the MFMA instructions, a
-// third more fragment reads.  Measured (tools/kbench.py, tools/ab_step.py mf,
-// profiles/r03m_gemm_mfma32_ab.txt): 7-11 % slower on the longer-K convs and most dense shapes;
-// on the level-1 320 -> 320 conv it won 5 % (-0.18 ms/step in-process) until the branch-free conv
-// loader took the same VALU out of the 16x16 form, after which it lost (+0.18 ms/step) — so the
-// automatic plan never takes it (g_g2_mf 0); -1 = the short-K level-1 convs only, 1 = every conv,
-// 2 = convs and dense GEMMs (vd_gemm_select_path 17 / 18, A/B).  Not for GEGLU.
-int g_g2_mf = 0;
-int g_g2_fd = 1;  // 0: v2's conv row setup with int64 divisions (round 2's form; vd_gemm_select_path(20), A/B)
-inline bool mf32_ok(const vd_gemm_desc& d) {
-  if (d.act == VD_ACT_GEGLU || d.N % 32 || d.ldc % 8 || ((uintptr_t)d.out & 15)) return false;
-  if (g_g2_mf < 0) return d.a_mode == VD_A_CONV3X3 && d.K <= 2880 && d.M >= 65536;
-  return g_g2_mf == 2 || (g_g2_mf == 1 && d.a_mode == VD_A_CONV3X3);
-}
-
 template <int BN>
 int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
   const int64_t units = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + BN - 1) / BN) * split;
   // persistent: one workgroup per CU, ceil(units / grid) rounds, balanced grid
   const int64_t rounds = (units + g_num_cus - 1) / g_num_cus;
   const int64_t grid = (units + rounds - 1) / rounds;
-  const int pf = g_g2_pf >= 0 ? g_g2_pf : 2;
-#define G2_LAUNCH(MODE_, PF_) \
-  hipLaunchKernelGGL((gemm2_kernel<BN, MODE_, PF_>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split)
-  if constexpr (BN == 160) {
-    if (mf32_ok(d)) {
-      if (d.a_mode == VD_A_CONV3X3)
-        hipLaunchKernelGGL((gemm2_kernel<160, VD_A_CONV3X3, 1, 1>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b,
-                           a1b, wb, split);
-      else
-        hipLaunchKernelGGL((gemm2_kernel<160, VD_A_DENSE, 1, 1>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b,
-                           a1b, wb, split);
-      goto launched;
-    }
-  }
-  if (d.a_mode == VD_A_CONV3X3 && !g_g2_fd && pf == 2) {  // A/B: round 2's conv row setup
-    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3, 2, 0, false>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b,
-                       a1b, wb, split);
-  } else if (d.a_mode == VD_A_CONV3X3) {
-    if (pf == 0) G2_LAUNCH(VD_A_CONV3X3, 0);
-    else if (pf == 1) G2_LAUNCH(VD_A_CONV3X3, 1);
-    else G2_LAUNCH(VD_A_CONV3X3, 2);
-  } else {
-    if (pf == 0) G2_LAUNCH(VD_A_DENSE, 0);
-    else if (pf == 1) G2_LAUNCH(VD_A_DENSE, 1);
-    else G2_LAUNCH(VD_A_DENSE, 2);
-  }
-#undef G2_LAUNCH
-launched:
+  if (d.a_mode == VD_A_CONV3X3)
+    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
+  else
+    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
   int rc = vd_launch_status();
   if (rc != VD_OK || split == 1) return rc;
   const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
@@ -2075,18 +1860,12 @@ int launch4(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   if (d.a_mode == VD_A_CONV3X3)
     hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_CONV3X3>), dim3((unsigned)grid), dim3(C::NT), 0,
                        s, d, a0b, a1b, wb, split);
-  else if (d.ln_out && g_g4_roll)  // plan() only lets a fusable descriptor keep ln_out
+  else if (d.ln_out)  // plan() only lets a fusable descriptor keep ln_out
     hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_DENSE, true>), dim3((unsigned)grid), dim3(C::NT), 0,
                        s, d, a0b, a1b, wb, split);
-  else if (d.ln_out)
-    hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_DENSE, true, false>), dim3((unsigned)grid),
-                       dim3(C::NT), 0, s, d, a0b, a1b, wb, split);
-  else if (g_g4_roll)
+  else
     hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_DENSE>), dim3((unsigned)grid), dim3(C::NT), 0, s,
                        d, a0b, a1b, wb, split);
-  else
-    hipLaunchKernelGGL((gemm4_kernel<BN, WM, WN, STAGES, VD_A_DENSE, false, false>), dim3((unsigned)grid),
-                       dim3(C::NT), 0, s, d, a0b, a1b, wb, split);
   int rc = vd_launch_status();
   if (rc != VD_OK || split == 1) return rc;
   const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
@@ -2104,14 +1883,10 @@ int launch6(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   }
   const int64_t wgs = tiles * split;
   const dim3 grid((unsigned)wgs);
-#define G6_LAUNCH(S)                                                                                           \
-  if (d.a_mode == VD_A_CONV3X3 && g_g2_old)                                                                    \
-    hipLaunchKernelGGL((gemm6_kernel<VD_A_CONV3X3, S, false>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split); \
-  else if (d.a_mode == VD_A_CONV3X3)                                                                           \
-    hipLaunchKernelGGL((gemm6_kernel<VD_A_CONV3X3, S>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split);        \
-  else if (g_g2_old)                                                                                           \
-    hipLaunchKernelGGL((gemm6_kernel<VD_A_DENSE, S, false>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split);   \
-  else                                                                                                         \
+#define G6_LAUNCH(S)                                                                                    \
+  if (d.a_mode == VD_A_CONV3X3)                                                                         \
+    hipLaunchKernelGGL((gemm6_kernel<VD_A_CONV3X3, S>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split); \
+  else                                                                                                  \
     hipLaunchKernelGGL((gemm6_kernel<VD_A_DENSE, S>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split);
   if (wgs <= g_num_cus) {
     G6_LAUNCH(6)
@@ -2124,14 +1899,13 @@ int launch6(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   return vd_launch_status();
 }
 
-int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split,
-            bool persistent) {
+int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
   const int64_t units = ((d.M + G3_BM - 1) / G3_BM) * ((d.N + G3_BN - 1) / G3_BN) * split;
   if (units > 0x7fffffff) return VD_EINVAL;
   // persistent: one workgroup per CU, ceil(units / CUs) units each, balanced grid
-  const int64_t rounds = persistent ? (units + g_num_cus - 1) / g_num_cus : 1;
+  const int64_t rounds = (units + g_num_cus - 1) / g_num_cus;
   const int64_t grid = (units + rounds - 1) / rounds;
-  const int fast = g_g3_fast && split == 1 && !d.res && !d.rowbias && !d.out_f32 && d.N % 8 == 0 &&
+  const int fast = split == 1 && !d.res && !d.rowbias && !d.out_f32 && d.N % 8 == 0 &&
                    d.N <= G3_BIAS_N && d.ldc % 8 == 0 && ((uintptr_t)d.out & 15) == 0 &&
                    d.M * d.ldc * 2 < (int64_t)G2_OOB;
   hipLaunchKernelGGL((gemm3_kernel<VD_A_DENSE>), dim3((unsigned)grid), dim3(G3_NT), 0, s, d, a0b, a1b, wb, split,
@@ -2146,29 +1920,24 @@ int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool al8(const void* p) { return ((uintptr_t)p & 7) == 0; }
-int g_path = 0;  // 0 auto, 1 v1, 2 v2, 3 v3, 5 v5, 6 v6, 7 auto without v6, 8 v6 unsplit,
-                  // 9 auto with split-K cap 8, 10 v3 one unit per workgroup, 11 auto with v3
-                  // one unit per workgroup (tests / benchmarks)
-
 struct Plan {
   int ver = 1;
   int bn = 128, split = 1;
-  bool persist = true;  // v3: persistent flat K-tile stream
   bool ln_fused = false;  // v5 writes ln_out in its epilogue
   uint32_t a0b = 0, a1b = 0, wb = 0;
   int64_t ws_bytes = 0;
 };
 
 // max K slices of the v2/v3/v5 split path: 32 (L4 convs at 4-8 images per rank, 64 -> 176
-// workgroups: 66 -> 38 us, 41 -> 30 us; neutral elsewhere — profiles/r01_gemm_paths.txt);
-// path 9 restores the earlier cap of 8 for comparisons
-int g_split_cap = 32;
+// workgroups: 66 -> 38 us, 41 -> 30 us against a cap of 8; neutral elsewhere —
+// profiles/r01_gemm_paths.txt)
+constexpr int SPLIT_CAP = 32;
 
 inline int split_for(int64_t tiles, int64_t nk) {
   if (tiles >= 192 || nk < 16) return 1;
   int64_t sp = (256 + tiles - 1) / tiles;
   sp = sp < nk / 8 ? sp : nk / 8;
-  return (int)(sp < g_split_cap ? sp : g_split_cap);
+  return (int)(sp < SPLIT_CAP ? sp : SPLIT_CAP);
 }
 
 // LDS-DMA kernels wherever the operands fit 32-bit buffer offsets: v3 (256x256,
@@ -2186,10 +1955,18 @@ void read_num_cus() {  // once per process: the plan (and the workspace size) de
   }
 }
 
+// d.path (per call, stateless): 0 = this automatic plan; 1 / 2 / 3 / 5 / 6 force v1 / v2 / v3 /
+// v5 / v6 (forced v6 also splits K toward 2 workgroups per CU) wherever that kernel takes the
+// shape, else the automatic choice — the parity tests run every path.  d.plan_m > 0 makes
+// every decision (kernel, tile count, split-K, LayerNorm fusion) as if M were plan_m while the
+// launch covers all M rows: an unsharded run planned with a frame shard's M reproduces that
+// shard's arithmetic exactly (split-K fixes the summation order).
 Plan plan(const vd_gemm_desc& d) {
   read_num_cus();
   Plan p;
-  if (g_path == 1 || d.K % G4_BK || d.k0 % G4_BK || d.M < G6_BM || (d.N < 64 && d.N > 32)) return p;
+  const int path = d.path;
+  const int64_t M = d.plan_m > 0 ? d.plan_m : d.M;  // the row count the plan is made for
+  if (path == 1 || d.K % G4_BK || d.k0 % G4_BK || M < G6_BM || (d.N < 64 && d.N > 32)) return p;
   const int64_t a_rows = d.a_mode == VD_A_CONV3X3
                              ? (int64_t)d.n_img / d.frames_out * d.frames_in * d.h_in * d.w_in : d.M;
   const int64_t a0b = a_rows * d.lda0 * 2, a1b = d.a1 ? a_rows * d.lda1 * 2 : 0, wb = d.N * d.ldw * 2;
@@ -2204,8 +1981,8 @@ Plan plan(const vd_gemm_desc& d) {
     p.ln_fused = d.a_mode == VD_A_DENSE && d.N == 320 && d.K % G4_BK == 0 && d.k0 == d.K && !d.a1 &&
                  d.ldc % 8 == 0 && d.ld_ln % 8 == 0 && ((uintptr_t)d.out & 15) == 0 && ((uintptr_t)d.ln_out & 15) == 0 &&
                  (!d.res || (d.ld_res % 8 == 0 && ((uintptr_t)d.res & 15) == 0)) &&
-                 (d.M + G4_BM - 1) / G4_BM >= 128 && !d.rowbias && d.act == VD_ACT_NONE && !d.out_f32 &&
-                 (g_path == 0 || g_path == 5 || g_path == 11);
+                 (M + G4_BM - 1) / G4_BM >= 128 && !d.rowbias && d.act == VD_ACT_NONE && !d.out_f32 &&
+                 (path == 0 || path == 5);
     if (p.ln_fused) {
       p.ver = 5;
       p.bn = 320;
@@ -2215,17 +1992,17 @@ Plan plan(const vd_gemm_desc& d) {
   // N <= 32 (conv_out, N = 4): 256 x 32 v2 tiles — v1's 128 x 64 tiles ran the full-size
   // conv_out (M 131072, K 2880) in 177 us (profiles/r02b_step_breakdown_f16.txt)
   if (d.N <= 32) {
-    if (!k64 || d.M < G2_BM || d.act == VD_ACT_GEGLU || (g_path != 0 && g_path != 2 && g_path != 11)) return p;
+    if (!k64 || M < G2_BM || d.act == VD_ACT_GEGLU || (path != 0 && path != 2)) return p;
     p.ver = 2;
     p.bn = 32;
-    p.split = split_for((d.M + G2_BM - 1) / G2_BM, d.K / BK);
+    p.split = split_for((M + G2_BM - 1) / G2_BM, d.K / BK);
     p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 : 0;
     return p;
   }
   // fewer rows than one 256-row tile (the deep levels of a 1-2 image rank): 64 x 64 tiles
   // (v1's 128-row tiles left L4's K = 11520 convs on 8 workgroups: 453 us vs ~30)
-  if (d.M < G2_BM) {
-    if (!k64 || d.kt > 1 || d.ks == 1 || (g_path != 0 && g_path != 6 && g_path != 8 && g_path != 11)) return p;  // v6: 2-D 3x3 taps
+  if (M < G2_BM) {
+    if (!k64 || d.kt > 1 || d.ks == 1 || (path != 0 && path != 6)) return p;  // v6: 2-D 3x3 taps
     p.ver = 6;
     p.bn = 64;
     return p;
@@ -2235,7 +2012,7 @@ Plan plan(const vd_gemm_desc& d) {
     p.ver = 2;
     const int64_t p128 = (d.N + 127) / 128 * 128, p160 = (d.N + 159) / 160 * 160;
     p.bn = (p160 < p128 || (p160 == p128 && d.N % 160 == 0)) ? 160 : 128;
-    p.split = split_for(((d.M + G2_BM - 1) / G2_BM) * ((d.N + p.bn - 1) / p.bn), d.K / BK);
+    p.split = split_for(((M + G2_BM - 1) / G2_BM) * ((d.N + p.bn - 1) / p.bn), d.K / BK);
     p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 : 0;
     return p;
   }
@@ -2243,13 +2020,13 @@ Plan plan(const vd_gemm_desc& d) {
   // it wins (tools/kbench.py: the L1 attention QKV projection M 131072 x N 960 x K 320)
   // (round 2) and the L1 projections N = K = 320 with or without a residual: one 320-column
   // tile covers the whole row (+res 75 vs 85 us on v2, profiles/r02_gemm_paths_vs_hipblaslt_miopen.txt)
-  const bool v5auto = d.a_mode == VD_A_DENSE && d.M >= 65536 && d.K <= 320 && !d.rowbias && d.act != VD_ACT_GEGLU &&
+  const bool v5auto = d.a_mode == VD_A_DENSE && M >= 65536 && d.K <= 320 && !d.rowbias && d.act != VD_ACT_GEGLU &&
                       ((d.N % 320 == 0 && d.N >= 640 && d.N < 2560 && !d.res) || d.N == 320);
-  if (g_path == 5 || ((g_path == 0 || g_path == 7 || g_path == 11) && (!k64 || v5auto))) {
+  if (path == 5 || (path == 0 && (!k64 || v5auto))) {
     if (!cin32) return p;
     p.ver = 5;
     p.bn = 320;
-    const int64_t tiles = ((d.M + G4_BM - 1) / G4_BM) * ((d.N + 319) / 320);
+    const int64_t tiles = ((M + G4_BM - 1) / G4_BM) * ((d.N + 319) / 320);
     p.split = split_for(tiles, d.K / BK);
     p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 : 0;
     return p;
@@ -2263,26 +2040,26 @@ Plan plan(const vd_gemm_desc& d) {
   // tools/kb_sweep.sh, profiles/r01_gemm_paths.txt: 4 images L3/L4 projections 21-27 ->
   // 11 us, L4 qkv 24 -> 11 us; v2/v3 stay faster on long K, wide N at M >= 2048, and convs.
   {
-    const int64_t tiles6 = ((d.M + G6_BM - 1) / G6_BM) * ((d.N + G6_BN - 1) / G6_BN);
-    const int64_t tiles256 = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + 159) / 160);
+    const int64_t tiles6 = ((M + G6_BM - 1) / G6_BM) * ((d.N + G6_BN - 1) / G6_BN);
+    const int64_t tiles256 = ((M + G2_BM - 1) / G2_BM) * ((d.N + 159) / 160);
     const bool v6auto = tiles256 < g_num_cus && (d.N <= 1280 || tiles6 <= 4 * g_num_cus) &&
                         (d.act != VD_ACT_GEGLU || 2 * tiles256 <= g_num_cus) &&
                         (d.K <= 1280 || (d.K <= 2560 && tiles6 >= 2 * g_num_cus));
-    if (g_path == 6 || g_path == 8 || ((g_path == 0 || g_path == 11) && v6auto)) {
+    if (path == 6 || (path == 0 && v6auto)) {
       p.ver = 6;
       p.bn = 64;
       int64_t sp = 1;
       // forced v6: aim for >= 2 workgroups per CU, each slice >= 4 k-tiles (the automatic
       // choice never splits: the in-kernel reduction's agent-scope release/acquire fences
       // write back / invalidate L2 and cost ~25 us — profiles/r01_gemm_paths.txt)
-      while (g_path == 6 && tiles6 * sp < 2 * g_num_cus && nk / (sp * 2) >= 4 && sp < 16) sp *= 2;
+      while (path == 6 && tiles6 * sp < 2 * g_num_cus && nk / (sp * 2) >= 4 && sp < 16) sp *= 2;
       p.split = (int)sp;
-      p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 + ((tiles6 * 4 + 255) / 256) * 256 : 0;
+      const int64_t rtiles6 = ((d.M + G6_BM - 1) / G6_BM) * ((d.N + G6_BN - 1) / G6_BN);  // launched tiles
+      p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 + ((rtiles6 * 4 + 255) / 256) * 256 : 0;
       return p;
     }
   }
-  const bool v3ok = d.a_mode == VD_A_DENSE && d.N >= 256 && g_path != 2;
-  p.persist = g_path != 10 && g_path != 11;
+  const bool v3ok = d.a_mode == VD_A_DENSE && d.N >= 256 && path != 2;
   const int64_t p256 = (d.N + 255) / 256 * 256;
   // measured (tools/kbench.py): v3 wins on the wide projections (qkv, GEGLU) once the
   // grid fills the chip without split-K; v2's persistent stream wins on N <= 640 and
@@ -2293,21 +2070,21 @@ Plan plan(const vd_gemm_desc& d) {
   // persistent v3 (round 2) also wins at 1/8 padding with short K: L2 qkv N 1920 -> 2048,
   // K 640: 98 vs 109 us on v2 (profiles/r02_gemm3_persistent.txt)
   const bool v3pad = (p256 - d.N) * 8 <= d.N;
-  const int64_t tiles3 = ((d.M + G3_BM - 1) / G3_BM) * (p256 / 256);
+  const int64_t tiles3 = ((M + G3_BM - 1) / G3_BM) * (p256 / 256);
   // GEGLU on v3 only from 3 tiles per CU: after the v2 fragment-order fix (round 2) v2's 256 x 128
   // tiles win the 320-640-tile GEGLUs (4 images L1 46 vs 51 us, L2 41 vs 52; 32 images L4 66 vs
   // 81 us; tools/plan_sweep.py, profiles/r02f_plan_sweep.txt)
   const bool v3auto = v3ok && d.N >= 768 && v3pad && tiles3 >= 256 &&
                       (d.act != VD_ACT_GEGLU || tiles3 >= 3 * g_num_cus);
-  if (g_path == 3 || g_path == 10 ? v3ok : v3auto) {
+  if (path == 3 ? v3ok : v3auto) {
     p.ver = 3;
     p.bn = 256;
-    p.split = split_for(((d.M + G3_BM - 1) / G3_BM) * (p256 / 256), nk);
+    p.split = split_for(((M + G3_BM - 1) / G3_BM) * (p256 / 256), nk);
   } else {
     p.ver = 2;
     const int64_t p128 = (d.N + 127) / 128 * 128, p160 = (d.N + 159) / 160 * 160;
     p.bn = d.act != VD_ACT_GEGLU && (p160 < p128 || (p160 == p128 && d.N % 160 == 0)) ? 160 : 128;
-    p.split = split_for(((d.M + G2_BM - 1) / G2_BM) * ((d.N + p.bn - 1) / p.bn), nk);
+    p.split = split_for(((M + G2_BM - 1) / G2_BM) * ((d.N + p.bn - 1) / p.bn), nk);
   }
   p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 : 0;
   return p;
@@ -2329,29 +2106,6 @@ vd_gemm_desc normalized(const vd_gemm_desc& in) {
 }
 
 extern "C" int64_t vd_gemm_ws_bytes(const vd_gemm_desc* d) { return d ? plan(normalized(*d)).ws_bytes : 0; }
-
-// Test/benchmark hooks: force the v1 (register-staged) GEMM path / pick a path.
-extern "C" int vd_gemm_force_v1(int32_t on) {
-  g_path = on ? 1 : 0;
-  return VD_OK;
-}
-extern "C" int vd_gemm_select_path(int32_t path) {
-  if (path < 0 || path > 20 || path == 4) return VD_EINVAL;
-  g_g2_fd = path != 20;
-  if (path == 20) path = 0;  // auto plan, v2 conv rows set up with round 2's divisions (A/B)
-  g_g2_mf = path == 17 ? 1 : path == 18 ? 2 : path == 19 ? -1 : 0;
-  if (path >= 17) path = 0;  // auto plan, v2 in the 32x32x16 form for convs / convs + dense / short-K L1 convs (A/B)
-  g_g4_roll = path != 16;
-  if (path == 16) path = 0;  // auto plan, v5 with round 1's fragment halves (A/B)
-  g_g3_fast = path != 15;
-  if (path == 15) path = 0;  // auto plan, v3 with gemm_epilogue (A/B)
-  g_g2_old = path == 12;
-  g_g2_pf = path == 12 ? 0 : path == 13 ? 2 : path == 14 ? 1 : -1;
-  if (path >= 12) path = 0;  // auto plan; v2 / v6 fragment-read order forced (A/B)
-  g_split_cap = path == 9 ? 8 : 32;
-  g_path = path == 9 ? 0 : path;
-  return VD_OK;
-}
 
 extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   if (!dp) return VD_EINVAL;
@@ -2410,7 +2164,7 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
     return vd_layernorm(d.out, d.ldc, d.M, d.N, d.ln_gamma, d.ln_beta, d.ln_eps, d.ln_pe, d.ln_pe_div,
                         d.ln_pe_period, d.ln_out, d.ld_ln, stream);
   }
-  if (p.ver == 3) return launch3(d, s, p.a0b, p.a1b, p.wb, p.split, p.persist);
+  if (p.ver == 3) return launch3(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 6) return launch6(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 5) return launch4<320, 4, 2, 4>(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 2)

@@ -5,15 +5,15 @@
 // SDPA over the F frames of every position (experiments/03_trace_forward_pass.py:160-169).
 // The unfused path writes the [rows][3C] QKV projection to HBM and the attention kernel
 // reads it back (at level 1: 252 MB each way per layer, 10 layers per step).  Here one
-// workgroup owns P positions x all 16 frames of one video (P*16 NHWC rows, read from
-// their row stride H*W): it stages those rows of the normed activations in LDS once, then
-// for every head h streams that head's 3d rows of the fused QKV weight through a two-slot
-// LDS ring, accumulates Q_h|K_h|V_h of its 16 tokens per wave on 16x16x32 MFMAs (C^T =
-// W.A^T as in gemm.hip: lane (fr, fq) ends with frame fr, channels 16a + 4fq + j), rounds
-// them to bf16 into a per-wave scratch, and runs the 16-frame attention of that position
-// and head exactly as temporal_mfma_kernel does (S^T = K.Q^T, softmax in log2 units, O^T =
-// V^T.P^T with V's ones column giving the row sum).  Only the normed rows are read and O
-// is written: the QKV round trip and one launch per attention disappear.
+// workgroup owns P positions (x PW per wave) x all 16 frames of one video (P*16 NHWC rows, read
+// from their row stride H*W): each wave holds its own positions' 16 token rows of the normed
+// activations as register fragments, and for every head h that head's 3d rows of the fused QKV
+// weight stream through an LDS-DMA ring; Q_h|K_h|V_h of the wave's 16 tokens accumulate on
+// 16x16x32 MFMAs (C^T = W.A^T as in gemm.hip: lane (fr, fq) ends with frame fr, channels
+// 16a + 4fq + j), are rounded to bf16 into a per-wave scratch, and the 16-frame attention of
+// that position and head runs exactly as temporal_mfma_kernel does (S^T = K.Q^T, softmax in log2
+// units, O^T = V^T.P^T with V's ones column giving the row sum).  Only the normed rows are read
+// and O is written: the QKV round trip and one launch per attention disappear.
 //
 // The projection's k order (32-wide MFMA steps, ascending) and the attention arithmetic
 // are those of the unfused v5 GEMM + temporal_mfma_kernel, so the output is bit-identical
@@ -57,191 +57,15 @@ struct MqCfg {
 // 16x16x32 fragment reads (ds_read_b128) are conflict-free (gemm.hip's lds_off)
 __device__ __forceinline__ int sw64(int row, int chunk) { return row * 64 + ((chunk ^ (row & 7)) << 3); }
 
-template <int D>
-__global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn_kernel(
-    const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw, bf16_t* __restrict__ o,
-    int64_t ldo, int64_t batch, int64_t positions, float c) {
-  using Cf = MqCfg<D>;
-  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
-  bf16_t* a_l = lds;                                     // [C/64 blocks][ROWS][64]
-  bf16_t* w_l = lds + Cf::A_ELEMS;                       // 2 slots x [NWP][64]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int fr = lane & 15, fq = lane >> 4;
-  bf16_t* s_l = lds + Cf::A_ELEMS + 2 * Cf::W_ELEMS + wave * Cf::S_ELEMS;
-  bf16_t* q_s = s_l;                                     // [16][DPAD]
-  bf16_t* k_s = s_l + MF * Cf::DPAD;                     // [16][DPAD]
-  bf16_t* v_s = s_l + 2 * MF * Cf::DPAD;                 // V image [16][VS]
-
-  const int64_t nblk_p = (positions + Cf::P - 1) / Cf::P;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t b = lid / nblk_p;
-  const int64_t p0 = (lid - b * nblk_p) * Cf::P;
-  const bool pok = p0 + wave < positions;
-
-  // ---- scratch padding (written once; the heads only write columns < D): Q/K columns
-  // [D, DPAD) zero; the V image zero except column D = 1.0 (the row-sum column)
-  for (int i = lane; i < Cf::S_ELEMS / 8; i += 64) *(uint4*)(s_l + i * 8) = make_uint4(0, 0, 0, 0);
-  // ring pad rows [3D, NWP) of both slots: zero (never written by the weight loads)
-  for (int i = tid; i < 2 * (Cf::NWP - 3 * D) * 8; i += Cf::NT) {
-    const int slot = i / ((Cf::NWP - 3 * D) * 8), r = (i / 8) % (Cf::NWP - 3 * D) + 3 * D, ch = i % 8;
-    *(uint4*)(w_l + slot * Cf::W_ELEMS + r * 64 + ch * 8) = make_uint4(0, 0, 0, 0);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (lane < MF) v_s[lane * Cf::VS + D] = (bf16_t)0x3F80;
-
-  // ---- token tile: row r = wave' * 16 + f  <-  video b, frame f, position p0 + wave'
-  {
-    u32x4 st[Cf::AREG];
-#pragma unroll
-    for (int i = 0; i < Cf::AREG; ++i) {
-      const int idx = tid + i * Cf::NT;
-      if (idx < Cf::ACH) {
-        const int r = idx / (Cf::C / 8), cc = idx % (Cf::C / 8);
-        int64_t p = p0 + r / MF;
-        p = p < positions ? p : positions - 1;
-        const int64_t grow = (b * MF + r % MF) * positions + p;
-        st[i] = *(const u32x4*)(x + grow * ldx + cc * 8);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < Cf::AREG; ++i) {
-      const int idx = tid + i * Cf::NT;
-      if (idx < Cf::ACH) {
-        const int r = idx / (Cf::C / 8), cc = idx % (Cf::C / 8);
-        *(u32x4*)(a_l + (cc / 8) * Cf::ROWS * 64 + sw64(r, cc % 8)) = st[i];
-      }
-    }
-  }
-  // ---- weight chunk t = (head h, k-chunk kc): ring rows n < 3D are W rows
-  // (n / D) * C + h * D + n % D (q | k | v of head h), columns kc*64 .. +63
-  // one register set: chunk t+1 loads while chunk t is in the MFMAs (a three-set, two-ahead
-  // variant measured slower: 251 vs 226 us at level 1)
-  u32x4 wst[Cf::WREG];
-  // (macros, not lambdas: a lambda capturing the staging array left it on the scratch stack)
-#define MQ_W_LOAD(T_)                                                                       \
-  {                                                                                         \
-    const int h_ = (T_) / Cf::NCH, kc_ = (T_) % Cf::NCH;                                    \
-    _Pragma("unroll") for (int i = 0; i < Cf::WREG; ++i) {                                  \
-      const int idx = tid + i * Cf::NT;                                                     \
-      if (idx < Cf::WCH) {                                                                  \
-        const int n = idx / 8, cc = idx % 8;                                                \
-        const int64_t grow = (int64_t)(n / D) * Cf::C + h_ * D + n % D;                     \
-        wst[i] = *(const u32x4*)(w + grow * ldw + kc_ * Cf::KC + cc * 8);                   \
-      }                                                                                     \
-    }                                                                                       \
-  }
-#define MQ_W_STORE(SLOT)                                                                    \
-  {                                                                                         \
-    _Pragma("unroll") for (int i = 0; i < Cf::WREG; ++i) {                                  \
-      const int idx = tid + i * Cf::NT;                                                     \
-      if (idx < Cf::WCH) *(u32x4*)(w_l + (SLOT) * Cf::W_ELEMS + sw64(idx / 8, idx % 8)) = wst[i]; \
-    }                                                                                       \
-  }
-  MQ_W_LOAD(0)
-  MQ_W_STORE(0)
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  const bool unitc = c == 1.0f;
-  const int vtr = (4 * fq + (fr >> 2)) * Cf::VS + 4 * (fr & 3);  // tr-read lane offset (temporal_mfma_kernel)
-  const int arow = wave * MF + fr;                                // this lane's token row in the tile
-  f32x4 acc[Cf::NBLK];
-#pragma unroll
-  for (int a = 0; a < Cf::NBLK; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int T = 8 * Cf::NCH;
-  for (int t = 0; t < T; ++t) {
-    const int kc = t % Cf::NCH, slot = t & 1;
-    if (t + 1 < T) MQ_W_LOAD(t + 1)
-    const bf16_t* ws = w_l + slot * Cf::W_ELEMS;
-#pragma unroll
-    for (int ks = 0; ks < Cf::KC / 32; ++ks) {
-      const int kk = kc * Cf::KC + ks * 32;  // absolute k of this step
-      const bf16x8 xf = *(const bf16x8*)(a_l + (kk / 64) * Cf::ROWS * 64 + sw64(arow, (kk % 64) / 8 + fq));
-#pragma unroll
-      for (int a = 0; a < Cf::NBLK; ++a) {
-        const bf16x8 wf = *(const bf16x8*)(ws + sw64(a * 16 + fr, ks * 4 + fq));
-        acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[a], 0, 0, 0);
-      }
-    }
-    if (kc == Cf::NCH - 1) {  // ---- head h = t / NCH done: attention of (position p0 + wave, head h)
-      const int h = t / Cf::NCH;
-      // Q_h | K_h | V_h (frame fr, channel 16a + 4fq + j) -> bf16 scratch
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous head's scratch reads
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int a = 0; a < Cf::NBLK; ++a) {
-        const int ch = a * 16 + 4 * fq;
-        if (ch < 3 * D) {
-          const int part = ch / D, cd = ch - part * D;
-          bf16_t* dst = part == 0 ? q_s + fr * Cf::DPAD + cd : (part == 1 ? k_s + fr * Cf::DPAD + cd : v_s + fr * Cf::VS + cd);
-          *(uint2*)dst = make_uint2(pack2(acc[a][0], acc[a][1]), pack2(acc[a][2], acc[a][3]));
-        }
-        acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      // S^T = K . Q^T
-      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < Cf::KSTEPS; ++ks) {
-        const bf16x8 kq = *(const bf16x8*)(k_s + fr * Cf::DPAD + ks * 32 + 8 * fq);
-        const bf16x8 qq = *(const bf16x8*)(q_s + fr * Cf::DPAD + ks * 32 + 8 * fq);
-        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kq, qq, s, 0, 0, 0);
-      }
-      // softmax over keys 4*fq + j of query fr (log2 units)
-      float mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (!unitc) s[j] *= c;
-        mx = fmaxf(mx, s[j]);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      bf16x8 pf;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pf[j] = (__bf16)__builtin_amdgcn_exp2f(s[j] - mx);
-        pf[4 + j] = (__bf16)0.0f;
-      }
-      // O^T = V^T . P^T
-      f32x4 ot[Cf::DB];
-#pragma unroll
-      for (int a = 0; a < Cf::DB; ++a) {
-        const bf16x4 tv = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (bf16x4 __attribute__((address_space(3)))*)(v_s + vtr + 16 * a));
-        const bf16x8 vf = {tv[0], tv[1], tv[2], tv[3], (__bf16)0.0f, (__bf16)0.0f, (__bf16)0.0f, (__bf16)0.0f};
-        ot[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      }
-      const float l = __shfl(ot[D / 16][(D % 16) % 4], ((D % 16) / 4) * 16 + fr, 64);
-      const float inv = __builtin_amdgcn_rcpf(l);
-      if (pok) {
-        bf16_t* orow = o + ((b * MF + fr) * positions + p0 + wave) * ldo + (int64_t)h * D;
-#pragma unroll
-        for (int a = 0; a < Cf::DB; ++a) {
-          const int dd = 16 * a + 4 * fq;
-          if (dd + 4 <= D)
-            *(uint2*)(orow + dd) =
-                make_uint2(pack2(ot[a][0] * inv, ot[a][1] * inv), pack2(ot[a][2] * inv, ot[a][3] * inv));
-        }
-      }
-    }
-    if (t + 1 < T) MQ_W_STORE((t + 1) & 1)  // that slot was last read in step t - 1
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-#undef MQ_W_LOAD
-#undef MQ_W_STORE
-}
-
-// ---------------------------------------------------------------- v2 (round 3)
-// The same arithmetic (bit-identical output), re-staged: a wave only ever reads ITS OWN 16
-// token rows, so their A fragments live in registers (40 VGPRs: all 10 32-deep k-steps, loaded
-// once) instead of an 80 KiB LDS tile, and the 80 KiB go to the weight stream: a 6-slot ring of
-// 16 KiB chunks (128 ring rows x 64 k) filled by LDS-DMA (16 x 1 KiB pieces per chunk, two per
-// wave, the sw64 swizzle applied on the source address, pad rows zero-filled by the buffer
-// range check), five chunks in flight behind counted vmcnt waits — v1 staged one chunk through
-// registers one step ahead and waited out an L2 round trip per 256 cycles of MFMA.
+// ---------------------------------------------------------------- the kernel (round 3)
+// Round 2's form staged the token rows in an 80 KiB LDS tile and streamed register-staged weight
+// chunks one step ahead (an L2 round trip exposed per 256 cycles of MFMA).  Here a wave only ever
+// reads ITS OWN 16 token rows, so their A fragments live in registers (40 VGPRs: all 10 32-deep
+// k-steps, loaded once), and the LDS holds the weight stream: a 6-slot ring of 16 KiB chunks
+// (128 ring rows x 64 k) filled by LDS-DMA (16 x 1 KiB pieces per chunk, two per wave, the sw64
+// swizzle applied on the source address, pad rows zero-filled by the buffer range check), five
+// chunks in flight behind counted vmcnt waits: 212.5 -> 157.3 us per level-1 layer, bit-identical
+// (profiles/r03k_motion_qkv_v2.txt).
 constexpr int MQ2_S = 6;  // ring slots
 
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4m;
@@ -469,10 +293,6 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
-int g_mq_any = 0;  // 1: take the fused kernel at any grid size (A/B hook, vd_attention_select(33 / 34))
-int g_mq_ver = 2;  // 1: round 2's kernel (LDS token tile, register-staged weight chunks); vd_attention_select(31 / 32)
-int g_mq_pw = 0;   // v2 positions per wave: 0 automatic (2 when that fills the chip), 1 / 2 forced (vd_attention_select 40 / 41)
-
 extern "C" int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* wqkv, int64_t ldw, void* o,
                                        int64_t ldo, int64_t batch, int32_t frames, int64_t positions,
                                        int32_t heads, int32_t d, float scale, vd_stream_t stream) {
@@ -490,8 +310,8 @@ extern "C" int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* w
   if (hipGetDevice(&dev) == hipSuccess &&
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
-  if (nwg < (g_mq_ver == 2 ? 1 : 2) * (int64_t)cus && !g_mq_any) return VD_EUNSUPPORTED;
-  if (g_mq_ver == 2) {
+  if (nwg < (int64_t)cus) return VD_EUNSUPPORTED;
+  {
     using C2 = Mq2Cfg<40>;
     static bool attr2_set = false;
     if (!attr2_set) {
@@ -502,9 +322,10 @@ extern "C" int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* w
         return vd_launch_status();
       attr2_set = true;
     }
-    // two positions per wave where that still gives one round of the chip (g_mq_pw: A/B hook)
+    // two positions per wave where that still gives one round of the chip (156 -> 128 us per
+    // level-1 layer, profiles/r03s_motion_pw2.txt)
     const int64_t nwg2 = batch * ((positions + 2 * Cf::P - 1) / (2 * Cf::P));
-    if (g_mq_pw != 1 && (nwg2 >= (int64_t)cus || g_mq_pw == 2)) {
+    if (nwg2 >= (int64_t)cus) {
       hipLaunchKernelGGL((motion_qkv_attn2_kernel<40, 2>), dim3((unsigned)nwg2), dim3(Cf::NT), C2::LDS_BYTES,
                          (hipStream_t)stream, (const bf16_t*)x, ldx, (const bf16_t*)wqkv, ldw, (bf16_t*)o, ldo, batch,
                          positions, scale * 1.4426950408889634f);
@@ -515,15 +336,4 @@ extern "C" int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* w
                        positions, scale * 1.4426950408889634f);
     return vd_launch_status();
   }
-  static bool attr_set = false;
-  if (!attr_set) {  // > 64 KiB of dynamic LDS
-    if (hipFuncSetAttribute((const void*)motion_qkv_attn_kernel<40>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            Cf::LDS_BYTES) != hipSuccess)
-      return vd_launch_status();
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(motion_qkv_attn_kernel<40>, dim3((unsigned)nwg), dim3(Cf::NT), Cf::LDS_BYTES,
-                     (hipStream_t)stream, (const bf16_t*)x, ldx, (const bf16_t*)wqkv, ldw, (bf16_t*)o, ldo, batch,
-                     positions, scale * 1.4426950408889634f);
-  return vd_launch_status();
 }

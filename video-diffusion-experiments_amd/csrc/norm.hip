@@ -474,8 +474,6 @@ __global__ __launch_bounds__(NT) void layernorm_rows_kernel(const bf16_t* x, int
   }
 }
 
-int g_ln_rows = 1;  // 0: always the one-row-per-wave kernel (vd_layernorm_select)
-
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
@@ -569,7 +567,7 @@ extern "C" int vd_layernorm(const void* x, int64_t ldx, int64_t rows, int64_t C,
                        pe_period, (bf16_t*)y, ldy);                                                        \
     return vd_launch_status();                                                                             \
   }
-  if (g_ln_rows) {
+  {  // several rows per wave for the UNet's widths; one row per wave otherwise
     if (C == 320) LN_ROWS(8, 5)
     if (C == 640) LN_ROWS(16, 5)
     if (C == 1280) LN_ROWS(32, 5)
@@ -582,8 +580,3 @@ extern "C" int vd_layernorm(const void* x, int64_t ldx, int64_t rows, int64_t C,
   return vd_launch_status();
 }
 
-// Test/benchmark hook: 0 forces the one-row-per-wave LayerNorm kernel for every C.
-extern "C" int vd_layernorm_select(int32_t multi_row) {
-  g_ln_rows = multi_row != 0;
-  return VD_OK;
-}

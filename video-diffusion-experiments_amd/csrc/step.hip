@@ -252,7 +252,7 @@ extern "C" const char* vd_strerror(int code) {
   }
 }
 
-extern "C" int vd_version(void) { return 3; }  // 3: vd_gemm_desc grew the ln_* fields (round 2)
+extern "C" int vd_version(void) { return 4; }  // 4: per-call path / plan_m in vd_gemm_desc, no selector state (round 4)
 
 #ifndef VD_BUILD_HASH
 #define VD_BUILD_HASH "unhashed"

@@ -26,12 +26,6 @@ SIGNATURES = {
     "vd_build_hash": ([], C.c_char_p),
     "vd_build_arch": ([], C.c_char_p),
     "vd_gemm": ([c_vp, c_vp], c_i32),
-    "vd_gemm_force_v1": ([c_i32], c_i32),
-    "vd_gemm_select_path": ([c_i32], c_i32),
-    "vd_attention_force_v1": ([c_i32], c_i32),
-    "vd_attention_select": ([c_i32], c_i32),
-    "vd_attention_stamps": ([c_vp, c_i64, c_vp], c_i32),
-    "vd_temporal_force_valu": ([c_i32], c_i32),
     "vd_gemm_ws_bytes": ([c_vp], c_i64),
     "vd_gn_partial": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp], c_i32),
     "vd_gn_finalize": ([c_vp, c_i64, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp], c_i32),
@@ -39,10 +33,12 @@ SIGNATURES = {
     "vd_gn_partial_g": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp], c_i32),
     "vd_gn_apply_g": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64, c_i64, c_vp], c_i32),
     "vd_layernorm": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
-    "vd_layernorm_select": ([c_i32], c_i32),
     "vd_attention": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_i64, c_f32, c_vp], c_i32),
     "vd_attention_f32": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_i64, c_f32, c_vp], c_i32),
+    "vd_attention_ex": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_i64, c_f32,
+                         c_i32, c_i32, c_vp], c_i32),
     "vd_temporal_attention": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
+    "vd_temporal_attention_valu": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
     "vd_temporal_attention_kv": ([c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
     "vd_motion_qkv_attention": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
     "vd_temporal_attention_rope": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_f32, c_vp], c_i32),
@@ -93,6 +89,7 @@ class GemmDesc(C.Structure):
         ("ln_gamma", c_vp), ("ln_beta", c_vp), ("ln_eps", c_f32),
         ("ln_pe", c_vp), ("ln_pe_div", c_i64), ("ln_pe_period", c_i64),
         ("ln_out", c_vp), ("ld_ln", c_i64),
+        ("path", c_i32), ("plan_m", c_i64),
     ]
 
 

@@ -15,8 +15,12 @@ combine and the DDIM update stay local).  A motion module needs:
      which is why this build uses all-to-all rather than the K/V all-gather.
 
 Collectives go through torch.distributed (backend "nccl" = RCCL over xGMI on
-MI355X, "gloo" in the CPU tests) on the current stream, so they are captured
-into the step's hipGraph.  The row permutations around the all-to-alls are
+MI355X, "gloo" in the CPU tests) and every one of them — the GroupNorm-record and K/V
+all-gathers, the all-to-all re-shards, the conv halo's all-gather — is issued from the
+capturing stream: ProcessGroupNCCL joins its internal stream to the current stream with
+events, which capture as graph edges, and nothing waits on the host, so they are captured
+into the step's hipGraph (tests/test_gpu_dist.py captures all three windows at world 1).
+The chunked overlap issues its compute, never a collective, on the side stream.  The row permutations around the all-to-alls are
 `transpose(src, nb, na, nc)` — the HIP kernel vd_block_transpose in the product
 path, injected so the decomposition itself is testable on CPU.
 
@@ -164,25 +168,18 @@ class FrameShard:
         """rows (b, f_loc, p) -> rows (b, f_loc + 2, p): every video's local frames between the
         last frame of the previous rank and the first frame of the next (zeros at the video's
         ends = the conv's temporal zero padding) — the one-frame halo a kt = 3 temporal conv
-        (ops.conv3d with frames_in = f_loc + 2, t_off = 1) needs under frame sharding.  Point to
-        point: each rank sends 2 frames per video to each neighbour."""
+        (ops.conv3d with frames_in = f_loc + 2, t_off = 1) needs under frame sharding.
+        One all-gather of every rank's first and last frame per video (2 frames x world per
+        video, ~MBs), issued on the current stream like the module's other collectives — no
+        point-to-point requests and no host-side wait, so the halo is captured into the step's
+        hipGraph as it is (round 3 used batch_isend_irecv + req.wait())."""
         C = x.shape[1]
         W, r = self.world, self.rank
         v = x.view(batch, frames_local, hw, C)
-        first, last = v[:, 0].contiguous(), v[:, -1].contiguous()
-        left = torch.zeros_like(first)
-        right = torch.zeros_like(last)
-        g = (lambda k: dist.get_global_rank(self.group, k)) if self.group is not None else (lambda k: k)
-        ops = []
-        if r > 0:
-            ops += [dist.P2POp(dist.isend, first, g(r - 1), self.group),
-                    dist.P2POp(dist.irecv, left, g(r - 1), self.group)]
-        if r < W - 1:
-            ops += [dist.P2POp(dist.isend, last, g(r + 1), self.group),
-                    dist.P2POp(dist.irecv, right, g(r + 1), self.group)]
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+        ends = torch.stack([v[:, 0], v[:, -1]], 1).contiguous()                 # (b, 2, p, C)
+        allr = self._all_gather(ends.view(-1, C)).view(W, batch, 2, hw, C)     # (r, b, {first, last}, p, C)
+        left = allr[r - 1, :, 1] if r > 0 else torch.zeros_like(v[:, 0])     # previous rank's last frame
+        right = allr[r + 1, :, 0] if r < W - 1 else torch.zeros_like(v[:, 0])  # next rank's first frame
         return torch.cat([left[:, None], v, right[:, None]], 1).reshape(-1, C)
 
     def all_gather_frames(self, x: torch.Tensor) -> torch.Tensor:

@@ -6,6 +6,7 @@ non-CUDA tensors are rejected and a missing library raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import math
 
@@ -42,8 +43,35 @@ def _rows(t, dtype=BF16):
 
 
 # ---------------------------------------------------------------- GEMM / conv
+class _GemmPlan:
+    path = 0       # vd_gemm_desc.path for the GEMMs issued (0 = the automatic plan)
+    plan_div = 0   # > 0: plan every GEMM whose M it divides as if M were M / plan_div
+
+
+_PLAN = _GemmPlan()
+
+
+@contextlib.contextmanager
+def gemm_plan(path: int = 0, plan_div: int = 0):
+    """Test / benchmark hook on the Python side only — the C ABI takes both values per call in
+    vd_gemm_desc and keeps no state.  Inside the block every vd_gemm carries `path` (1 v1, 2 v2,
+    3 v3, 5 v5, 6 v6: forced where that kernel takes the shape) and, with plan_div = N, plan_m =
+    M / N for each GEMM whose M N divides: an unsharded model planned like one of N frame shards
+    (same kernels, split-K and LayerNorm fusion, so the same summation order), which makes the
+    sharded-vs-unsharded comparison of tests/test_gpu_dist2.py bit-exact under the product plan."""
+    old = (_PLAN.path, _PLAN.plan_div)
+    _PLAN.path, _PLAN.plan_div = int(path), int(plan_div)
+    try:
+        yield
+    finally:
+        _PLAN.path, _PLAN.plan_div = old
+
+
 def _run_gemm(d, device, what):
     """Attach the split-K workspace the C side asks for (if any), then launch."""
+    d.path = _PLAN.path
+    if _PLAN.plan_div > 1 and d.M % _PLAN.plan_div == 0:
+        d.plan_m = d.M // _PLAN.plan_div
     nbytes = lib().vd_gemm_ws_bytes(C.byref(d))
     ws = None
     if nbytes > 0:
@@ -266,22 +294,28 @@ def layer_norm(x, gamma, beta, eps=1e-5, pe=None, pe_div=1, pe_period=1, out=Non
 
 
 # ---------------------------------------------------------------- attention
-def attention(q, k, v, batch, heads, sq, skv, d, kv_div=1, scale=None, out=None, out_f32=False):
+ATTN_KERNELS = {"auto": 0, "v1": 1, "flash32": 2, "flash40": 3}
+
+
+def attention(q, k, v, batch, heads, sq, skv, d, kv_div=1, scale=None, out=None, out_f32=False, kernel="auto"):
     """q/k/v: 2-D row views (may be column slices of a fused QKV buffer).  out_f32: O in fp32
-    (vd_attention_f32; the tests' north-star-tolerance mode)."""
+    (the tests' north-star-tolerance mode).  kernel: "auto" (the product choice) or, for the
+    parity tests, "v1" / "flash32" / "flash40" (vd_attention_ex)."""
     _dev(q, k, v, out)
     if out is None:
         out = torch.empty(batch * sq, heads * d, device=q.device, dtype=torch.float32 if out_f32 else BF16)
     scale = d ** -0.5 if scale is None else scale
-    fn = lib().vd_attention_f32 if out_f32 else lib().vd_attention
-    check(fn(_p(q), q.stride(0), _p(k), k.stride(0), _p(v), v.stride(0), _p(out), out.stride(0), batch, heads, sq,
-             skv, d, kv_div, scale, _stream()), "vd_attention_f32" if out_f32 else "vd_attention")
+    check(lib().vd_attention_ex(_p(q), q.stride(0), _p(k), k.stride(0), _p(v), v.stride(0), _p(out), out.stride(0),
+                                batch, heads, sq, skv, d, kv_div, scale, int(out_f32), ATTN_KERNELS[kernel],
+                                _stream()), "vd_attention_ex")
     return out
 
 
-def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, out=None, rope_theta=None):
+def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, out=None, rope_theta=None,
+                       valu=False):
     """rope_theta: apply the temporal 1-D RoPE (rope_qk mode 1) to q/k inside the kernel
-    (vd_temporal_attention_rope: d = 64, 17..32 frames); q and k are read un-rotated."""
+    (vd_temporal_attention_rope: d = 64, 17..32 frames); q and k are read un-rotated.
+    valu: the VALU kernel for every shape (vd_temporal_attention_valu; parity tests)."""
     _dev(q, k, v, out)
     if not (q.stride(0) == k.stride(0) == v.stride(0)):
         raise ValueError("q/k/v must share a row stride")
@@ -289,13 +323,13 @@ def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, 
         out = torch.empty(q.shape[0], heads * d, device=q.device, dtype=BF16)
     scale = d ** -0.5 if scale is None else scale
     if rope_theta is not None:
-        rc = lib().vd_temporal_attention_rope(_p(q), _p(k), _p(v), q.stride(0), _p(out), out.stride(0), batch,
-                                              frames, positions, heads, d, scale, rope_theta, _stream())
-        if rc != VD_EUNSUPPORTED:
-            check(rc, "vd_temporal_attention_rope")
+        if not valu:
+            check(lib().vd_temporal_attention_rope(_p(q), _p(k), _p(v), q.stride(0), _p(out), out.stride(0), batch,
+                                                   frames, positions, heads, d, scale, rope_theta, _stream()),
+                  "vd_temporal_attention_rope")
             return out
-        # no fused variant (the force-VALU test hook): rotate a COPY of q|k (the caller's
-        # buffer stays un-rotated, as the fused kernel leaves it), then attend on the copy
+        # the VALU kernel has no fused RoPE: rotate a COPY of q|k (the caller's buffer stays
+        # un-rotated, as the fused kernel leaves it), then attend on the copy
         C = heads * d
         qkv = torch.empty(q.shape[0], 3 * C, device=q.device, dtype=BF16)
         qkv[:, :C].copy_(q[:, :C])
@@ -303,9 +337,9 @@ def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, 
         qkv[:, 2 * C:].copy_(v[:, :C])
         rope_qk(qkv, 2 * C, d, 1, frames, 1, positions, rope_theta)
         q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
-    check(lib().vd_temporal_attention(_p(q), _p(k), _p(v), q.stride(0), _p(out), out.stride(0), batch,
-                                      frames, positions, heads, d, scale, _stream()),
-          "vd_temporal_attention")
+    fn = lib().vd_temporal_attention_valu if valu else lib().vd_temporal_attention
+    check(fn(_p(q), _p(k), _p(v), q.stride(0), _p(out), out.stride(0), batch, frames, positions, heads, d, scale,
+             _stream()), "vd_temporal_attention")
     return out
 
 
