@@ -50,24 +50,50 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def time_attention(n_img, reps, stream, stress=False):
+def capture_l1_attention(unet, frames, ehs_dim):
+    """The step's own level-1 self-attention operands: one eager UNet forward of the bench
+    workload (both CFG halves of `frames` frames, t = 981) with an ops.ATTN_TAP that keeps the
+    first d = 40, S = 4096 self-attention call's q | k | v (in the model's fused [rows][3C]
+    layout, softmax scale folded into q by Attention.prepare)."""
+    from vdiff import ops
+    got = {}
+
+    def tap(q, k, v, batch, heads, sq, skv, d, scale):
+        if "qkv" not in got and d == 40 and sq == 4096 and skv == 4096:
+            got["qkv"] = torch.cat([q, k, v], 1)
+            got["scale"] = scale
+    g = torch.Generator().manual_seed(42)
+    x = torch.randn((1, 4, frames, 64, 64), generator=g).cuda()
+    ehs = torch.randn((2, 77, ehs_dim), generator=torch.Generator().manual_seed(1)).cuda()
+    ops.ATTN_TAP = tap
+    try:
+        with torch.no_grad():
+            unet(torch.cat([x, x]), 981, encoder_hidden_states=ehs)
+    finally:
+        ops.ATTN_TAP = None
+    torch.cuda.synchronize()
+    return got["qkv"], got["scale"]
+
+
+def time_attention(n_img, reps, stream, stress=False, model_qkv=None):
     """The L1 spatial self-attention kernel alone: 4*S^2*d*heads*n_img FLOPs per launch.
 
-    Inputs as the model's call produces them: q, k, v ~ N(0, 1.5^2) per element out of their
-    projections, and the softmax scale d^-1/2 * log2(e) folded into the Q projection
-    (Attention.prepare), so the kernel's exp2 argument q.k has a std of about 3.2 log2 units
-    (2.2 nats, the range of a trained network's attention logits).  stress=True drops the
-    folded scale (q.k std about 14 log2 units: the row max moves by 2^30 and more between key
-    tiles, so the kernel's deferred-max fast pass rescales often) — round 1's bench input,
-    reported beside the roofline as `stress`."""
+    model_qkv: the step's own q | k | v of that call (capture_l1_attention) — the roofline
+    line.  Without it the synthetic inputs of rounds 1-3: q, k, v ~ N(0, 1.5^2) with the softmax
+    scale d^-1/2 * log2(e) folded into q (exp2-argument std about 3.2 log2 units); stress=True
+    drops the folded scale (std about 14: the deferred-max fast pass rescales often)."""
     from vdiff import ops
     S, heads, d = 4096, 8, 40
     C = heads * d
-    g = torch.Generator(device="cuda").manual_seed(7)
-    qkv = torch.randn(n_img * S, 3 * C, device="cuda", generator=g) * 1.5
-    if not stress:
-        qkv[:, :C] *= d ** -0.5 * math.log2(math.e)
-    qkv = qkv.to(torch.bfloat16)
+    if model_qkv is not None:
+        qkv = model_qkv
+        assert qkv.shape == (n_img * S, 3 * C)
+    else:
+        g = torch.Generator(device="cuda").manual_seed(7)
+        qkv = torch.randn(n_img * S, 3 * C, device="cuda", generator=g) * 1.5
+        if not stress:
+            qkv[:, :C] *= d ** -0.5 * math.log2(math.e)
+        qkv = qkv.to(torch.bfloat16)
     out = torch.empty(n_img * S, C, device="cuda", dtype=torch.bfloat16)
     q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
     scale = 1.0 / math.log2(math.e)   # the model's call: softmax scale folded into to_q (Attention.prepare)
@@ -195,8 +221,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if args.roofline_only:
-        imgs = 2 * (args.frames or 16)
-        roof = time_attention(imgs, args.attn_reps, torch.cuda.current_stream())
+        from vdiff.weights import materialize_synthetic
+        frames = args.frames or 16
+        unet = materialize_synthetic(args.config, device="cuda", seed=0)
+        unet.prepare()
+        mqkv, _ = capture_l1_attention(unet, frames, unet.config["cross_attention_dim"])
+        del unet
+        roof = time_attention(2 * frames, args.attn_reps, torch.cuda.current_stream(), model_qkv=mqkv)
         roof["kernel_src_hash"] = roof_src_hash()
         print(json.dumps({"roofline": roof}), flush=True)
         return
@@ -283,11 +314,19 @@ def main():
         del loop1
 
     imgs = (2 // lay.cfg_ranks) * fl  # images per rank in the CFG run
-    roof = time_attention(imgs, args.attn_reps, torch.cuda.current_stream())
+    mqkv = None
+    if lay.frame_shard is None and lay.cfg_shard is None:  # one GPU: the step's own operands
+        mqkv, _ = capture_l1_attention(unet, fl, cfg["cross_attention_dim"])
+    roof = time_attention(imgs, args.attn_reps, torch.cuda.current_stream(), model_qkv=mqkv)
+    syn = time_attention(imgs, args.attn_reps, torch.cuda.current_stream())
     st = time_attention(imgs, args.attn_reps, torch.cuda.current_stream(), stress=True)
+    roof["synthetic"] = {k: syn[k] for k in ("achieved", "frac", "avg_launch_ms")}
     roof["stress"] = {k: st[k] for k in ("achieved", "frac", "avg_launch_ms")}
-    roof["inputs"] = ("q, k, v ~ N(0, 1.5^2), softmax scale d^-1/2 log2 e folded into q as the model's to_q does "
-                      "(exp2 argument std ~3.2); `stress`: the scale not folded (std ~14)")
+    roof["inputs"] = (("the step's own level-1 self-attention q | k | v (one eager forward of the workload, "
+                       "t = 981; softmax scale folded into q by to_q)") if mqkv is not None else
+                      "synthetic (multi-rank run)") + (
+                      "; `synthetic`: q, k, v ~ N(0, 1.5^2) with the scale folded (exp2 argument std ~3.2), "
+                      "rounds 1-3's roofline input; `stress`: the scale not folded (std ~14)")
     roof["traffic"], roof["traffic_source"] = pmc_traffic(imgs)
     roof["mfma_busy"], roof["mfma_busy_source"] = pmc_mfma_busy()
     roof["kernel_src_hash"] = roof_src_hash()

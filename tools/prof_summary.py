@@ -40,7 +40,7 @@ for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:40]:
 
 # the same kernel inside the step (the L1 spatial self-attention: flash40<unit-c>; before round 3
 # flash32<40, unit-c> launches longer than 300 us, the shorter ones being its text cross-attention)
-ROOF = "flash40_kernel<true," if any("flash40_kernel<true," in r["Kernel_Name"] for r in rows) else "flash32_kernel<40, true, false, 2>"
+ROOF = "flash40_kernel<true>" if any("flash40_kernel<true>" in r["Kernel_Name"] for r in rows) else "flash40_kernel<true,"
 ins = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win if ROOF in r["Kernel_Name"]]
 ins = [x for x in ins if x > 300e3]
 if ins:
@@ -51,14 +51,20 @@ if ins:
 # (the bench line's roofline.avg_launch_ms), then on the stress inputs (roofline.stress);
 # those launches close the trace and their averages must agree with the bench line.
 after = [r for r in rows if int(r["Start_Timestamp"]) > t1 and ROOF in r["Kernel_Name"]]
+FIXK = "flash32_kernel<40, true, true, 2>"  # flash40's exact fix-up (round 4 template order: D, UNITC, FIX, QB)
 fixk = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows
-        if int(r["Start_Timestamp"]) > t1 and "flash32_kernel<40, true, false, 2, true>" in r["Kernel_Name"]]
+        if int(r["Start_Timestamp"]) > t1 and FIXK in r["Kernel_Name"]]
 if fixk:
-    print(f"exact fix-up launches after the step loop (flash32_kernel<40, true, false, 2, true>): {len(fixk)}, "
+    print(f"exact fix-up launches after the step loop ({FIXK}): {len(fixk)}, "
           f"avg {sum(fixk) / len(fixk) / 1e3:.1f} us")
-halves = [after[:len(after) // 2], after[len(after) // 2:]] if len(after) >= 8 else [after]
+# after the step loop: the operand-capture forward (5 level-1 self-attention launches), then three
+# timed sets of WARM + reps launches each: the step's own operands (the bench line's roofline),
+# the synthetic N(0, 1.5^2) inputs (roofline.synthetic) and the stress inputs (roofline.stress)
 WARM = 10  # bench.py WARM_ATTN
-for tag, part in zip(("model-scale inputs", "stress inputs"), halves):
+cap = 5 if len(after) >= 5 and (len(after) - 5) % 3 == 0 else 0
+per = (len(after) - cap) // 3
+sets = [after[cap + i * per: cap + (i + 1) * per] for i in range(3)] if per > WARM else [after]
+for tag, part in zip(("the step's own operands = the bench line", "synthetic inputs", "stress inputs"), sets):
     if len(part) <= WARM:
         continue
     timed = part[WARM:]

@@ -27,12 +27,12 @@ cp $ST $R/gpurun_out/${ROUND}_kernel_stats.csv
 i=0
 for c in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $OUT/p$i -o p -- python3 $R/bench.py --roofline-only \
+  timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d $OUT/p$i -o p -- python3 $R/bench.py --roofline-only \
     > $OUT/p$i.log 2>&1 || { echo "pmc pass $c failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 $R/tools/pmc_traffic.py $OUT "flash40_kernel<true," $R/gpurun_out/${ROUND}_traffic.json \
-  "bench.py --roofline-only (10 warm + 20 timed launches, 32 images)" || exit 1
-timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA --output-format csv -d $OUT/mb -o p -- \
+python3 $R/tools/pmc_traffic.py $OUT "flash40_kernel<true>" $R/gpurun_out/${ROUND}_traffic.json \
+  "bench.py --roofline-only (the step's own L1 operands: 5 in-model + 10 warm + 20 timed launches, 32 images)" || exit 1
+timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA --output-format csv -d $OUT/mb -o p -- \
   python3 $R/bench.py --roofline-only > $OUT/mb.log 2>&1 || { echo "mfma pass failed"; tail -5 $OUT/mb.log; exit 1; }
 python3 $R/tools/mfma_busy.py $OUT/mb $R/gpurun_out/${ROUND}_mfma_busy.json > $R/gpurun_out/${ROUND}_mfma_busy.txt || exit 1
 cat $R/gpurun_out/${ROUND}_roofline_trace.txt | tail -4; cat $R/gpurun_out/${ROUND}_traffic.json; cat $R/gpurun_out/${ROUND}_mfma_busy.txt

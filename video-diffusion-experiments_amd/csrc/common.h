@@ -29,8 +29,12 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(bf16_t, b);
 }
+// two floats -> packed bf16x2 in ONE v_cvt_pk_bf16_f32 (RNE, as f2bf); the scalar casts
+// combined with a shift and an or compiled to four instructions (round 4)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
 
 // 8 bf16 <-> 8 floats through a 16-byte vector.
@@ -63,6 +67,25 @@ __device__ __forceinline__ float erf_fast(float x) {
 }
 // diffusers GEGLU/FeedForward gelu(approximate="none"): 0.5 x (1 + erf(x / sqrt 2))
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+// gelu_erf of two values with the same operations in the same order (bit-identical per element),
+// the multiplies / FMAs as packed fp32 (v_pk_mul_f32 / v_pk_fma_f32: two lanes' worth per issue
+// slot — the GEGLU epilogue is VALU-bound, round 4); the transcendentals and the sign stay scalar.
+typedef f32x2_t f32x2;
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 y = x * 0.70710678118654752f;
+  const f32x2 ax = {fabsf(y[0]), fabsf(y[1])};
+  f32x2 t = __builtin_elementwise_fma(f32x2{0.3275911f, 0.3275911f}, ax, f32x2{1.0f, 1.0f});
+  t = f32x2{__builtin_amdgcn_rcpf(t[0]), __builtin_amdgcn_rcpf(t[1])};
+  f32x2 p = __builtin_elementwise_fma(f32x2{1.061405429f, 1.061405429f}, t, f32x2{-1.453152027f, -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, f32x2{1.421413741f, 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, f32x2{-0.284496736f, -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.254829592f, 0.254829592f});
+  const f32x2 ea = (-1.4426950408889634f * ax) * ax;
+  const f32x2 e = {__builtin_amdgcn_exp2f(ea[0]), __builtin_amdgcn_exp2f(ea[1])};
+  const f32x2 r = __builtin_elementwise_fma(-p * t, e, f32x2{1.0f, 1.0f});
+  const f32x2 erf = {copysignf(r[0], y[0]), copysignf(r[1], y[1])};
+  return (0.5f * x) * (1.0f + erf);
+}
 // pointwise GEMM epilogue activation: VD_ACT_SILU or VD_ACT_GELU (erf form)
 __device__ __forceinline__ float act_pw(int act, float x) { return act == VD_ACT_GELU ? gelu_erf(x) : silu_f(x); }
 

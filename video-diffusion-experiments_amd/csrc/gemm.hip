@@ -99,12 +99,12 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
             uint32_t x[2], y[2];
 #pragma unroll
             for (int h2 = 0; h2 < 2; ++h2) {
-              const float o0 = (acc[a][b][2 * h2] + bh0[2 * h2]) * gelu_erf(acc[a + 1][b][2 * h2] + bg0[2 * h2]);
-              const float o1 = (acc[a][b][2 * h2 + 1] + bh0[2 * h2 + 1]) *
-                               gelu_erf(acc[a + 1][b][2 * h2 + 1] + bg0[2 * h2 + 1]);
-              const float p0 = (acc[a + 2][b][2 * h2] + bh1[2 * h2]) * gelu_erf(acc[a + 3][b][2 * h2] + bg1[2 * h2]);
-              const float p1 = (acc[a + 2][b][2 * h2 + 1] + bh1[2 * h2 + 1]) *
-                               gelu_erf(acc[a + 3][b][2 * h2 + 1] + bg1[2 * h2 + 1]);
+              const f32x2 go = gelu_erf2(f32x2{acc[a + 1][b][2 * h2] + bg0[2 * h2], acc[a + 1][b][2 * h2 + 1] + bg0[2 * h2 + 1]});
+              const f32x2 gp = gelu_erf2(f32x2{acc[a + 3][b][2 * h2] + bg1[2 * h2], acc[a + 3][b][2 * h2 + 1] + bg1[2 * h2 + 1]});
+              const float o0 = (acc[a][b][2 * h2] + bh0[2 * h2]) * go[0];
+              const float o1 = (acc[a][b][2 * h2 + 1] + bh0[2 * h2 + 1]) * go[1];
+              const float p0 = (acc[a + 2][b][2 * h2] + bh1[2 * h2]) * gp[0];
+              const float p1 = (acc[a + 2][b][2 * h2 + 1] + bh1[2 * h2 + 1]) * gp[1];
               auto r = __builtin_amdgcn_permlane16_swap(pack2(o0, o1), pack2(p0, p1), false, false);
               x[h2] = r[0];
               y[h2] = r[1];
@@ -136,8 +136,12 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
           VD_EPI_ROW(b)
           if (!mok_) continue;
           float o[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = (acc[a][b][j] + bh[j]) * gelu_erf(acc[a + 1][b][j] + bg[j]);
+          const f32x2 g01 = gelu_erf2(f32x2{acc[a + 1][b][0] + bg[0], acc[a + 1][b][1] + bg[1]});
+          const f32x2 g23 = gelu_erf2(f32x2{acc[a + 1][b][2] + bg[2], acc[a + 1][b][3] + bg[3]});
+          o[0] = (acc[a][b][0] + bh[0]) * g01[0];
+          o[1] = (acc[a][b][1] + bh[1]) * g01[1];
+          o[2] = (acc[a][b][2] + bh[2]) * g23[0];
+          o[3] = (acc[a][b][3] + bh[3]) * g23[1];
           *(uint2*)(out + (uint32_t)(mrow_ * (int)d.ldc + nout)) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
         }
       }
@@ -433,6 +437,8 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // Fragment-read order (round 2): without a pin hipcc sinks each X fragment read to its 4 MFMAs
 // behind an lgkmcnt(0) — 8 exposed LDS latencies per K-tile.  k-step 0's 9 reads issue right
@@ -444,7 +450,9 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
                                                          uint32_t a1_bytes, uint32_t w_bytes,
                                                          int split) {
   using C = G2<BN>;
-  __shared__ __attribute__((aligned(1024))) char smem[G2_STAGES * C::STAGE];
+  // (+16 B: the split-K "last arriver" flag, inside the one LDS array — a second __shared__
+  // object can make hipcc drain vmcnt before every k-step's fragment reads)
+  __shared__ __attribute__((aligned(1024))) char smem[G2_STAGES * C::STAGE + 16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
@@ -661,6 +669,57 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
       if (split == 1) {
         gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::MB * 16, (int)n0 + wcb, lane,
                                     ODDMAP ? (int)n0 + wodd : -1);
+      } else if (d.tile_cnt) {
+        // split-K reduced in the kernel (round 4): write-through (sc1) fp32 slab, drain, one lane
+        // takes a ticket on the tile's counter (relaxed, agent scope — the fence-free hand-off of
+        // cdna_hip_programming.md Guideline 16); the tile's last slice sums every slab in split
+        // order (gemm_splitk_reduce's order: bit-identical) with sc1 loads, runs the epilogue and
+        // resets the counter, so no reduce launch follows.
+        const __amdgpu_buffer_rsrc_t rws =
+            __builtin_amdgcn_make_buffer_rsrc(d.ws, 0, (uint32_t)((int64_t)split * M * N * 4), 0x00020000);
+        auto soff = [&](int s2, int a, int b) -> uint32_t {
+          const int64_t n = n0 + (a == C::NB - 1 ? wodd : wcb + a * 16) + 4 * fq;
+          const int64_t m = m0 + wm * 64 + b * 16 + fr;
+          return (n < N && m < M) ? (uint32_t)((((int64_t)s2 * M + m) * N + n) * 4) : G2_OOB;
+        };
+#pragma unroll
+        for (int a = 0; a < C::NB; ++a)
+#pragma unroll
+          for (int b = 0; b < C::MB; ++b)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u32x4{__float_as_uint(acc[a][b][0]), __float_as_uint(acc[a][b][1]), __float_as_uint(acc[a][b][2]),
+                      __float_as_uint(acc[a][b][3])},
+                rws, soff(sp, a, b), 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+        __syncthreads();
+        int* last_flag = (int*)(smem + G2_STAGES * C::STAGE);
+        if (tid == 0) {
+          const int prev = __hip_atomic_fetch_add(d.tile_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int last = prev == split - 1;
+          if (last) __hip_atomic_store(d.tile_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *last_flag = last;
+        }
+        __syncthreads();
+        if (*last_flag) {
+#pragma unroll
+          for (int a = 0; a < C::NB; ++a)
+#pragma unroll
+            for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int s2 = 0; s2 < split; ++s2) {
+#pragma unroll
+            for (int a = 0; a < C::NB; ++a) {
+              u32x4 u[C::MB];
+#pragma unroll
+              for (int b = 0; b < C::MB; ++b) u[b] = __builtin_amdgcn_raw_buffer_load_b128(rws, soff(s2, a, b), 0, 16);
+#pragma unroll
+              for (int b = 0; b < C::MB; ++b)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[a][b][j] += __uint_as_float(u[b][j]);
+            }
+          }
+          gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::MB * 16, (int)n0 + wcb, lane,
+                                      ODDMAP ? (int)n0 + wodd : -1);
+        }
       } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
         float* slab = (float*)d.ws + (int64_t)sp * M * N;
 #pragma unroll
@@ -686,8 +745,6 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
   }
 }
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // Load-free epilogue (v5, split == 1, bf16 out, no residual / row bias): the bias
 // comes from the unit's LDS slot (DMA'd with its first k-step) and every store is
@@ -724,10 +781,12 @@ __device__ __forceinline__ int epi_fast(const vd_gemm_desc& d, f32x4 (&acc)[NB][
         uint32_t x[2], y[2];
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
-          const float o0 = (acc[a][b][2 * h2] + bh0[2 * h2]) * gelu_erf(acc[a + 1][b][2 * h2] + bg0[2 * h2]);
-          const float o1 = (acc[a][b][2 * h2 + 1] + bh0[2 * h2 + 1]) * gelu_erf(acc[a + 1][b][2 * h2 + 1] + bg0[2 * h2 + 1]);
-          const float p0 = (acc[a + 2][b][2 * h2] + bh1[2 * h2]) * gelu_erf(acc[a + 3][b][2 * h2] + bg1[2 * h2]);
-          const float p1 = (acc[a + 2][b][2 * h2 + 1] + bh1[2 * h2 + 1]) * gelu_erf(acc[a + 3][b][2 * h2 + 1] + bg1[2 * h2 + 1]);
+          const f32x2 go = gelu_erf2(f32x2{acc[a + 1][b][2 * h2] + bg0[2 * h2], acc[a + 1][b][2 * h2 + 1] + bg0[2 * h2 + 1]});
+          const f32x2 gp = gelu_erf2(f32x2{acc[a + 3][b][2 * h2] + bg1[2 * h2], acc[a + 3][b][2 * h2 + 1] + bg1[2 * h2 + 1]});
+          const float o0 = (acc[a][b][2 * h2] + bh0[2 * h2]) * go[0];
+          const float o1 = (acc[a][b][2 * h2 + 1] + bh0[2 * h2 + 1]) * go[1];
+          const float p0 = (acc[a + 2][b][2 * h2] + bh1[2 * h2]) * gp[0];
+          const float p1 = (acc[a + 2][b][2 * h2 + 1] + bh1[2 * h2 + 1]) * gp[1];
           auto r = __builtin_amdgcn_permlane16_swap(pack2(o0, o1), pack2(p0, p1), false, false);
           x[h2] = r[0];
           y[h2] = r[1];
@@ -748,8 +807,12 @@ __device__ __forceinline__ int epi_fast(const vd_gemm_desc& d, f32x4 (&acc)[NB][
       for (int b = 0; b < MB; ++b) {
         const int m = mbase + b * 16 + fr;
         float o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = (acc[a][b][j] + bh[j]) * gelu_erf(acc[a + 1][b][j] + bg[j]);
+        const f32x2 g01 = gelu_erf2(f32x2{acc[a + 1][b][0] + bg[0], acc[a + 1][b][1] + bg[1]});
+        const f32x2 g23 = gelu_erf2(f32x2{acc[a + 1][b][2] + bg[2], acc[a + 1][b][3] + bg[3]});
+        o[0] = (acc[a][b][0] + bh[0]) * g01[0];
+        o[1] = (acc[a][b][1] + bh[1]) * g01[1];
+        o[2] = (acc[a][b][2] + bh[2]) * g23[0];
+        o[3] = (acc[a][b][3] + bh[3]) * g23[1];
         const bool ok = m < M && 2 * nout < N;
         const uint32_t off = ok ? (uint32_t)(m * ldc + nout) * 2u : G2_OOB;
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])}, ro, off, 0, 0);
@@ -1831,7 +1894,7 @@ int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   else
     hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
   int rc = vd_launch_status();
-  if (rc != VD_OK || split == 1) return rc;
+  if (rc != VD_OK || split == 1 || d.tile_cnt) return rc;  // tile counters: reduced in the kernel
   const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
   const int64_t blocks = (work + 255) / 256;
   hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, d, split);
@@ -2156,6 +2219,15 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   }
   const Plan p = plan(d);
   if (p.ver >= 2 && p.split > 1) VD_CHECK_ARG(d.ws && al16(d.ws) && d.ws_bytes >= p.ws_bytes);
+  if (d.tile_cnt) {  // in-kernel split-K reduction: v2 only, one counter per output tile
+    VD_CHECK_ARG(((uintptr_t)d.tile_cnt & 3) == 0);
+    const int64_t tiles = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + p.bn - 1) / p.bn);
+    if (p.ver != 2 || p.split == 1 || tiles > d.tile_cnt_len) {
+      vd_gemm_desc g = d;
+      g.tile_cnt = nullptr;
+      return vd_gemm(&g, stream);
+    }
+  }
   if (d.ln_out && !p.ln_fused) {  // the GEMM, then vd_layernorm over its output
     vd_gemm_desc g = d;
     g.ln_out = nullptr;
