@@ -1286,12 +1286,18 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
       return vd_launch_status();
     }
   }
-  if (sq >= 1024 && D <= 40) {
-    const dim3 grid((unsigned)((sq + 255) / 256), (unsigned)heads, (unsigned)batch);
-    hipLaunchKernelGGL((flash_attn_kernel<D, 4>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                       (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv,
-                       kv_div, c, out_f32);
-  } else {
+  // (QBLK 4 only for D <= 40: wider heads' QBLK-4 instances spill 94-280 VGPRs, so they are
+  // not instantiated at all)
+  if constexpr (D <= 40) {
+    if (sq >= 1024) {
+      const dim3 grid((unsigned)((sq + 255) / 256), (unsigned)heads, (unsigned)batch);
+      hipLaunchKernelGGL((flash_attn_kernel<D, 4>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                         (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv,
+                         kv_div, c, out_f32);
+      return vd_launch_status();
+    }
+  }
+  {
     const dim3 grid((unsigned)((sq + 127) / 128), (unsigned)heads, (unsigned)batch);
     hipLaunchKernelGGL((flash_attn_kernel<D, 2>), grid, dim3(NT), 0, s, (const bf16_t*)q, ldq,
                        (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv,

@@ -54,11 +54,15 @@ _SYNC = {}
 
 def _sync_counters(device):
     """One zeroed int32 array per device for the kernels' in-launch hand-offs (GEMM split-K tile
-    counters): every launch leaves its counters zero again, so the array serves every call."""
-    buf = _SYNC.get(device)
+    counters): every launch leaves its counters zero again, so the array serves every call
+    stream-ordered.  (No two GEMMs run concurrently in this product: the chunked temporal window
+    runs all its GEMMs on its one side stream.  The array is made by the eager priming step, so
+    a captured graph adds no node for it.)"""
+    key = device
+    buf = _SYNC.get(key)
     if buf is None:
         buf = torch.zeros(1 << 16, device=device, dtype=torch.int32)
-        _SYNC[device] = buf
+        _SYNC[key] = buf
     return buf
 
 
@@ -286,11 +290,13 @@ _GN_COUNTERS = {}
 
 def _gn_counters(device, n):
     """Arrival / departure counters of vd_gn_fused: zero on entry and left zero by every launch,
-    so one zeroed array per device serves every call (stream-ordered)."""
-    buf = _GN_COUNTERS.get(device)
+    so one zeroed array per device serves every call (stream-ordered; GroupNorms run on the
+    step's main stream only)."""
+    key = device
+    buf = _GN_COUNTERS.get(key)
     if buf is None or buf.numel() < 2 * n:
         buf = torch.zeros(max(2 * n, 4096), device=device, dtype=torch.int32)
-        _GN_COUNTERS[device] = buf
+        _GN_COUNTERS[key] = buf
     return buf
 
 
