@@ -179,4 +179,6 @@ def test_tiny_module_path_matches_oracle(cuda):
     out, rec, _ = trace(unet, 99, torch.cat([lat, lat]), 961, encoder_hidden_states=ehs)
     err = rel_l2(out.sample, torch.from_numpy(gold["eps_t961"]))
     print(f"tiny module path vs fp32 oracle: rel-L2 {err:.5f} ({len(rec)} modules)")
-    assert err < 0.03, err
+    # measured 0.0182 (the hooked module path rounds every module output to bf16, the fused
+    # product path 0.0137): 1.3x headroom
+    assert err < 0.024, err
