@@ -117,13 +117,6 @@ typedef struct vd_gemm_desc {
    * summation order bit for bit (tests/test_gpu_dist2.py). */
   int32_t path;
   int64_t plan_m;
-  /* Optional split-K tile counters (round 4): tile_cnt_len int32, ZERO on entry and left zero by
-   * every call (a zeroed array serves every call on a stream).  When given, a split-K launch of
-   * the v2 kernel reduces in the kernel — each output tile's last-arriving K slice sums the fp32
-   * slabs in slice order (the reduce kernel's order: the same bits) and runs the epilogue — and no
-   * reduce launch follows.  NULL: slabs + the reduce kernel. */
-  int32_t* tile_cnt;
-  int64_t tile_cnt_len;
 } vd_gemm_desc;
 
 int vd_gemm(const vd_gemm_desc* d, vd_stream_t stream);
@@ -167,21 +160,6 @@ int vd_gn_apply_g(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int6
                   int32_t n_split_total, int32_t groups, float eps, const float* gamma,
                   const float* beta, int32_t silu, void* y, int64_t ldy, int64_t rows_per_blk,
                   vd_stream_t stream);
-
-/* One-launch GroupNorm(+SiLU) of image instances (round 4; ResnetBlock2D / Transformer2DModel norms):
- * the workgroups of an image each publish their rows' group statistics, wait (bounded) for the
- * image's other blocks through an arrival counter, merge the records and apply to their own rows.
- * rows_per_blk: rows per workgroup (ceil(pix_per_inst / rows_per_blk) <= 16 blocks per image);
- * records: n_inst * blocks * groups float2 workspace (no initialisation needed); counters: 2 *
- * n_inst int32 that are ZERO on entry and left zero on exit (a zeroed array can be reused by every
- * call on a stream).  groups <= 32, 256 % groups == 0, C <= 2560.  Equal to vd_gn_partial_g +
- * vd_gn_apply_g with splits = blocks up to fp32 rounding; a wait that times out (a grid beyond
- * the resident capacity) recomputes the other blocks' records in the waiting block — the same
- * result, only slower. */
-int vd_gn_fused(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1, int64_t C,
-                int64_t n_inst, int64_t pix_per_inst, int32_t groups, float eps, const float* gamma,
-                const float* beta, int32_t silu, void* y, int64_t ldy, int64_t rows_per_blk, float* records,
-                int32_t* counters, vd_stream_t stream);
 
 /* ---------------------------------------------------------------- LayerNorm
  * BasicTransformerBlock.norm1/2/3 (eps 1e-5) over the last dim of bf16 rows,

@@ -159,4 +159,4 @@ def test_product_library_has_no_selector_state():
     data = [name for _, kind, name in syms if kind in "BDGRSV" and not name.startswith("__hip_cuid_")]
     assert data == [], data
     fields = [f for f, _ in L.GemmDesc._fields_]
-    assert fields[-4:] == ["path", "plan_m", "tile_cnt", "tile_cnt_len"]
+    assert fields[-2:] == ["path", "plan_m"]

@@ -331,11 +331,12 @@ def test_gemm_splitk_dense(cuda):
 
 
 @pytest.mark.parametrize("case", ["dense", "dense_f32_silu", "geglu", "conv", "conv_concat_rowbias"])
-def test_gemm_splitk_in_kernel_reduction_bit_identical(cuda, case):
-    """Round 4: split-K launches of the v2 kernel reduce in the kernel (the tile's last K slice
-    sums the slabs in slice order and runs the epilogue; vd_gemm_desc.tile_cnt) instead of the
-    reduce launch — the same bits as slabs + gemm_splitk_reduce, twice in a row (the counters are
-    left zero), and the fp64 reference to bf16 / fp32 tolerance."""
+def test_gemm_splitk_deterministic(cuda, case):
+    """Split-K launches (slabs + gemm_splitk_reduce, which applies every epilogue form) at the
+    shapes of a 2-frame rank: the fp64 reference to bf16 / fp32 tolerance, and the same bits run
+    after run (fixed slice order, no atomics).  (Round 4 tried reducing in the v2 kernel — the
+    tile's last K slice summing the slabs — and measured it slower at every such shape,
+    profiles/r04_gemm_splitk_inkernel_refuted.txt; it is gone.)"""
     torch.manual_seed(17)
     if case.startswith("conv"):
         n, h, w, ci, co = 4, 16, 16, 640, 640           # level 3 at 2 frames per rank: 32 tiles -> split
@@ -369,12 +370,9 @@ def test_gemm_splitk_in_kernel_reduction_bit_identical(cuda, case):
             def run():
                 return ops.gemm(a, wm, bias=b, act=ops.ACT_SILU, out_f32=True)
             want = F.silu(a.double() @ wm.double().T + b.double())
-    with ops.gemm_plan(tile_counters=False):
-        ref = run()
+    ref = run()
     got, again = run(), run()
     assert torch.equal(got, ref) and torch.equal(again, ref)
-    torch.cuda.synchronize()
-    assert all(int(c.abs().sum()) == 0 for c in ops._SYNC.values())
     if ref.dtype == torch.float32:
         close_f32(got, want, rtol=1e-3, atol=1e-3)
     else:
@@ -542,51 +540,6 @@ def test_group_norm_paths(cuda, n_inst, pix, C, c0, silu, path):
     want = F.group_norm(t, 32, g.double(), be.double(), 1e-6)
     want = (F.silu(want) if silu else want).permute(0, 2, 1).reshape(-1, C)
     close_bf16(got, want)
-
-
-@pytest.mark.parametrize("n_inst,pix,c0,c1,silu", [(4, 4096, 320, 0, True), (3, 1024, 640, 0, False),
-                                                  (2, 256, 1280, 1280, True), (5, 64, 1280, 640, True),
-                                                  (2, 4096, 64, 64, True), (1, 100, 64, 0, False),
-                                                  (32, 4096, 320, 0, True)])
-def test_group_norm_fused(cuda, n_inst, pix, c0, c1, silu):
-    """The one-launch GroupNorm (vd_gn_fused, round 4): blocks of an image publish their group
-    records, wait for each other and apply — UNet image shapes (level 1 at 2 and 16 frames, the
-    up-block concat at levels 3/4, the tiny config's 2 channels per group, a ragged last block)
-    against fp64 F.group_norm(+SiLU); the product dispatch (ops.group_norm) takes this form; the
-    counters are left zero."""
-    torch.manual_seed(n_inst + pix + c0)
-    x0 = rnd(n_inst * pix, c0) * 1.5 + 0.7
-    x1 = rnd(n_inst * pix, c1) * 0.5 - 0.2 if c1 else None
-    C = c0 + c1
-    g, b = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda) * 0.2
-    rows = ops.gn_fused_plan(n_inst, pix, C, 32)
-    assert rows is not None
-    got = ops.group_norm_fused(x0, n_inst, pix, 32, 1e-5, g, b, silu=silu, x1=x1)
-    assert torch.equal(got, ops.group_norm(x0, n_inst, pix, 32, 1e-5, g, b, silu=silu, x1=x1))
-    xx = x0 if x1 is None else torch.cat([x0, x1], 1)
-    t = xx.double().reshape(n_inst, pix, C).permute(0, 2, 1)
-    want = F.group_norm(t, 32, g.double(), b.double(), 1e-5)
-    want = (F.silu(want) if silu else want).permute(0, 2, 1).reshape(-1, C)
-    close_bf16(got, want)
-    torch.cuda.synchronize()
-    assert all(int(c.abs().sum()) == 0 for c in ops._GN_COUNTERS.values())
-
-
-def test_group_norm_fused_oversize_grid_falls_back_bit_identically(cuda):
-    """A grid far beyond the resident capacity (1024 images x 4 blocks): blocks waiting for blocks
-    that cannot be resident time out and recompute the missing records themselves with the same
-    function — no hang, and the output equals the same images normalised in small launches bit
-    for bit."""
-    n_inst, pix, C = 1024, 4096, 64
-    x = rnd(n_inst * pix, C) * 2 + 0.1
-    g, b = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda)
-    rows = 1024
-    big = ops.group_norm_fused(x, n_inst, pix, 32, 1e-6, g, b, silu=True, rows_per_blk=rows)
-    parts = [ops.group_norm_fused(x[i * pix:(i + 64) * pix], 64, pix, 32, 1e-6, g, b, silu=True, rows_per_blk=rows)
-             for i in range(0, n_inst, 64)]
-    assert torch.equal(big, torch.cat(parts))
-    torch.cuda.synchronize()
-    assert all(int(c.abs().sum()) == 0 for c in ops._GN_COUNTERS.values())
 
 
 @pytest.mark.parametrize("C,rows", [(320, 4 * 16 * 24 + 5), (640, 1000), (1280, 333), (64, 77), (128, 301),

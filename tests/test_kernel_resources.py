@@ -62,7 +62,7 @@ def _kernels(tmp_path):
 def test_no_hot_kernel_spills_registers(tmp_path):
     ks = _kernels(tmp_path)
     # one bundle per translation unit: the GEMM, norm and attention kernels are all present
-    for fam in ("gemm2_kernel", "gemm3_kernel", "gemm4_kernel", "gn_fused_kernel", "flash40_kernel"):
+    for fam in ("gemm2_kernel", "gemm3_kernel", "gemm4_kernel", "gn_apply_g_kernel", "flash40_kernel"):
         assert any(fam in k for k in ks), f"{fam} not found in the code objects"
     bad = []
     for name, r in ks.items():

@@ -448,16 +448,12 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // after the barrier (sched_barrier), then k-step 1's reads interleave one per two of k-step 0's
 // MFMAs (sched_group_barrier), so the MFMA chain waits on counted lgkmcnt only (52.79 vs 53.50
 // ms/step for the unpinned order, 53.11 with all reads ahead; profiles/r02f_fragment_order.txt).
-// SKR: split-K reduced in the kernel through d.tile_cnt (its own instance: the hand-off code's
-// registers pushed the split == 1 instance from ~50 to ~160 spilled SGPRs, round 4)
-template <int BN, int MODE, bool SKR>
+template <int BN, int MODE>
 __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                          uint32_t a1_bytes, uint32_t w_bytes,
                                                          int split) {
   using C = G2<BN>;
-  // (+16 B: the split-K "last arriver" flag, inside the one LDS array — a second __shared__
-  // object can make hipcc drain vmcnt before every k-step's fragment reads)
-  __shared__ __attribute__((aligned(1024))) char smem[G2_STAGES * C::STAGE + 16];
+  __shared__ __attribute__((aligned(1024))) char smem[G2_STAGES * C::STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
@@ -671,66 +667,10 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     if (++ckt == ckt1) {  // unit finished: epilogue (its memory ops precede the next DMA)
       const int tile = cu / split, sp = cu % split;
       const int64_t m0 = (int64_t)(tile / tiles_n) * G2_BM, n0 = (int64_t)(tile % tiles_n) * BN;
-      // ONE epilogue call site: a second inlined gemm_epilogue (in the in-kernel reduction's
-      // last-arriver branch) pushed the kernel past 256 VGPRs and spilled 88-171 of them to
-      // scratch — every v2 GEMM ran 2x slower (round 4, gpurun_out r04c)
-      bool epi = split == 1;
-      if (SKR && split != 1) {
-        // split-K reduced in the kernel (round 4): write-through (sc1) fp32 slab, drain, one lane
-        // takes a ticket on the tile's counter (relaxed, agent scope — the fence-free hand-off of
-        // cdna_hip_programming.md Guideline 16); the tile's last slice sums every slab in split
-        // order (gemm_splitk_reduce's order: bit-identical) with sc1 loads into acc, runs the
-        // epilogue and resets the counter, so no reduce launch follows.
-        const __amdgpu_buffer_rsrc_t rws =
-            __builtin_amdgcn_make_buffer_rsrc(d.ws, 0, (uint32_t)((int64_t)split * M * N * 4), 0x00020000);
-        const int mrow = (int)m0 + wm * 64 + fr, ncol = (int)n0 + 4 * fq;
-        const uint32_t slab_b = (uint32_t)(M * N * 4);
-#pragma unroll
-        for (int a = 0; a < C::NB; ++a) {
-          const int n = ncol + (a == C::NB - 1 ? wodd : wcb + a * 16);
-#pragma unroll
-          for (int b = 0; b < C::MB; ++b) {
-            const int m = mrow + b * 16;
-            const uint32_t o = (n < (int)N && m < (int)M) ? (uint32_t)(sp * slab_b + ((uint32_t)m * (uint32_t)N + n) * 4) : G2_OOB;
-            __builtin_amdgcn_raw_buffer_store_b128(
-                u32x4{__float_as_uint(acc[a][b][0]), __float_as_uint(acc[a][b][1]), __float_as_uint(acc[a][b][2]),
-                      __float_as_uint(acc[a][b][3])},
-                rws, o, 0, 16);
-          }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-        __syncthreads();
-        int* last_flag = (int*)(smem + G2_STAGES * C::STAGE);
-        if (tid == 0) {
-          const int prev = __hip_atomic_fetch_add(d.tile_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const int last = prev == split - 1;
-          if (last) __hip_atomic_store(d.tile_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          *last_flag = last;
-        }
-        __syncthreads();
-        epi = *last_flag != 0;
-        if (epi) {
-#pragma unroll
-          for (int a = 0; a < C::NB; ++a)
-#pragma unroll
-            for (int b = 0; b < C::MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-          for (int s2 = 0; s2 < split; ++s2) {
-#pragma unroll
-            for (int a = 0; a < C::NB; ++a) {
-              const int n = ncol + (a == C::NB - 1 ? wodd : wcb + a * 16);
-#pragma unroll
-              for (int b = 0; b < C::MB; ++b) {
-                const int m = mrow + b * 16;
-                const uint32_t o =
-                    (n < (int)N && m < (int)M) ? (uint32_t)(s2 * slab_b + ((uint32_t)m * (uint32_t)N + n) * 4) : G2_OOB;
-                const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rws, o, 0, 16);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[a][b][j] += __uint_as_float(u[j]);
-              }
-            }
-          }
-        }
-      } else if (split != 1) {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
+      if (split == 1) {
+        gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::MB * 16, (int)n0 + wcb, lane,
+                                    ODDMAP ? (int)n0 + wodd : -1);
+      } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
         float* slab = (float*)d.ws + (int64_t)sp * M * N;
 #pragma unroll
         for (int a = 0; a < C::NB; ++a) {
@@ -744,9 +684,6 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
           }
         }
       }
-      if (epi)
-        gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::MB * 16, (int)n0 + wcb, lane,
-                                    ODDMAP ? (int)n0 + wodd : -1);
 #pragma unroll
       for (int a = 0; a < C::NB; ++a)
 #pragma unroll
@@ -1904,20 +1841,12 @@ int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   // persistent: one workgroup per CU, ceil(units / grid) rounds, balanced grid
   const int64_t rounds = (units + g_num_cus - 1) / g_num_cus;
   const int64_t grid = (units + rounds - 1) / rounds;
-  const bool skr = split > 1 && d.tile_cnt;
-  if (d.a_mode == VD_A_CONV3X3) {
-    if (skr)
-      hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3, true>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
-    else
-      hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3, false>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
-  } else {
-    if (skr)
-      hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE, true>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
-    else
-      hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE, false>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
-  }
+  if (d.a_mode == VD_A_CONV3X3)
+    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
+  else
+    hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
   int rc = vd_launch_status();
-  if (rc != VD_OK || split == 1 || skr) return rc;  // tile counters: reduced in the kernel
+  if (rc != VD_OK || split == 1) return rc;
   const int64_t work = d.M * ((d.act == VD_ACT_GEGLU ? d.N / 2 : d.N) / 4);
   const int64_t blocks = (work + 255) / 256;
   hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, d, split);
@@ -2242,16 +2171,6 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   }
   const Plan p = plan(d);
   if (p.ver >= 2 && p.split > 1) VD_CHECK_ARG(d.ws && al16(d.ws) && d.ws_bytes >= p.ws_bytes);
-  if (d.tile_cnt) {  // in-kernel split-K reduction: v2 only, one counter per output tile
-    VD_CHECK_ARG(((uintptr_t)d.tile_cnt & 3) == 0);
-    const int64_t tiles = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + p.bn - 1) / p.bn);
-    // (the slabs' byte offsets are 32-bit and must stay below the OOB marker G2_OOB)
-    if (p.ver != 2 || p.split == 1 || tiles > d.tile_cnt_len || p.split * d.M * d.N * 4 >= (int64_t)G2_OOB) {
-      vd_gemm_desc g = d;
-      g.tile_cnt = nullptr;
-      return vd_gemm(&g, stream);
-    }
-  }
   if (d.ln_out && !p.ln_fused) {  // the GEMM, then vd_layernorm over its output
     vd_gemm_desc g = d;
     g.ln_out = nullptr;

@@ -474,244 +474,6 @@ __global__ __launch_bounds__(NT) void layernorm_rows_kernel(const bf16_t* x, int
   }
 }
 
-
-// ---------------------------------------------------------------- one-launch GroupNorm (round 4)
-// Image-instance GroupNorm(+SiLU) in ONE launch: workgroup (inst, blk) owns rows_per_blk rows of
-// one image.  (1) It computes its rows' group statistics {mean, M2} (per-lane shifted sums,
-// Chan-merged over pixel lanes, then the channels of a group with their equal counts) and
-// publishes them as write-through (sc1) stores; (2) one lane adds to the instance's arrival
-// counter (relaxed, agent scope: the fence-free hand-off of cdna_hip_programming.md Guideline
-// 16) and polls it, with a bounded spin, until every block of the image has arrived; (3) it
-// reads the image's bpi x groups records (sc1 loads), merges them in block order, and (4)
-// applies y = (x - mean) rstd gamma + beta (+SiLU) to its own rows, which it read moments ago
-// (L2 / MALL-resident).  Against the two-launch partial + apply pair this drops a launch per
-// norm.  Correctness never depends on co-residency: a block whose wait times out (200 us — a
-// grid larger than the resident capacity, or another process's kernel holding the CUs)
-// recomputes the missing records itself with the same function, so its result is identical.
-// The last block to leave resets the instance's two counters (arrive, depart), so a zeroed
-// counter array stays zeroed between launches.  bpi and rows_per_blk are functions of the
-// image size alone, so frame-sharded ranks normalise their images bit-identically to the
-// unsharded run.
-typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
-constexpr int GNF_RMAX = 16;      // blocks per instance
-constexpr int GNF_GMAX = 32;      // groups
-constexpr int GNF_BUF = GN_CMAX;  // float2 slots: per-lane records (<= NT * 8) / per-channel / {a, b}
-
-// {mean, M2} of rows [row0, row0 + nrows) for each group, into gout[g] (LDS); n = nrows * cpg.
-__device__ __forceinline__ void gnf_block_stats(const bf16_t* x0, int64_t ldx0, int c0, const bf16_t* x1,
-                                                int64_t ldx1, int C, int64_t row0, int nrows, int groups,
-                                                float2* buf, float2* gout) {
-  const int tid = threadIdx.x;
-  const int nch = C / 8;
-  const int PL = nch >= NT ? 1 : NT / nch;
-  for (int task = tid; task < PL * nch; task += NT) {
-    const int pl = task / nch, j = task - pl * nch;
-    float s1[8], s2[8], sh[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; sh[e] = 0.f; }
-    int cnt = 0;
-    int p = pl;
-    if (p < nrows) {
-      float f[8];
-      unpack8(*(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row0 + p, (int64_t)j * 8), f);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sh[e] = f[e];
-      cnt = 1;
-      p += PL;
-    }
-    for (; p + 3 * PL < nrows; p += 4 * PL) {
-      uint4 u[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) u[r] = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row0 + p + r * PL, (int64_t)j * 8);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float f[8];
-        unpack8(u[r], f);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float t = f[e] - sh[e];
-          s1[e] += t;
-          s2[e] = fmaf(t, t, s2[e]);
-        }
-      }
-      cnt += 4;
-    }
-    for (; p < nrows; p += PL) {
-      float f[8];
-      unpack8(*(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row0 + p, (int64_t)j * 8), f);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float t = f[e] - sh[e];
-        s1[e] += t;
-        s2[e] = fmaf(t, t, s2[e]);
-      }
-      ++cnt;
-    }
-    const float n = (float)cnt;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float mean = cnt ? sh[e] + s1[e] / n : 0.f;
-      const float m2 = cnt ? fmaxf(s2[e] - s1[e] * s1[e] / n, 0.f) : 0.f;
-      buf[task * 8 + e] = make_float2(mean, m2);  // PL == 1: task == j, so this IS the channel record
-    }
-  }
-  __syncthreads();
-  if (PL > 1) {  // Chan-merge the PL pixel lanes of each channel (lane q holds ceil((nrows - q) / PL) rows)
-    constexpr int CPT = (GN_CMAX + NT - 1) / NT;
-    float2 v[CPT];
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int c = tid + k * NT;
-      if (c >= C) break;
-      const int jj = c >> 3, e = c & 7;
-      float n = 0.f, mean = 0.f, m2 = 0.f;
-      for (int q = 0; q < PL; ++q) {
-        const int cq = q < nrows ? (nrows - q + PL - 1) / PL : 0;
-        const float2 r = buf[(q * nch + jj) * 8 + e];
-        chan_merge(n, mean, m2, (float)cq, r.x, r.y);
-      }
-      v[k] = make_float2(mean, m2);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int c = tid + k * NT;
-      if (c >= C) break;
-      buf[c] = v[k];
-    }
-    __syncthreads();
-  }
-  // channels of a group, equal counts n = nrows: mean_g = avg(mean_c), M2_g = sum(M2_c + n (mean_c - mean_g)^2);
-  // tpg consecutive lanes per group, fixed xor-shuffle trees (deterministic)
-  const int tpg = NT / groups, cpg = C / groups;
-  const int g = tid / tpg, sub = tid % tpg;
-  float sm = 0.f;
-  for (int q = sub; q < cpg; q += tpg) sm += buf[g * cpg + q].x;
-  for (int o = 1; o < tpg; o <<= 1) sm += __shfl_xor(sm, o, 64);
-  const float mg = sm / (float)cpg;
-  float sq = 0.f;
-  for (int q = sub; q < cpg; q += tpg) {
-    const float2 r = buf[g * cpg + q];
-    const float dlt = r.x - mg;
-    sq += r.y + (float)nrows * dlt * dlt;
-  }
-  for (int o = 1; o < tpg; o <<= 1) sq += __shfl_xor(sq, o, 64);
-  if (sub == 0) gout[g] = make_float2(mg, sq);
-  __syncthreads();
-}
-
-__global__ __launch_bounds__(NT) void gn_fused_kernel(const bf16_t* x0, int64_t ldx0, int c0, const bf16_t* x1,
-                                                      int64_t ldx1, int C, int pix_per_inst, int rows_per_blk,
-                                                      int bpi, int groups, float eps, const float* gamma,
-                                                      const float* beta, int silu, bf16_t* y, int64_t ldy,
-                                                      float2* rec, int* cnt) {
-  __shared__ float2 buf[GNF_BUF];
-  __shared__ float2 recs[GNF_RMAX * GNF_GMAX];
-  __shared__ float2 gst[GNF_GMAX];
-  __shared__ int flag;
-  const int tid = threadIdx.x;
-  const int inst = blockIdx.x / bpi, blk = blockIdx.x % bpi;
-  const int64_t ibase = (int64_t)inst * pix_per_inst;
-  auto blk_rows = [&](int b) { return min(pix_per_inst, (b + 1) * rows_per_blk) - b * rows_per_blk; };
-  const int nrows = blk_rows(blk);
-  // (1) this block's group records, published write-through
-  gnf_block_stats(x0, ldx0, c0, x1, ldx1, C, ibase + (int64_t)blk * rows_per_blk, nrows, groups, buf,
-                  recs + blk * groups);
-  const __amdgpu_buffer_rsrc_t rr =
-      __builtin_amdgcn_make_buffer_rsrc(rec + (int64_t)inst * bpi * groups, 0, bpi * groups * 8, 0x00020000);
-  if (tid < groups) {
-    const float2 r = recs[blk * groups + tid];
-    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(r.x), __float_as_uint(r.y)}, rr,
-                                          (uint32_t)((blk * groups + tid) * 8), 0, 16);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  // (2) arrive, then wait (bounded) for the image's other blocks
-  int* arrive = cnt + 2 * inst;
-  if (tid == 0) {
-    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    int ok = 1;
-    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < bpi) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 20000) { ok = 0; break; }  // 200 us
-      __builtin_amdgcn_s_sleep(2);
-    }
-    flag = ok;
-  }
-  __syncthreads();
-  // (3) every block's records: sc1 loads, or (timeout) recomputed here with the same function
-  if (flag) {
-    for (int i = tid; i < bpi * groups; i += NT) {
-      if (i / groups == blk) continue;
-      const u32x2 u = __builtin_amdgcn_raw_buffer_load_b64(rr, (uint32_t)(i * 8), 0, 16);
-      recs[i] = make_float2(__uint_as_float(u[0]), __uint_as_float(u[1]));
-    }
-  } else {
-    for (int b = 0; b < bpi; ++b)
-      if (b != blk)
-        gnf_block_stats(x0, ldx0, c0, x1, ldx1, C, ibase + (int64_t)b * rows_per_blk, blk_rows(b), groups, buf,
-                        recs + b * groups);
-  }
-  __syncthreads();
-  if (tid == 0) {  // leave: the last block out resets the counters (all have arrived and passed the wait)
-    const int prev = __hip_atomic_fetch_add(arrive + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == bpi - 1) {
-      __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(arrive + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  const int cpg = C / groups;
-  if (tid < groups) {  // Chan-merge the image's blocks in block order
-    float n = 0.f, mean = 0.f, m2 = 0.f;
-    for (int b = 0; b < bpi; ++b) {
-      const float2 r = recs[b * groups + tid];
-      chan_merge(n, mean, m2, (float)(blk_rows(b) * cpg), r.x, r.y);
-    }
-    const float var = n > 0.f ? m2 / n : 0.f;
-    gst[tid] = make_float2(mean, rsqrtf(var + eps));
-  }
-  __syncthreads();
-  for (int c = tid; c < C; c += NT) {
-    const float2 st = gst[c / cpg];
-    const float a = st.y * gamma[c];
-    buf[c] = make_float2(a, beta[c] - st.x * a);
-  }
-  __syncthreads();
-  // (4) apply to this block's rows
-  const int nch = C / 8;
-  const int64_t r0 = ibase + (int64_t)blk * rows_per_blk;
-  const int total = nrows * nch;
-  constexpr int U = 4;
-  for (int base = tid; base < total; base += U * NT) {
-    uint4 u[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int idx = base + k * NT;
-      const int q = idx / nch, r = idx - q * nch;
-      if (idx < total) u[k] = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, r0 + q, (int64_t)r * 8);
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int idx = base + k * NT;
-      if (idx >= total) break;
-      const int q = idx / nch, r = idx - q * nch;
-      const int64_t c = (int64_t)r * 8;
-      float f[8];
-      unpack8(u[k], f);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float2 t = buf[c + e];
-        f[e] = fmaf(f[e], t.x, t.y);
-      }
-      if (silu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = silu_f(f[e]);
-      }
-      *(uint4*)(y + (r0 + q) * ldy + c) = pack8(f);
-    }
-  }
-}
-
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
@@ -759,26 +521,6 @@ extern "C" int vd_gn_apply_g(const void* x0, int64_t ldx0, int64_t c0, const voi
   hipLaunchKernelGGL(gn_apply_g_kernel, dim3((unsigned)(n_inst * bpi)), dim3(NT), 0, (hipStream_t)stream,
                      (const bf16_t*)x0, ldx0, c0, (const bf16_t*)x1, ldx1, C, pix_per_inst, rows_per_blk, (int)bpi,
                      (const float4*)ws, n_split_total, groups, eps, gamma, beta, silu, (bf16_t*)y, ldy);
-  return vd_launch_status();
-}
-
-extern "C" int vd_gn_fused(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1, int64_t C,
-                           int64_t n_inst, int64_t pix_per_inst, int32_t groups, float eps, const float* gamma,
-                           const float* beta, int32_t silu, void* y, int64_t ldy, int64_t rows_per_blk,
-                           float* records, int32_t* counters, vd_stream_t stream) {
-  VD_CHECK_ARG(x0 && y && gamma && beta && records && counters && C > 0 && C % 8 == 0 && C <= GN_CMAX);
-  VD_CHECK_ARG(c0 % 8 == 0 && c0 > 0 && c0 <= C && groups > 0 && groups <= GNF_GMAX && NT % groups == 0 &&
-               C % groups == 0);
-  VD_CHECK_ARG(ldx0 % 8 == 0 && ldy % 8 == 0 && al16(x0) && al16(y) && ((uintptr_t)records & 7) == 0 &&
-               ((uintptr_t)counters & 3) == 0);
-  if (c0 < C) VD_CHECK_ARG(x1 && ldx1 % 8 == 0 && al16(x1));
-  VD_CHECK_ARG(n_inst > 0 && pix_per_inst > 0 && rows_per_blk > 0 && pix_per_inst < 0x40000000);
-  const int64_t bpi = (pix_per_inst + rows_per_blk - 1) / rows_per_blk;
-  VD_CHECK_ARG(bpi <= GNF_RMAX && rows_per_blk * (C / 8) < 0x7fffffff && n_inst * bpi < 0x7fffffff);
-  hipLaunchKernelGGL(gn_fused_kernel, dim3((unsigned)(n_inst * bpi)), dim3(NT), 0, (hipStream_t)stream,
-                     (const bf16_t*)x0, ldx0, (int)c0, (const bf16_t*)x1, ldx1, (int)C, (int)pix_per_inst,
-                     (int)rows_per_blk, (int)bpi, groups, eps, gamma, beta, silu, (bf16_t*)y, ldy, (float2*)records,
-                     counters);
   return vd_launch_status();
 }
 

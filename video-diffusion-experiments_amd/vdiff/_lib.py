@@ -32,8 +32,6 @@ SIGNATURES = {
     "vd_gn_apply": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_i64, c_vp], c_i32),
     "vd_gn_partial_g": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp], c_i32),
     "vd_gn_apply_g": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64, c_i64, c_vp], c_i32),
-    "vd_gn_fused": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64,
-                     c_i64, c_vp, c_vp, c_vp], c_i32),
     "vd_layernorm": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
     "vd_attention": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_i64, c_f32, c_vp], c_i32),
     "vd_attention_f32": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_i64, c_f32, c_vp], c_i32),
@@ -92,7 +90,6 @@ class GemmDesc(C.Structure):
         ("ln_pe", c_vp), ("ln_pe_div", c_i64), ("ln_pe_period", c_i64),
         ("ln_out", c_vp), ("ld_ln", c_i64),
         ("path", c_i32), ("plan_m", c_i64),
-        ("tile_cnt", c_vp), ("tile_cnt_len", c_i64),
     ]
 
 

@@ -46,44 +46,25 @@ def _rows(t, dtype=BF16):
 class _GemmPlan:
     path = 0       # vd_gemm_desc.path for the GEMMs issued (0 = the automatic plan)
     plan_div = 0   # > 0: plan every GEMM whose M it divides as if M were M / plan_div
-    tile_counters = True  # split-K reduced in the kernel (vd_gemm_desc.tile_cnt), no reduce launch
-
-
-_SYNC = {}
-
-
-def _sync_counters(device):
-    """One zeroed int32 array per device for the kernels' in-launch hand-offs (GEMM split-K tile
-    counters): every launch leaves its counters zero again, so the array serves every call
-    stream-ordered.  (No two GEMMs run concurrently in this product: the chunked temporal window
-    runs all its GEMMs on its one side stream.  The array is made by the eager priming step, so
-    a captured graph adds no node for it.)"""
-    key = device
-    buf = _SYNC.get(key)
-    if buf is None:
-        buf = torch.zeros(1 << 16, device=device, dtype=torch.int32)
-        _SYNC[key] = buf
-    return buf
 
 
 _PLAN = _GemmPlan()
 
 
 @contextlib.contextmanager
-def gemm_plan(path: int = 0, plan_div: int = 0, tile_counters: bool = True):
+def gemm_plan(path: int = 0, plan_div: int = 0):
     """Test / benchmark hook on the Python side only — the C ABI takes both values per call in
     vd_gemm_desc and keeps no state.  Inside the block every vd_gemm carries `path` (1 v1, 2 v2,
     3 v3, 5 v5, 6 v6: forced where that kernel takes the shape) and, with plan_div = N, plan_m =
     M / N for each GEMM whose M N divides: an unsharded model planned like one of N frame shards
     (same kernels, split-K and LayerNorm fusion, so the same summation order), which makes the
-    sharded-vs-unsharded comparison of tests/test_gpu_dist2.py bit-exact under the product plan.
-    tile_counters=False: split-K slabs + the reduce kernel instead of the in-kernel reduction."""
-    old = (_PLAN.path, _PLAN.plan_div, _PLAN.tile_counters)
-    _PLAN.path, _PLAN.plan_div, _PLAN.tile_counters = int(path), int(plan_div), bool(tile_counters)
+    sharded-vs-unsharded comparison of tests/test_gpu_dist2.py bit-exact under the product plan."""
+    old = (_PLAN.path, _PLAN.plan_div)
+    _PLAN.path, _PLAN.plan_div = int(path), int(plan_div)
     try:
         yield
     finally:
-        _PLAN.path, _PLAN.plan_div, _PLAN.tile_counters = old
+        _PLAN.path, _PLAN.plan_div = old
 
 
 def _run_gemm(d, device, what):
@@ -91,9 +72,6 @@ def _run_gemm(d, device, what):
     d.path = _PLAN.path
     if _PLAN.plan_div > 1 and d.M % _PLAN.plan_div == 0:
         d.plan_m = d.M // _PLAN.plan_div
-    if _PLAN.tile_counters:
-        cnt = _sync_counters(device)
-        d.tile_cnt, d.tile_cnt_len = cnt.data_ptr(), cnt.numel()
     nbytes = lib().vd_gemm_ws_bytes(C.byref(d))
     ws = None
     if nbytes > 0:
@@ -271,67 +249,17 @@ def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, ga
     Image instances always take the two-launch path, whose splits depend on the image size
     alone: a frame-sharded rank normalises its images bit-identically to the unsharded run
     (round 3; the four-launch path was 1-2 us faster on a 2-frame rank's few deep-level
-    instances, tools/gn_bench.py)."""
+    instances, tools/gn_bench.py).  A one-launch form (blocks waiting for their image's other
+    blocks on an arrival counter) was slower at every image norm of the step and is gone
+    (round 4, profiles/r04_gn_one_launch_refuted.txt)."""
     C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
     if two_pass and gather is None and C <= 2560 and 256 % groups == 0:
-        plan = gn_fused_plan(n_inst, pix, C, groups)
-        if plan is not None:
-            return group_norm_fused(x, n_inst, pix, groups, eps, gamma, beta, silu=silu, x1=x1, rows_per_blk=plan)
         return group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=silu, x1=x1)
     ws = gn_partial(x, C, n_inst, pix, n_split or gn_splits(n_inst, pix), x1=x1)
     if gather is not None:
         ws = gather(ws)
     ss = gn_finalize(ws, groups, eps, gamma, beta)
     return gn_apply(x, ss, pix, silu, x1=x1)
-
-
-_GN_COUNTERS = {}
-
-
-def _gn_counters(device, n):
-    """Arrival / departure counters of vd_gn_fused: zero on entry and left zero by every launch,
-    so one zeroed array per device serves every call (stream-ordered; GroupNorms run on the
-    step's main stream only)."""
-    key = device
-    buf = _GN_COUNTERS.get(key)
-    if buf is None or buf.numel() < 2 * n:
-        buf = torch.zeros(max(2 * n, 4096), device=device, dtype=torch.int32)
-        _GN_COUNTERS[key] = buf
-    return buf
-
-
-def gn_fused_plan(n_inst, pix, C, groups):
-    """rows per workgroup of the one-launch GroupNorm, or None where the two-launch form stays:
-    ~64K elements per block, <= 16 blocks per image — a function of the image size alone (frame
-    shards normalise bit-identically) — with the whole grid within 2 workgroups per CU (resident:
-    the blocks of an image wait for each other) and <= 512 KB per block (the VAE's 512^2 images
-    keep the two-launch pass over >1000 workgroups)."""
-    if groups > 32 or 256 % groups or C % groups or C > 2560:
-        return None
-    bpi = max(1, min(16, -(-pix * C // 65536)))
-    rows = -(-pix // bpi)
-    bpi = -(-pix // rows)
-    if n_inst * bpi > 512 or rows * C > 1 << 18:
-        return None
-    return rows
-
-
-def group_norm_fused(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, out=None, rows_per_blk=None):
-    """vd_gn_fused: GroupNorm(+SiLU) of image instances in one launch."""
-    _dev(x, x1, gamma, beta, out)
-    C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
-    rows = rows_per_blk or gn_fused_plan(n_inst, pix, C, groups)
-    if rows is None:
-        raise ValueError("shape outside the one-launch GroupNorm (use group_norm)")
-    bpi = -(-pix // rows)
-    rec = torch.empty(n_inst * bpi * groups * 2, device=x.device, dtype=torch.float32)
-    cnt = _gn_counters(x.device, n_inst)
-    if out is None:
-        out = torch.empty(x.shape[0], C, device=x.device, dtype=BF16)
-    x1p, ld1 = (_p(x1), _rows(x1)) if x1 is not None else (None, 0)
-    check(lib().vd_gn_fused(_p(x), _rows(x), x.shape[1], x1p, ld1, C, n_inst, pix, groups, eps, _p(gamma), _p(beta),
-                            int(silu), _p(out), _rows(out), rows, _p(rec), _p(cnt), _stream()), "vd_gn_fused")
-    return out
 
 
 def group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, out=None, n_split=None):
