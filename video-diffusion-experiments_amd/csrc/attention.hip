@@ -954,8 +954,8 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
       for (int i = 0; i < 16; ++i) oacc[db][qb][i] *= alpha;
     if (hh == C::MU_H) qf[qb][C::MU_KS][C::MU_J] = (__bf16)(-nmu);
   };
-  // flash32 tile_generic's decisions for tile t, taken right after QK^T(t) at the end of the M
-  // phase that computed S(t) (the lowest register pressure of the loop): the tile max on tile 0
+  // flash32 tile_generic's decisions for tile t, taken after QK^T(t) and before softmax(t) (at the
+  // start of tile t's V phase; the prologue's QK^T(0) for tile 0): the tile max on tile 0
   // (every tile on the exact pass), else the fast pass's row-sum check over tiles 0..t-1 (PV(t-1)
   // ran earlier in this phase) — the same values at the same point of the tile order as flash32
   auto decide = [&](int t) {
@@ -1017,7 +1017,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
         }
   };
   // M(t) = PV(t) then QK^T(t+1): d-block 1's V reads and key block 0's K' reads go out first,
-  // key block 1's under d-block 0's MFMAs; the decisions for tile t+1 follow its QK^T
+  // key block 1's under d-block 0's MFMAs
   auto mphase = [&](int t) {
     const bool more = t + 1 < T;
     // the M wave takes issue priority for its phase: its MFMAs go out every 32 cycles and the
@@ -1039,7 +1039,6 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
       qk(1);
     }
     __builtin_amdgcn_s_setprio(0);
-    if (more) decide(t + 1);
   };
   // tile u's DMA: issued at phase 2u-4 (u >= 2), waited for at the end of phase 2u-1
   auto issue = [&](int u) {
@@ -1070,6 +1069,12 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   bar();
   for (int t = 0; t < T; ++t) {
     if (!g0) issue(t + 3);
+    // tile t's decisions open its V phase (round 4; they closed the M phase that computed S(t)):
+    // the same data at the same point of the tile order — after QK^T(t), before softmax(t),
+    // PV(t) and QK^T(t+1) — but the M wave now reaches the barrier straight after its last MFMA
+    // issue instead of waiting out the MFMA latency and the VALU checks (stamps: 268 + 116 of the
+    // M phase's 2208 cycles), and the V wave has the slack (it waited 454-596 at the barrier)
+    if (t > 0) decide(t);
     softmax();
     __builtin_amdgcn_sched_barrier(0);
     read_v(t, 0);
