@@ -44,7 +44,8 @@ ROOF = "flash40_kernel<true>" if any("flash40_kernel<true>" in r["Kernel_Name"] 
 ins = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win if ROOF in r["Kernel_Name"]]
 ins = [x for x in ins if x > 300e3]
 if ins:
-    print(f"roofline kernel inside the step (L1 self-attention): {len(ins)} launches, avg {sum(ins) / len(ins) / 1e3:.1f} us")
+    print(f"roofline kernel inside the step (L1 self-attention): {len(ins)} launches, avg {sum(ins) / len(ins) / 1e3:.1f} us"
+          f" (min {min(ins) / 1e3:.1f}, max {max(ins) / 1e3:.1f})")
 
 # bench.py's roofline kernel: after the last step, time_attention() launches the L1
 # self-attention kernel (10 warm-up + attn_reps timed) on its own, first on model-scale inputs
@@ -71,4 +72,5 @@ for tag, part in zip(("the step's own operands = the bench line", "synthetic inp
     d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed]
     print(f"roofline kernel (bench time_attention, {tag}): {len(d)} timed launches of "
           f"{timed[0]['Kernel_Name'].replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0][:60]} "
-          f"grid={timed[0]['Grid_Size_X']}, avg {sum(d) / len(d) / 1e3:.1f} us")
+          f"grid={timed[0]['Grid_Size_X']}, avg {sum(d) / len(d) / 1e3:.1f} us "
+          f"(first 5 {sum(d[:5]) / 5e3:.1f}, last 5 {sum(d[-5:]) / 5e3:.1f}: back-to-back launches drift as the clock settles)")

@@ -12,7 +12,7 @@
 # usage (GPU box): bash tools/roofline_prof.sh r03a
 set -o pipefail
 R=$GRAFT_REPO_ROOT; ROUND=${1:-r03}
-OUT=$R/gpurun_out/roof_$ROUND; rm -rf $OUT; mkdir -p $OUT
+OUT=/tmp/vd_roof_$ROUND; rm -rf $OUT; mkdir -p $OUT  # raw traces stay on the box (gpurun copies back < 64 MiB)
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
@@ -24,6 +24,7 @@ ST=$(find $OUT/trace -name "*kernel_stats.csv" | head -1)
   python3 -c "import json,sys; r=json.load(open(sys.argv[1]))['roofline']; print('  roofline.avg_launch_ms', r['avg_launch_ms'], 'achieved', r['achieved'], 'TF/s frac', r['frac'], 'stress', r['stress'])" $OUT/bench_prof.json; } \
   > $R/gpurun_out/${ROUND}_roofline_trace.txt || exit 1
 cp $ST $R/gpurun_out/${ROUND}_kernel_stats.csv
+cp $OUT/bench_prof.json $R/gpurun_out/${ROUND}_bench_prof.json
 i=0
 for c in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
