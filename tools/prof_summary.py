@@ -73,4 +73,4 @@ for tag, part in zip(("the step's own operands = the bench line", "synthetic inp
     print(f"roofline kernel (bench time_attention, {tag}): {len(d)} timed launches of "
           f"{timed[0]['Kernel_Name'].replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0][:60]} "
           f"grid={timed[0]['Grid_Size_X']}, avg {sum(d) / len(d) / 1e3:.1f} us "
-          f"(first 5 {sum(d[:5]) / 5e3:.1f}, last 5 {sum(d[-5:]) / 5e3:.1f}: back-to-back launches drift as the clock settles)")
+          + (f"(first 5 {sum(d[:5]) / 5e3:.1f}, last 5 {sum(d[-5:]) / 5e3:.1f} us)" if len(d) >= 10 else ""))
