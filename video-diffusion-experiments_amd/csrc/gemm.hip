@@ -2057,9 +2057,12 @@ Plan plan(const vd_gemm_desc& d) {
   {
     const int64_t tiles6 = ((M + G6_BM - 1) / G6_BM) * ((d.N + G6_BN - 1) / G6_BN);
     const int64_t tiles256 = ((M + G2_BM - 1) / G2_BM) * ((d.N + 159) / 160);
+    // (round 4: also the L1 3x3 convs of a 2-frame rank, K = 2880 over >= 4 tiles per CU:
+    // 45.5 vs 50.2 us for v2's split-2 + reduce, tools/kbench.py at 4 images)
     const bool v6auto = tiles256 < g_num_cus && (d.N <= 1280 || tiles6 <= 4 * g_num_cus) &&
                         (d.act != VD_ACT_GEGLU || 2 * tiles256 <= g_num_cus) &&
-                        (d.K <= 1280 || (d.K <= 2560 && tiles6 >= 2 * g_num_cus));
+                        (d.K <= 1280 || (d.K <= 2560 && tiles6 >= 2 * g_num_cus) ||
+                         (d.a_mode == VD_A_CONV3X3 && d.K <= 2880 && tiles6 >= 4 * g_num_cus));
     if (path == 6 || (path == 0 && v6auto)) {
       p.ver = 6;
       p.bn = 64;

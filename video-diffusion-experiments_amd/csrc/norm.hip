@@ -60,7 +60,10 @@ __global__ __launch_bounds__(NT) void gn_partial_kernel(const bf16_t* x0, int64_
     for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; sh[e] = 0.f; }
     if (active) {
       // shift = the first pixel of this lane's run (shifted sums: no cancellation
-      // when |mean| >> std); then 4 independent 16-byte loads in flight per step
+      // when |mean| >> std); then U independent 16-byte loads in flight per step (round 4: 8 for
+      // the motion norm's per-channel records, 78.9 -> 68.6 us at L1; the group-record form keeps 4,
+      // whose 40 KB of LDS already caps it at 4 blocks per CU and 8 cost it one more: 51 -> 57 us)
+      constexpr int U = GREC ? 4 : 8;
       int64_t p = pb + pl;
       if (p < pe) {
         float f[8];
@@ -70,12 +73,12 @@ __global__ __launch_bounds__(NT) void gn_partial_kernel(const bf16_t* x0, int64_
         cnt = 1;
         p += PL;
       }
-      for (; p + 3 * PL < pe; p += 4 * PL) {
-        uint4 u[4];
+      for (; p + (U - 1) * PL < pe; p += U * PL) {
+        uint4 u[U];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) u[r] = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row0 + p + r * PL, (int64_t)j * 8);
+        for (int r = 0; r < U; ++r) u[r] = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row0 + p + r * PL, (int64_t)j * 8);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < U; ++r) {
           float f[8];
           unpack8(u[r], f);
 #pragma unroll
@@ -85,7 +88,7 @@ __global__ __launch_bounds__(NT) void gn_partial_kernel(const bf16_t* x0, int64_
             s2[e] = fmaf(t, t, s2[e]);
           }
         }
-        cnt += 4;
+        cnt += U;
       }
       for (; p < pe; p += PL) {
         float f[8];
