@@ -2,6 +2,7 @@
 // (buffer_load_dwordx4 ... lds) vs register loads (buffer_load_dwordx4), by waves per
 // workgroup and instructions in flight per wave.  One workgroup per CU (LDS 64 KiB).
 // build: hipcc --offload-arch=gfx950 -O3 -o mb_ldsdma tools/mb/ldsdma_bw.hip
+// (round 4: also MALL / HBM-sized windows; results in profiles/r04_ldsdma_fill.txt)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
@@ -52,17 +53,21 @@ void run(const char* src, uint32_t window, int wg_threads, int cus, float* sink)
 
 int main() {
   int cus = 0; hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-  const uint32_t window = 2u << 20;  // 2 MiB per XCD: L2-resident, > L1
-  char* src; hipMalloc(&src, 8 * (size_t)window); hipMemset(src, 1, 8 * (size_t)window);
   float* sink; hipMalloc(&sink, 4);
-  for (int wt : {256, 512, 1024}) {
-    run<2, true>(src, window, wt, cus, sink);
-    run<4, true>(src, window, wt, cus, sink);
-    run<8, true>(src, window, wt, cus, sink);
-    run<16, true>(src, window, wt, cus, sink);
-    run<4, false>(src, window, wt, cus, sink);
-    run<8, false>(src, window, wt, cus, sink);
+  // per-XCD windows: 2 MiB (L2-resident), 64 MiB (512 MiB in all: beyond the 256 MiB MALL... per
+  // XCD it streams from MALL/HBM), 256 MiB (2 GiB in all: HBM streaming)
+  for (uint32_t window : {2u << 20, 64u << 20, 256u << 20}) {
+    char* src; hipMalloc(&src, 8 * (size_t)window); hipMemset(src, 1, 8 * (size_t)window);
+    printf("window %u MiB per XCD\n", window >> 20);
+    for (int wt : {256, 512}) {
+      run<2, true>(src, window, wt, cus, sink);
+      run<4, true>(src, window, wt, cus, sink);
+      run<8, true>(src, window, wt, cus, sink);
+      run<16, true>(src, window, wt, cus, sink);
+      run<4, false>(src, window, wt, cus, sink);
+      run<8, false>(src, window, wt, cus, sink);
+    }
+    hipFree(src);
   }
-  // HBM streaming: window = 1 GiB (> MALL)
   return 0;
 }
