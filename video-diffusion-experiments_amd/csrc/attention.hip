@@ -916,6 +916,34 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks) kfr[kb][ks] = *(const bf16x8*)(smem + sb + 2048 * ks);
   };
+  // piecewise forms of read_v(t, 1) and read_k(t, 0) (round 4): one LDS read per call, so the
+  // M phase can place them between PV(d-block 0)'s MFMAs
+  bf16x4 v1lo[2][2], v1hi[2][2];
+  auto read_v1_piece = [&](int t, int i) {  // i = 0..7: (kb, s2, half)
+    const int kb = i >> 2, s2 = (i >> 1) & 1, h = i & 1;
+    const uint32_t sb = (uint32_t)((t % F4_RING) * F4_SLOT);
+    const uint32_t R = (uint32_t)(kb * 32 + 16 * s2);
+    const uint32_t a = sb + v1l + R * 16 + (h ? 128 : 0);
+    const bf16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(smem + a));
+    if (h) v1hi[kb][s2] = x; else v1lo[kb][s2] = x;
+  };
+  auto v1_join = [&]() {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x4 lo = v1lo[kb][s2], hi = v1hi[kb][s2];
+        vfr[1][kb][s2] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+  };
+  auto read_k0_piece = [&](int t, int ks) {
+    const uint32_t sb = (uint32_t)((t % F4_RING) * F4_SLOT) + kl0;
+    kfr[0][ks] = *(const bf16x8*)(smem + sb + 2048 * ks);
+  };
+  auto pv0_mfma = [&](int i) {  // i = 0..7: (kb, s2, qb) in pv(0)'s order
+    const int kb = i >> 2, s2 = (i >> 1) & 1, qb = i & 1;
+    oacc[0][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[0][kb][s2], pf[kb][s2][qb], oacc[0][qb], 0, 0, 0);
+  };
   auto qk = [&](int kb) {  // S(kb) = K'.Q'^T from the fragments read_k left
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks)
@@ -1025,11 +1053,21 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
     // VALU stream held the issue port and the two phases ran one after the other: stamps, ~1.6k
     // cycles per M phase against 896 of MFMA)
     __builtin_amdgcn_s_setprio(1);
-    read_v(t, 1);
-    if (more) read_k(t + 1, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    pv(0);
-    __builtin_amdgcn_sched_barrier(0);
+    // PV(d-block 0) needs nothing new (its V^T and P came from the V phase): the d-block-1 V reads
+    // and key block 0's K' reads go out two per MFMA gap between its 8 MFMAs (round 4; they were
+    // issued as one block before the first MFMA)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      pv0_mfma(i);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 2 * i; r < 2 * i + 2; ++r) {
+        if (r < 8) read_v1_piece(t, r);
+        else if (r < 11 && more) read_k0_piece(t + 1, r - 8);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    v1_join();
     if (more) read_k(t + 1, 1);
     __builtin_amdgcn_sched_barrier(0);
     pv(1);
