@@ -180,6 +180,39 @@ def test_gemm_v5_load_free_epilogue(cuda, path, M, N, K, epi):
             close_bf16(got, F.silu(want) if epi == "silu" else want)
 
 
+@pytest.mark.parametrize("M,N,kind", [(131072, 320, "res"), (65536 + 37, 960, "nobias"), (70000 + 5, 320, "res"),
+                                      (65536, 640, "silu"), (65600, 160, "gelu"), (98304, 5120, "bias")])
+def test_gemm_v8_weight_stationary(cuda, M, N, kind):
+    """v8 (one 160 x 320 W tile + bias resident in LDS per workgroup, A streamed into registers,
+    output staged through LDS):
+    ragged M (a partial last 32-row block, unequal XCD ranges), 1 / 2 / 4 / 6 / 32 column tiles
+    per XCD (idle workgroups when 32 % tiles != 0), every epilogue it takes — and bit-equal to
+    v2, whose k-order per output and epilogue arithmetic it keeps."""
+    K = 320
+    a = rnd(M, K)
+    w = rnd(N, K, std=K ** -0.5)
+    bias = None if kind == "nobias" else torch.randn(N, device=cuda)
+    kw = {}
+    if kind == "res":
+        kw["res"] = rnd(M, N)
+    elif kind in ("silu", "gelu"):
+        kw["act"] = ops.ACT_SILU if kind == "silu" else ops.ACT_GELU
+    with ops.gemm_plan(path=8):
+        got = ops.gemm(a, w, bias=bias, **kw)
+    with ops.gemm_plan(path=2):
+        ref = ops.gemm(a, w, bias=bias, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), f"v8 != v2 bits: max |diff| {(got.float() - ref.float()).abs().max().item()}"
+    x = a.float() @ w.float().T + (bias if bias is not None else 0)
+    if kind == "res":
+        x = x + kw["res"].float()
+    elif kind == "silu":
+        x = F.silu(x)
+    elif kind == "gelu":
+        x = F.gelu(x)
+    close_bf16(got, x)
+
+
 @pytest.mark.parametrize("M,N,K,kind", [(256, 1280, 1280, "res"), (1024, 1280, 5120, "rowbias"), (100, 320, 2560, "silu"),
                                        (256, 2560, 1280, "geglu"), (4096, 640, 640, "f32"), (64, 1280, 23040, "res")])
 def test_gemm_v6_small_m_splitk(cuda, M, N, K, kind):
@@ -288,7 +321,8 @@ def test_conv3x3_small_n(cuda, co, out_f32, M):
                                          (40000, 320, True, True), (3000, 320, True, True), (32768, 640, True, False)])
 def test_gemm_ln(cuda, M, N, res, pe):
     """vd_gemm with ln_out: the LayerNorm fused into the 256 x 320 GEMM epilogue (N = 320,
-    >= 128 row tiles) or run after the GEMM (smaller M, other N): out equals the plain GEMM
+    >= 128 row tiles, M < 65536; forced with path 5) or run after the GEMM (v8 at M >= 65536,
+    smaller M, other N): out equals the plain GEMM
     and ln_out the LayerNorm of out (+ PE by frame) to bf16 rounding."""
     from vdiff._lib import lib
     K, frames, pos = 320, 16, 64
@@ -314,6 +348,10 @@ def test_gemm_ln(cuda, M, N, res, pe):
         out2, ln2 = ops.gemm_ln(a, w, g, be, bias=b, res=r, **kw)
     assert torch.equal(ln2, want)
     assert (ln.float() - ln2.float()).abs().max().item() <= 2 ** -6 * (ln2.float().abs().max().item() + 1)
+    with ops.gemm_plan(path=5):  # the fused epilogue itself (at M >= 65536 the automatic plan takes v8 + vd_layernorm)
+        out5, ln5 = ops.gemm_ln(a, w, g, be, bias=b, res=r, **kw)
+    close_bf16(out5, plain.float())
+    assert (ln5.float() - ln2.float()).abs().max().item() <= 2 ** -6 * (ln2.float().abs().max().item() + 1)
 
 
 def test_gemm_splitk_dense(cuda):

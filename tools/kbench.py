@@ -67,7 +67,7 @@ for name, kind, M, N, K, res in cases:
             us = timeit(lambda: torch.nn.functional.linear(a, w))
             report(f"{name} [hipblaslt]", us, 2.0 * M * N * K, 2 * (M * K + N * K + M * N))
             continue
-        ops._PLAN.path = {"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6}[path]  # per-call vd_gemm_desc.path
+        ops._PLAN.path = {"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6, "v8": 8}[path]  # per-call vd_gemm_desc.path
         act = ops.ACT_GEGLU if kind == "geglu" else ops.ACT_NONE
         nout = N // 2 if kind == "geglu" else N
         out = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
@@ -90,7 +90,7 @@ for name, n, hw, ci, co in convs:
             report(f"{name} M={n*hw*hw} K={9*ci} [miopen]", us, 2.0 * n * hw * hw * co * 9 * ci,
                    2 * (n * hw * hw * (ci + co) + co * 9 * ci))
             continue
-        ops._PLAN.path = {"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6}[path]  # per-call vd_gemm_desc.path
+        ops._PLAN.path = {"auto": 0, "v1": 1, "v2": 2, "v3": 3, "v5": 5, "v6": 6, "v8": 8}[path]  # per-call vd_gemm_desc.path
         us = timeit(lambda: ops.conv3x3(x, n, hw, hw, w, out=out))
         report(f"{name} M={n*hw*hw} K={9*ci} [{path}]", us, 2.0 * n * hw * hw * co * 9 * ci,
                2 * (n * hw * hw * (ci + co) + co * 9 * ci))

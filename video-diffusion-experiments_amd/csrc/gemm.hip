@@ -1835,6 +1835,174 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
   }
 }
 
+// ============================================================================ v8
+// Weight-stationary GEMM for the short-K, tall-M L1 projections (K = 320, M >= 65536: the
+// attention / motion projections and the fused QKV of the 64 x 64 level).  Every other kernel
+// restages a W k-tile through LDS per 256-row tile and synchronises the workgroup per k-tile;
+// here a workgroup loads ONE 160-column W tile (160 x 320 bf16 = 100 KiB) and its bias into LDS
+// once and keeps them, and each of its 8 waves streams 16-row blocks of A straight from global
+// memory into MFMA B-operand registers — no A staging, no barrier after the W fill:
+//  * per row block a wave runs 10 k-steps x 10 column blocks = 100 MFMAs
+//    (v_mfma_f32_16x16x32_bf16); the W fragments are double-buffered in registers (k-step
+//    ks + 1's 10 ds_read_b128 go out before k-step ks's MFMAs);
+//  * the A registers are double-buffered: the next row block's 10 loads (and this block's
+//    residual rows) go out before this block's first MFMA, so each load has a whole row block
+//    of MFMA work to land, and the epilogue issues no load (bias from LDS, residual already in
+//    registers) — nothing in it waits for the prefetch;
+//  * the epilogue stages the wave's 16 x 160 output tile through LDS and writes it back as
+//    320-B row segments (1 KiB per store instruction over 3-4 rows) instead of 16 rows x 64 B;
+//  * blockIdx % 8 is the XCD; the row blocks are split into 8 contiguous ranges, one per XCD,
+//    and inside an XCD each 160-column W tile has 32 / tiles_n workgroups walking the XCD's row
+//    blocks in the same order, so an A row block is fetched from HBM once and served from that
+//    XCD's L2 to the other column tiles;
+//  * the k-order per output (k-steps 0..9, 32 deep each) and the epilogue arithmetic are v2's,
+//    so the results equal v2's bits (tests/test_gpu_kernels.py::test_gemm_v8_weight_stationary).
+// Measured (tools/kbench.py, 32 images, profiles/r04_gemm_v8.txt): L1 projection 36 vs 52 us,
+// with residual 45-50 vs 73-80 us, fused QKV N = 960 125 vs 137 us (v5).  Variants measured
+// and not kept: 32-row blocks (4 waves, accumulators in AGPRs: 0.5 W reads per MFMA, slower),
+// triple-buffered A, 12 waves per CU, unstaged 64-B stores.
+constexpr int G8_BN = 160, G8_KMAX = 320, G8_NW = 8;
+constexpr int G8_SUB = G8_BN * BK * 2;  // one 64-deep W sub-tile: 20 KiB
+
+template <bool RES>
+__global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
+                                                             uint32_t w_bytes, uint32_t c_bytes, int tiles_n,
+                                                             int groups) {
+  constexpr int KS = G8_KMAX / 32, NB = G8_BN / 16, NW = G8_NW;
+  constexpr int OROW = G8_BN * 2 + 16;  // staged output row (bytes, padded)
+  __shared__ __attribute__((aligned(1024))) char smem[(G8_KMAX / BK) * G8_SUB + G8_BN * 4 + NW * 16 * OROW];
+  float* sbias = (float*)(smem + (G8_KMAX / BK) * G8_SUB);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  char* obuf = smem + (G8_KMAX / BK) * G8_SUB + G8_BN * 4 + wid * 16 * OROW;
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  if (j >= groups * tiles_n) return;  // the XCD's workgroups beyond a whole number of W tiles
+  const int nt = j % tiles_n, grp = j / tiles_n;
+  const int M = (int)d.M, n0 = nt * G8_BN;
+  const int rbs = (M + 15) / 16;
+  const int rb0 = (int)((int64_t)rbs * xcd / 8), rb1 = (int)((int64_t)rbs * (xcd + 1) / 8);
+  const int gw = grp * NW + wid, GW = groups * NW;
+
+  // ---- W tile -> LDS (5 sub-tiles of 160 rows x 64 k, v2's swizzled B image) + bias, once
+  {
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)d.w, 0, w_bytes, 0x00020000);
+    const int rb = lane >> 3;
+    const uint32_t lc16 = (uint32_t)(((lane & 7) ^ rb) * 16);
+    constexpr int PIECES = (G8_KMAX / BK) * (G8_BN / 8);
+    for (int p = wid; p < PIECES; p += NW) {
+      const int s = p / (G8_BN / 8), pr = p - s * (G8_BN / 8);
+      const uint32_t n = (uint32_t)(n0 + pr * 8 + rb);
+      dma16(rw, smem + s * G8_SUB + pr * 1024, n * (uint32_t)(d.ldw * 2) + (uint32_t)(s * BK * 2) + lc16);
+    }
+    if (tid < G8_BN) sbias[tid] = d.bias ? d.bias[n0 + tid] : 0.f;
+    wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  int r = rb0 + gw;
+  if (r >= rb1) return;  // no barrier follows
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)d.a0, 0, a0_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)d.out, 0, c_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(RES ? d.res : d.out), 0, RES ? (uint32_t)(d.M * d.ld_res * 2) : 0u,
+                                        0x00020000);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int wcol = 16 * (fq & 1) + 8 * (fq >> 1);  // lane's column offset inside a swapped pair
+  // this lane's A fragments of row block rb: past the buffer (read as zeros, no traffic) for
+  // rows >= M and for row blocks past the XCD's range
+  auto load_a = [&](bf16x8 (&x)[KS], int rb) {
+    const int m = rb * 16 + fr;
+    const uint32_t o = (rb < rb1 && m < M) ? (uint32_t)m * (uint32_t)(d.lda0 * 2) + (uint32_t)(fq * 16) : G2_OOB;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      x[ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, o + (uint32_t)(ks * 64), 0, 0));
+  };
+  u32x4 rsv[NB / 2];
+  auto load_res = [&](int rb) {
+    const int m = rb * 16 + fr;
+#pragma unroll
+    for (int pr = 0; pr < NB / 2; ++pr) {
+      const uint32_t off = m < M ? (uint32_t)(m * (int)d.ld_res + n0 + pr * 32 + wcol) * 2u : G2_OOB;
+      rsv[pr] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+    }
+  };
+  const uint32_t wl = 2 * lds_off(fr, fq);  // lane's W fragment byte offset (column block 0, k-step 0)
+  auto block = [&](const bf16x8 (&x)[KS], int rb) {
+    f32x4 acc[NB];
+#pragma unroll
+    for (int a = 0; a < NB; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // k-step ks = sub-tile ks / 2, chunks 4 (ks & 1) + fq: the XOR with (row & 7) is the same
+    // for every 16-row column block, so (ks & 1) flips bit 2 of the chunk index (byte bit 6)
+    bf16x8 wf[2][NB];
+    auto read_w = [&](bf16x8 (&f)[NB], int ks) {
+      const char* sb = smem + (ks >> 1) * G8_SUB;
+      const uint32_t wk = (ks & 1) ? (wl ^ 64u) : wl;
+#pragma unroll
+      for (int a = 0; a < NB; ++a) f[a] = *(const bf16x8*)(sb + wk + a * 16 * BK * 2);
+    };
+    read_w(wf[0], 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) read_w(wf[(ks + 1) & 1], ks + 1);
+#pragma unroll
+      for (int a = 0; a < NB; ++a)
+        acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks & 1][a], x[ks], acc[a], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // one k-step per region (unpinned, hipcc spilled)
+    }
+    // epilogue (gemm_epilogue's wide-path arithmetic): permlane16_swap of column blocks (a, a+1)
+    // leaves each lane 8 consecutive columns; bias from LDS, residual from rsv
+#pragma unroll
+    for (int a = 0; a < NB; a += 2) {
+      const int c = a * 16 + wcol;
+      const float4 t0 = *(const float4*)(sbias + c), t1 = *(const float4*)(sbias + c + 4);
+      const float bv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+      float o[8];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        auto rp = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[a][jj]), __float_as_uint(acc[a + 1][jj]),
+                                                   false, false);
+        o[jj] = __uint_as_float(rp[0]) + bv[jj];
+        o[4 + jj] = __uint_as_float(rp[1]) + bv[4 + jj];
+      }
+      if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU) {
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) o[jj] = act_pw(d.act, o[jj]);
+      }
+      if constexpr (RES) {
+        float rf[8];
+        const u32x4 rv = rsv[a / 2];
+        unpack8(make_uint4(rv[0], rv[1], rv[2], rv[3]), rf);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) o[jj] += rf[jj];
+      }
+      *(uint4*)(obuf + fr * OROW + c * 2) = pack8(o);
+    }
+    // the wave's 16 x 160 tile back out of LDS as 320-B row segments (in-order LDS: no barrier
+    // within the wave; out-of-range rows carry an offset past the output buffer, dropped)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < 5; ++it) {
+      const int q = it * 64 + lane, row = q / 20, ch = q - row * 20;
+      const uint4 v = *(const uint4*)(obuf + row * OROW + ch * 16);
+      const int m = rb * 16 + row;
+      const uint32_t off = m < M ? (uint32_t)(m * (int)d.ldc + n0 + ch * 8) * 2u : G2_OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rc, off, 0, 0);
+    }
+  };
+  bf16x8 x0[KS], x1[KS];
+  load_a(x0, r);
+  for (;;) {
+    if constexpr (RES) load_res(r);
+    load_a(x1, r + GW);
+    block(x0, r);
+    if ((r += GW) >= rb1) break;
+    if constexpr (RES) load_res(r);
+    load_a(x0, r + GW);
+    block(x1, r);
+    if ((r += GW) >= rb1) break;
+  }
+}
+
 template <int BN>
 int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
   const int64_t units = ((d.M + G2_BM - 1) / G2_BM) * ((d.N + BN - 1) / BN) * split;
@@ -1914,6 +2082,20 @@ int launch6(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   return vd_launch_status();
 }
 
+int launch8(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t wb) {
+  const int per_xcd = g_num_cus / 8;  // one workgroup per CU, blockIdx % 8 = XCD
+  const int tiles_n = (int)(d.N / G8_BN);
+  const int groups = per_xcd / tiles_n;
+  if (groups < 1) return VD_EINVAL;
+  const uint32_t cb = (uint32_t)(d.M * d.ldc * 2);
+  const dim3 grid((unsigned)(8 * per_xcd)), block(G8_NW * 64);
+  if (d.res)
+    hipLaunchKernelGGL(gemm8_kernel<true>, grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
+  else
+    hipLaunchKernelGGL(gemm8_kernel<false>, grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
+  return vd_launch_status();
+}
+
 int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
   const int64_t units = ((d.M + G3_BM - 1) / G3_BM) * ((d.N + G3_BN - 1) / G3_BN) * split;
   if (units > 0x7fffffff) return VD_EINVAL;
@@ -1970,8 +2152,8 @@ void read_num_cus() {  // once per process: the plan (and the workspace size) de
   }
 }
 
-// d.path (per call, stateless): 0 = this automatic plan; 1 / 2 / 3 / 5 / 6 force v1 / v2 / v3 /
-// v5 / v6 (forced v6 also splits K toward 2 workgroups per CU) wherever that kernel takes the
+// d.path (per call, stateless): 0 = this automatic plan; 1 / 2 / 3 / 5 / 6 / 8 force v1 / v2 / v3 /
+// v5 / v6 / v8 (forced v6 also splits K toward 2 workgroups per CU) wherever that kernel takes the
 // shape, else the automatic choice — the parity tests run every path.  d.plan_m > 0 makes
 // every decision (kernel, tile count, split-K, LayerNorm fusion) as if M were plan_m while the
 // launch covers all M rows: an unsharded run planned with a frame shard's M reproduces that
@@ -1990,6 +2172,16 @@ Plan plan(const vd_gemm_desc& d) {
   const bool cin32 = d.a_mode != VD_A_CONV3X3 || (d.K / 9) % G4_BK == 0;
   const bool k64 = d.K % BK == 0 && d.k0 % BK == 0 &&
                    (d.a_mode != VD_A_CONV3X3 || (d.K / (d.ks * d.ks * d.kt)) % BK == 0);
+  // v8 (weight-stationary, K = 320, dense, M >= 65536): the L1 projections and fused QKV —
+  // 36 vs 52 us (projection), 45-50 vs 73-80 us (+ residual), 125 vs 137 us (QKV N = 960) on
+  // the previous choices (profiles/r04_gemm_v8.txt).  The GEGLU (erf epilogue, MFMA-heavy)
+  // stays on v3; a LayerNorm-fused request is NOT fused on these shapes: v8 + vd_layernorm
+  // (≈ 47 + 19 us) beats v5's fused epilogue (≈ 93 us in the step).
+  const bool v8ok = d.a_mode == VD_A_DENSE && d.K == G8_KMAX && d.k0 == d.K && !d.a1 && d.N % G8_BN == 0 &&
+                    d.N / G8_BN <= g_num_cus / 8 && M >= 65536 && g_num_cus % 8 == 0 && !d.rowbias &&
+                    !d.out_f32 && d.act != VD_ACT_GEGLU && d.ldc % 8 == 0 && al16(d.out) &&
+                    d.M * d.ldc * 2 < (int64_t)G2_OOB &&
+                    (!d.res || (d.ld_res % 8 == 0 && al16(d.res) && d.M * d.ld_res * 2 < (int64_t)G2_OOB));
   // fused LayerNorm epilogue: one 256 x 320 tile owns whole rows (v5, unsplit; >= 128 tiles so
   // the unsplit grid fills half the chip — smaller M runs the GEMM + vd_layernorm instead)
   if (d.ln_out) {
@@ -1997,7 +2189,7 @@ Plan plan(const vd_gemm_desc& d) {
                  d.ldc % 8 == 0 && d.ld_ln % 8 == 0 && ((uintptr_t)d.out & 15) == 0 && ((uintptr_t)d.ln_out & 15) == 0 &&
                  (!d.res || (d.ld_res % 8 == 0 && ((uintptr_t)d.res & 15) == 0)) &&
                  (M + G4_BM - 1) / G4_BM >= 128 && !d.rowbias && d.act == VD_ACT_NONE && !d.out_f32 &&
-                 (path == 0 || path == 5);
+                 (path == 5 || (path == 0 && !v8ok));
     if (p.ln_fused) {
       p.ver = 5;
       p.bn = 320;
@@ -2029,6 +2221,11 @@ Plan plan(const vd_gemm_desc& d) {
     p.bn = (p160 < p128 || (p160 == p128 && d.N % 160 == 0)) ? 160 : 128;
     p.split = split_for(((M + G2_BM - 1) / G2_BM) * ((d.N + p.bn - 1) / p.bn), d.K / BK);
     p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 : 0;
+    return p;
+  }
+  if (v8ok && (path == 0 || path == 8)) {
+    p.ver = 8;
+    p.bn = G8_BN;
     return p;
   }
   // v5 (256 x 320, BK 32): forced, where K or k0 is not a multiple of 64, and on the shape
@@ -2182,6 +2379,7 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
     return vd_layernorm(d.out, d.ldc, d.M, d.N, d.ln_gamma, d.ln_beta, d.ln_eps, d.ln_pe, d.ln_pe_div,
                         d.ln_pe_period, d.ln_out, d.ld_ln, stream);
   }
+  if (p.ver == 8) return launch8(d, s, p.a0b, p.wb);
   if (p.ver == 3) return launch3(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 6) return launch6(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 5) return launch4<320, 4, 2, 4>(d, s, p.a0b, p.a1b, p.wb, p.split);

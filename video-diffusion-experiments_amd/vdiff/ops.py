@@ -55,7 +55,7 @@ _PLAN = _GemmPlan()
 def gemm_plan(path: int = 0, plan_div: int = 0):
     """Test / benchmark hook on the Python side only — the C ABI takes both values per call in
     vd_gemm_desc and keeps no state.  Inside the block every vd_gemm carries `path` (1 v1, 2 v2,
-    3 v3, 5 v5, 6 v6: forced where that kernel takes the shape) and, with plan_div = N, plan_m =
+    3 v3, 5 v5, 6 v6, 8 v8: forced where that kernel takes the shape) and, with plan_div = N, plan_m =
     M / N for each GEMM whose M N divides: an unsharded model planned like one of N frame shards
     (same kernels, split-K and LayerNorm fusion, so the same summation order), which makes the
     sharded-vs-unsharded comparison of tests/test_gpu_dist2.py bit-exact under the product plan."""
