@@ -2172,16 +2172,19 @@ Plan plan(const vd_gemm_desc& d) {
   const bool cin32 = d.a_mode != VD_A_CONV3X3 || (d.K / 9) % G4_BK == 0;
   const bool k64 = d.K % BK == 0 && d.k0 % BK == 0 &&
                    (d.a_mode != VD_A_CONV3X3 || (d.K / (d.ks * d.ks * d.kt)) % BK == 0);
-  // v8 (weight-stationary, K = 320, dense, M >= 65536): the L1 projections and fused QKV —
+  // v8 (weight-stationary, K = 320, dense, M >= 32768): the L1 projections and fused QKV —
   // 36 vs 52 us (projection), 45-50 vs 73-80 us (+ residual), 125 vs 137 us (QKV N = 960) on
   // the previous choices (profiles/r04_gemm_v8.txt).  The GEGLU (erf epilogue, MFMA-heavy)
   // stays on v3; a LayerNorm-fused request is NOT fused on these shapes: v8 + vd_layernorm
   // (≈ 47 + 19 us) beats v5's fused epilogue (≈ 93 us in the step).
   const bool v8ok = d.a_mode == VD_A_DENSE && d.K == G8_KMAX && d.k0 == d.K && !d.a1 && d.N % G8_BN == 0 &&
-                    d.N / G8_BN <= g_num_cus / 8 && M >= 65536 && g_num_cus % 8 == 0 && !d.rowbias &&
+                    d.N / G8_BN <= g_num_cus / 8 && M >= 4096 && g_num_cus % 8 == 0 && !d.rowbias &&
                     !d.out_f32 && d.act != VD_ACT_GEGLU && d.ldc % 8 == 0 && al16(d.out) &&
                     d.M * d.ldc * 2 < (int64_t)G2_OOB &&
                     (!d.res || (d.ld_res % 8 == 0 && al16(d.res) && d.M * d.ld_res * 2 < (int64_t)G2_OOB));
+  // (M >= 32768: 4-frame shards too — 17 vs 20 us, QKV 31-34 vs 35-37 us; at M = 16384 even,
+  // profiles/r04_gemm_v8.txt; the LayerNorm stays fused below M = 65536)
+  const bool v8auto = v8ok && M >= 32768;
   // fused LayerNorm epilogue: one 256 x 320 tile owns whole rows (v5, unsplit; >= 128 tiles so
   // the unsplit grid fills half the chip — smaller M runs the GEMM + vd_layernorm instead)
   if (d.ln_out) {
@@ -2189,7 +2192,7 @@ Plan plan(const vd_gemm_desc& d) {
                  d.ldc % 8 == 0 && d.ld_ln % 8 == 0 && ((uintptr_t)d.out & 15) == 0 && ((uintptr_t)d.ln_out & 15) == 0 &&
                  (!d.res || (d.ld_res % 8 == 0 && ((uintptr_t)d.res & 15) == 0)) &&
                  (M + G4_BM - 1) / G4_BM >= 128 && !d.rowbias && d.act == VD_ACT_NONE && !d.out_f32 &&
-                 (path == 5 || (path == 0 && !v8ok));
+                 (path == 5 || (path == 0 && !(v8auto && M >= 65536)));
     if (p.ln_fused) {
       p.ver = 5;
       p.bn = 320;
@@ -2223,7 +2226,7 @@ Plan plan(const vd_gemm_desc& d) {
     p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 : 0;
     return p;
   }
-  if (v8ok && (path == 0 || path == 8)) {
+  if ((v8auto && path == 0) || (v8ok && path == 8)) {
     p.ver = 8;
     p.bn = G8_BN;
     return p;
