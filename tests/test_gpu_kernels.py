@@ -181,7 +181,8 @@ def test_gemm_v5_load_free_epilogue(cuda, path, M, N, K, epi):
 
 
 @pytest.mark.parametrize("M,N,kind", [(131072, 320, "res"), (65536 + 37, 960, "nobias"), (70000 + 5, 320, "res"),
-                                      (65536, 640, "silu"), (65600, 160, "gelu"), (98304, 5120, "bias")])
+                                      (65536, 640, "silu"), (65600, 160, "gelu"), (98304, 5120, "bias"),
+                                      (65536 + 16 * 5 + 3, 2560, "geglu")])
 def test_gemm_v8_weight_stationary(cuda, M, N, kind):
     """v8 (one 160 x 320 W tile + bias resident in LDS per workgroup, A streamed into registers,
     output staged through LDS):
@@ -193,7 +194,10 @@ def test_gemm_v8_weight_stationary(cuda, M, N, kind):
     w = rnd(N, K, std=K ** -0.5)
     bias = None if kind == "nobias" else torch.randn(N, device=cuda)
     kw = {}
-    if kind == "res":
+    if kind == "geglu":
+        w, bias = pack_geglu(w), pack_geglu(bias)
+        kw["act"] = ops.ACT_GEGLU
+    elif kind == "res":
         kw["res"] = rnd(M, N)
     elif kind in ("silu", "gelu"):
         kw["act"] = ops.ACT_SILU if kind == "silu" else ops.ACT_GELU
@@ -210,6 +214,9 @@ def test_gemm_v8_weight_stationary(cuda, M, N, kind):
         x = F.silu(x)
     elif kind == "gelu":
         x = F.gelu(x)
+    elif kind == "geglu":  # packed: (hidden block i, gate block i) 16-column pairs
+        x = x.view(M, -1, 2, 16)
+        x = x[:, :, 0].reshape(M, -1) * F.gelu(x[:, :, 1].reshape(M, -1))
     close_bf16(got, x)
 
 

@@ -1864,7 +1864,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
 constexpr int G8_BN = 160, G8_KMAX = 320, G8_NW = 8;
 constexpr int G8_SUB = G8_BN * BK * 2;  // one 64-deep W sub-tile: 20 KiB
 
-template <bool RES>
+template <bool RES, bool GEGLU>
 __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                              uint32_t w_bytes, uint32_t c_bytes, int tiles_n,
                                                              int groups) {
@@ -1948,6 +1948,36 @@ __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc
       for (int a = 0; a < NB; ++a)
         acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks & 1][a], x[ks], acc[a], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);  // one k-step per region (unpinned, hipcc spilled)
+    }
+    if constexpr (GEGLU) {
+      // (hidden, gate) 16-column block pairs (a, a+1) -> 16 output columns: the lane's 4 outputs
+      // (h + bh) * gelu(g + bg) on fp32 pairs (gemm_epilogue's arithmetic), 8 B into the staged row
+#pragma unroll
+      for (int a = 0; a < NB; a += 2) {
+        const int c = a * 16 + 4 * fq;
+        const float4 th = *(const float4*)(sbias + c), tg = *(const float4*)(sbias + c + 16);
+        uint32_t pk[2];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const f32x2 go = gelu_erf2(f32x2{acc[a + 1][2 * h2], acc[a + 1][2 * h2 + 1]} +
+                                     (h2 ? f32x2{tg.z, tg.w} : f32x2{tg.x, tg.y}));
+          const f32x2 oo = (f32x2{acc[a][2 * h2], acc[a][2 * h2 + 1]} + (h2 ? f32x2{th.z, th.w} : f32x2{th.x, th.y})) * go;
+          pk[h2] = pack2(oo[0], oo[1]);
+        }
+        *(uint2*)(obuf + fr * OROW + ((a / 2) * 16 + 4 * fq) * 2) = make_uint2(pk[0], pk[1]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int it = 0; it < 3; ++it) {  // 16 rows x 160 B
+        const int q = it * 64 + lane, row = q / 10, ch = q - row * 10;
+        if (q < 160) {
+          const uint4 v = *(const uint4*)(obuf + row * OROW + ch * 16);
+          const int m = rb * 16 + row;
+          const uint32_t off = m < M ? (uint32_t)(m * (int)d.ldc + n0 / 2 + ch * 8) * 2u : G2_OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rc, off, 0, 0);
+        }
+      }
+      return;
     }
     // epilogue (gemm_epilogue's wide-path arithmetic): permlane16_swap of column blocks (a, a+1)
     // leaves each lane 8 consecutive columns; bias from LDS, residual from rsv
@@ -2089,10 +2119,12 @@ int launch8(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t wb) {
   if (groups < 1) return VD_EINVAL;
   const uint32_t cb = (uint32_t)(d.M * d.ldc * 2);
   const dim3 grid((unsigned)(8 * per_xcd)), block(G8_NW * 64);
-  if (d.res)
-    hipLaunchKernelGGL(gemm8_kernel<true>, grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
+  if (d.act == VD_ACT_GEGLU)
+    hipLaunchKernelGGL((gemm8_kernel<false, true>), grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
+  else if (d.res)
+    hipLaunchKernelGGL((gemm8_kernel<true, false>), grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
   else
-    hipLaunchKernelGGL(gemm8_kernel<false>, grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
+    hipLaunchKernelGGL((gemm8_kernel<false, false>), grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
   return vd_launch_status();
 }
 
@@ -2179,7 +2211,7 @@ Plan plan(const vd_gemm_desc& d) {
   // (≈ 47 + 19 us) beats v5's fused epilogue (≈ 93 us in the step).
   const bool v8ok = d.a_mode == VD_A_DENSE && d.K == G8_KMAX && d.k0 == d.K && !d.a1 && d.N % G8_BN == 0 &&
                     d.N / G8_BN <= g_num_cus / 8 && M >= 4096 && g_num_cus % 8 == 0 && !d.rowbias &&
-                    !d.out_f32 && d.act != VD_ACT_GEGLU && d.ldc % 8 == 0 && al16(d.out) &&
+                    !d.out_f32 && d.ldc % 8 == 0 && al16(d.out) &&
                     d.M * d.ldc * 2 < (int64_t)G2_OOB &&
                     (!d.res || (d.ld_res % 8 == 0 && al16(d.res) && d.M * d.ld_res * 2 < (int64_t)G2_OOB));
   // (M >= 32768: 4-frame shards too — 17 vs 20 us, QKV 31-34 vs 35-37 us; at M = 16384 even,
