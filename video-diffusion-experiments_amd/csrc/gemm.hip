@@ -2206,8 +2206,8 @@ Plan plan(const vd_gemm_desc& d) {
                    (d.a_mode != VD_A_CONV3X3 || (d.K / (d.ks * d.ks * d.kt)) % BK == 0);
   // v8 (weight-stationary, K = 320, dense, M >= 32768): the L1 projections and fused QKV —
   // 36 vs 52 us (projection), 45-50 vs 73-80 us (+ residual), 125 vs 137 us (QKV N = 960) on
-  // the previous choices (profiles/r04_gemm_v8.txt).  The GEGLU (erf epilogue, MFMA-heavy)
-  // stays on v3; a LayerNorm-fused request is NOT fused on these shapes: v8 + vd_layernorm
+  // the previous choices (profiles/r04_gemm_v8.txt); the L1 GEGLU too (same-box step A/B vs v3:
+  // -0.1..0.3 ms).  A LayerNorm-fused request is NOT fused on these shapes: v8 + vd_layernorm
   // (≈ 47 + 19 us) beats v5's fused epilogue (≈ 93 us in the step).
   const bool v8ok = d.a_mode == VD_A_DENSE && d.K == G8_KMAX && d.k0 == d.K && !d.a1 && d.N % G8_BN == 0 &&
                     d.N / G8_BN <= g_num_cus / 8 && M >= 4096 && g_num_cus % 8 == 0 && !d.rowbias &&
