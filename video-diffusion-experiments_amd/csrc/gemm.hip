@@ -2204,7 +2204,7 @@ Plan plan(const vd_gemm_desc& d) {
   const bool cin32 = d.a_mode != VD_A_CONV3X3 || (d.K / 9) % G4_BK == 0;
   const bool k64 = d.K % BK == 0 && d.k0 % BK == 0 &&
                    (d.a_mode != VD_A_CONV3X3 || (d.K / (d.ks * d.ks * d.kt)) % BK == 0);
-  // v8 (weight-stationary, K = 320, dense, M >= 32768): the L1 projections and fused QKV —
+  // v8 (weight-stationary, K = 320, dense, M >= 16384): the L1 projections and fused QKV —
   // 36 vs 52 us (projection), 45-50 vs 73-80 us (+ residual), 125 vs 137 us (QKV N = 960) on
   // the previous choices (profiles/r04_gemm_v8.txt); the L1 GEGLU too (same-box step A/B vs v3:
   // -0.1..0.3 ms).  A LayerNorm-fused request is NOT fused on these shapes: v8 + vd_layernorm
@@ -2214,9 +2214,10 @@ Plan plan(const vd_gemm_desc& d) {
                     !d.out_f32 && d.ldc % 8 == 0 && al16(d.out) &&
                     d.M * d.ldc * 2 < (int64_t)G2_OOB &&
                     (!d.res || (d.ld_res % 8 == 0 && al16(d.res) && d.M * d.ld_res * 2 < (int64_t)G2_OOB));
-  // (M >= 32768: 4-frame shards too — 17 vs 20 us, QKV 31-34 vs 35-37 us; at M = 16384 even,
+  // (M >= 16384: the 4- and 2-frame shards too — 17 vs 20 us, QKV 31-34 vs 35-37 us at M = 32768;
+  // even at M = 16384 in kbench, and the 2-frame step 12.47 -> 12.42 ms in a same-box A/B,
   // profiles/r04_gemm_v8.txt; the LayerNorm stays fused below M = 65536)
-  const bool v8auto = v8ok && M >= 32768;
+  const bool v8auto = v8ok && M >= 16384;
   // fused LayerNorm epilogue: one 256 x 320 tile owns whole rows (v5, unsplit; >= 128 tiles so
   // the unsplit grid fills half the chip — smaller M runs the GEMM + vd_layernorm instead)
   if (d.ln_out) {
