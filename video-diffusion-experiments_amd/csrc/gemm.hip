@@ -2208,15 +2208,16 @@ Plan plan(const vd_gemm_desc& d) {
   // 36 vs 52 us (projection), 45-50 vs 73-80 us (+ residual), 125 vs 137 us (QKV N = 960) on
   // the previous choices (profiles/r04_gemm_v8.txt); the L1 GEGLU too (same-box step A/B vs v3:
   // -0.1..0.3 ms).  A LayerNorm-fused request is NOT fused on these shapes: v8 + vd_layernorm
-  // (≈ 47 + 19 us) beats v5's fused epilogue (≈ 93 us in the step).
+  // (≈ 53 + 33 us at M = 131072) beats v5's fused epilogue (≈ 93 us in the step).
   const bool v8ok = d.a_mode == VD_A_DENSE && d.K == G8_KMAX && d.k0 == d.K && !d.a1 && d.N % G8_BN == 0 &&
                     d.N / G8_BN <= g_num_cus / 8 && M >= 4096 && g_num_cus % 8 == 0 && !d.rowbias &&
                     !d.out_f32 && d.ldc % 8 == 0 && al16(d.out) &&
                     d.M * d.ldc * 2 < (int64_t)G2_OOB &&
                     (!d.res || (d.ld_res % 8 == 0 && al16(d.res) && d.M * d.ld_res * 2 < (int64_t)G2_OOB));
   // (M >= 16384: the 4- and 2-frame shards too — 17 vs 20 us, QKV 31-34 vs 35-37 us at M = 32768;
-  // even at M = 16384 in kbench, and the 2-frame step 12.47 -> 12.42 ms in a same-box A/B,
-  // profiles/r04_gemm_v8.txt; the LayerNorm stays fused below M = 65536)
+  // even at M = 16384 in kbench, and the 2-frame step 12.47 -> 12.42 ms in a same-box A/B; with
+  // the LayerNorm unfused there as well the 4-frame step went 17.47 -> 17.04 ms,
+  // profiles/r04_gemm_v8.txt)
   const bool v8auto = v8ok && M >= 16384;
   // fused LayerNorm epilogue: one 256 x 320 tile owns whole rows (v5, unsplit; >= 128 tiles so
   // the unsplit grid fills half the chip — smaller M runs the GEMM + vd_layernorm instead)
@@ -2225,7 +2226,7 @@ Plan plan(const vd_gemm_desc& d) {
                  d.ldc % 8 == 0 && d.ld_ln % 8 == 0 && ((uintptr_t)d.out & 15) == 0 && ((uintptr_t)d.ln_out & 15) == 0 &&
                  (!d.res || (d.ld_res % 8 == 0 && ((uintptr_t)d.res & 15) == 0)) &&
                  (M + G4_BM - 1) / G4_BM >= 128 && !d.rowbias && d.act == VD_ACT_NONE && !d.out_f32 &&
-                 (path == 5 || (path == 0 && !(v8auto && M >= 65536)));
+                 (path == 5 || (path == 0 && !v8auto));
     if (p.ln_fused) {
       p.ver = 5;
       p.bn = 320;
