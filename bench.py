@@ -14,6 +14,15 @@ scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+`--gpus N > 1` without a torch.distributed environment (no WORLD_SIZE) starts the N ranks
+itself — `python -m torch.distributed.run --nproc-per-node N` as a CHILD process, before this
+process touches the GPU — forwards rank 0's JSON line and exits with the children's status.
+Under a launcher, WORLD_SIZE must equal --gpus (else exit 2).  `--layout replicas` is the
+SURVEY §8e upper-bound control: N independent 16-frame videos, one per GPU, no collective in
+the step; value = all ranks' steps / the slowest rank's time, labelled, never the headline.
+`--dry-run` goes through the same launch / rendezvous / max-over-ranks path on the CPU (gloo)
+without a model, for the CPU tests of this contract.
+
 Also reported: `roofline` for the spatial self-attention kernel at level 1
 (S=4096, d=40: the north-star kernel), timed with HIP events on its launch
 stream; `step_mfma` = the whole step's algorithmic FLOPs / step time vs the
@@ -191,6 +200,60 @@ def cpu_baseline(unet_gpu, cfg_name, frames_sample, frames_full):
                       f"attention core, 0.1 % of the FLOPs, is linear in frames; BASELINE.md §3)"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start n ranks of this script under torch.distributed.run as a child process (never an
+    exec: nothing here has touched the GPU, and the children initialise it themselves);
+    their stdout is this process's, so rank 0's JSON line comes through unchanged."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve())] + list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    log(f"[bench] --gpus {n}: launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_world(args):
+    """The rank environment against --gpus: (world, rank, local_rank) or SystemExit."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+              f"{world}-rank run as {args.gpus} GPUs", file=sys.stderr)
+        raise SystemExit(2)
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def dry_run(args, world, rank):
+    """The multi-rank contract without a GPU or a model: gloo rendezvous, the timed region's
+    barriers, max-over-ranks, one JSON line from rank 0 (tests/test_bench_launch.py)."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0 + 1e-6 * (rank + 1)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        ranks = [None] * world
+        dist.all_gather_object(ranks, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0"))})
+    else:
+        ranks = [{"rank": 0, "local_rank": 0}]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "denoising steps/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                          "layout": args.layout, "max_elapsed_s": el.item(), "ranks": ranks}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,13 +275,27 @@ def main():
     ap.add_argument("--window", default="a2a", choices=["a2a", "kv-gather"],
                     help="N>1: motion-module temporal window — all-to-all re-shard (default) or the north "
                          "star's K/V all-gather over the frame shards (vdiff.dist.FrameShard window)")
-    ap.add_argument("--layout", default="auto", choices=["auto", "frame", "cfg-frame"],
-                    help="N>1 placement (vdiff.dist.layout): auto = cfg-frame at 2 GPUs, frame otherwise")
+    ap.add_argument("--layout", default="auto", choices=["auto", "frame", "cfg-frame", "replicas"],
+                    help="N>1 placement (vdiff.dist.layout): auto = cfg-frame at 2 GPUs, frame otherwise; "
+                         "replicas = one independent video per GPU (SURVEY §8e upper-bound control, weak scaling)")
+    ap.add_argument("--no-replicas", action="store_true",
+                    help="N>1: skip the replicas control measured after the sharded run")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only: the launch / rendezvous / max-over-ranks path with gloo and no model")
     args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if not args.dry_run and torch.cuda.device_count() < args.gpus:  # counts devices without initialising HIP
+            print(f"bench.py: --gpus {args.gpus} but {torch.cuda.device_count()} GPUs visible", file=sys.stderr)
+            raise SystemExit(2)
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local = check_world(args)
+    if args.steps < 1 or args.warmup < 0:
+        ap.error("--steps must be >= 1 and --warmup >= 0")
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return
     torch.cuda.set_device(local)
     if args.roofline_only:
         from vdiff.weights import materialize_synthetic
@@ -240,78 +317,87 @@ def main():
 
     cfg_name = args.config
     frames = args.frames or (16 if cfg_name == "full" else 4)
+    replicas = args.layout == "replicas"
     t0 = time.time()
     from vdiff.dist import NodeLayout
-    lay = NodeLayout(args.layout, frames, cfg=True, world=world, rank=rank, overlap_chunks=args.overlap,
-                     window=args.window)
+    # replicas: every rank is a whole single-GPU job on its own video (no shard, no collective)
+    lay = NodeLayout("frame" if replicas else args.layout, frames, cfg=True, world=1 if replicas else world,
+                     rank=0 if replicas else rank, overlap_chunks=args.overlap, window=args.window)
     unet = materialize_synthetic(cfg_name, device="cuda", seed=0)
     unet.dist = lay.frame_shard
     unet.prepare()
-    log(f"[bench] model ready in {time.time() - t0:.1f}s; world={world} layout={lay.describe()}")
+    log(f"[bench] model ready in {time.time() - t0:.1f}s; world={world} layout="
+        f"{'replicas x%d' % world if replicas else lay.describe()}")
     cfg = unet.config
     fl = lay.frames_local
     g = torch.Generator().manual_seed(42)
     lat_all = torch.randn((1, 4, frames, 64, 64), generator=g)
-    lat = lat_all[:, :, lay.frame_slice()].cuda()
     ehs = torch.randn((2, 77, cfg["cross_attention_dim"]), generator=torch.Generator().manual_seed(1))
     sched = DDIMScheduler.from_config(DDIMScheduler().config, beta_schedule="linear", steps_offset=1,
                                       clip_sample=False)
     sched.set_timesteps(50)
     total = args.warmup + args.steps
     ts = sched.timesteps.repeat((total + 49) // 50)[:max(total, 50)]
-    loop = DenoiseLoop(unet, sched, lat, ehs.cuda(), 7.5, timesteps=ts, use_graph=not args.no_graph,
-                       cfg_shard=lay.cfg_shard)
-    loop.prime()
-    log(f"[bench] primed: graph={'yes' if loop.graph is not None else 'no'} {loop.graph_error or ''}")
-    loop.run(args.warmup)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    loop.run(args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        tt = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = tt.item()
-    assert torch.isfinite(loop.lat).all(), "non-finite latents"
-    sps = args.steps / elapsed
+
+    def timed(lay_, ehs_, guidance, cfg_shard=None):
+        """W untimed + K timed replays of a captured loop on this layout; the timed region is
+        bracketed by barrier + synchronize on both sides; returns (max-over-ranks seconds, loop)."""
+        lp = DenoiseLoop(unet, sched, lat_all[:, :, lay_.frame_slice()].cuda(), ehs_.cuda(), guidance,
+                         timesteps=ts, use_graph=not args.no_graph, cfg_shard=cfg_shard)
+        lp.prime()
+        lp.run(args.warmup)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        lp.run(args.steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t_start
+        if world > 1:
+            tt = torch.tensor([el], device="cuda", dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = tt.item()
+        assert torch.isfinite(lp.lat).all(), "non-finite latents"
+        return el, lp
+
+    elapsed, loop = timed(lay, ehs, 7.5, lay.cfg_shard)
+    log(f"[bench] graph={'yes' if loop.graph is not None else 'no'} {loop.graph_error or ''}")
+    videos = world if replicas else 1           # independent videos the node denoised per step
+    sps = videos * args.steps / elapsed
     graph_ok = loop.graph is not None
     ms = 1e3 * elapsed / args.steps
+    del loop
 
     # SURVEY §8d: the B=1 (no-CFG, guidance 1) variant, labelled — same graph-captured
     # loop on the conditional half only
     nocfg = None
     if not args.no_nocfg:
         # no CFG pair to split: frame-shard over all ranks
-        del loop
         lay1 = lay if lay.layout == "frame" else NodeLayout("frame", frames, cfg=False, world=world, rank=rank,
                                                              overlap_chunks=args.overlap, window=args.window)
         unet.dist = lay1.frame_shard
-        lat1 = lat_all[:, :, lay1.frame_slice()].cuda()
-        loop1 = DenoiseLoop(unet, sched, lat1, ehs[1:].cuda(), 1.0, timesteps=ts, use_graph=not args.no_graph)
-        loop1.prime()
-        loop1.run(args.warmup)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t1 = time.perf_counter()
-        loop1.run(args.steps)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        e1 = time.perf_counter() - t1
-        if world > 1:
-            tt = torch.tensor([e1], device="cuda", dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            e1 = tt.item()
-        nocfg = {"value": round(args.steps / e1, 4), "unit": "denoising steps/s", "ms_per_step": round(1e3 * e1 / args.steps, 3),
+        e1, lp1 = timed(lay1, ehs[1:], 1.0)
+        del lp1
+        nocfg = {"value": round(videos * args.steps / e1, 4), "unit": "denoising steps/s",
+                 "ms_per_step": round(1e3 * e1 / args.steps, 3),
                  "config": "guidance_scale 1 (no CFG): UNet batch 1 per step, same frames/latents"}
-        del loop1
+
+    # SURVEY §8e: the "replicas only" upper-bound control beside a sharded run — every rank
+    # denoises its own whole 16-frame video, no collective; labelled, never the headline
+    rep = None
+    if world > 1 and not replicas and not args.no_replicas:
+        lay_r = NodeLayout("frame", frames, cfg=True, world=1, rank=0)
+        unet.dist = None
+        er, lpr = timed(lay_r, ehs, 7.5)
+        del lpr
+        rep = {"value": round(world * args.steps / er, 4), "unit": "denoising steps/s (node, N videos)",
+               "ms_per_step": round(1e3 * er / args.steps, 3), "scaling": "weak",
+               "config": f"replicas x{world}: one independent {frames}-frame CFG video per GPU, no collective "
+                         "(SURVEY §8e upper-bound control, not the headline)"}
+    unet.dist = lay.frame_shard
 
     imgs = (2 // lay.cfg_ranks) * fl  # images per rank in the CFG run
     mqkv = None
@@ -322,15 +408,17 @@ def main():
     st = time_attention(imgs, args.attn_reps, torch.cuda.current_stream(), stress=True)
     roof["synthetic"] = {k: syn[k] for k in ("achieved", "frac", "avg_launch_ms")}
     roof["stress"] = {k: st[k] for k in ("achieved", "frac", "avg_launch_ms")}
-    roof["inputs"] = (("the step's own level-1 self-attention q | k | v (one eager forward of the workload, "
-                       "t = 981; softmax scale folded into q by to_q)") if mqkv is not None else
+    roof["inputs"] = (("q | k | v of the step's level-1 self-attention in the synthetic-weight model (one eager "
+                       "forward of the workload with its N(0, 0.02^2) random-init weights, t = 981; softmax scale "
+                       "folded into q by to_q) -- not a trained network's logit statistics") if mqkv is not None else
                       "synthetic (multi-rank run)") + (
                       "; `synthetic`: q, k, v ~ N(0, 1.5^2) with the scale folded (exp2 argument std ~3.2), "
                       "rounds 1-3's roofline input; `stress`: the scale not folded (std ~14)")
     roof["traffic"], roof["traffic_source"] = pmc_traffic(imgs)
     roof["mfma_busy"], roof["mfma_busy_source"] = pmc_mfma_busy()
     roof["kernel_src_hash"] = roof_src_hash()
-    step_tf = STEP_TFLOP[cfg_name] * (frames / (16 if cfg_name == "full" else 4)) / (ms * 1e-3) / world
+    gpu_tflop = STEP_TFLOP[cfg_name] * frames / (16 if cfg_name == "full" else 4) / (1 if replicas else world)
+    step_tf = gpu_tflop / (ms * 1e-3)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[bench] timing the CPU oracle baseline ...")
@@ -346,7 +434,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if replicas else "strong",
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (latents randn seed 42, text embeddings randn seed 1, weights N(0,0.02^2))",
@@ -357,16 +445,17 @@ def main():
                 if cfg_name == "full" else "BASELINE config 2: tiny UNetMotionModel, 4 frames x 64x64",
                 "model": f"UNetMotionModel[{cfg_name}]",
                 "frames": frames, "latent_hw": 64, "global_batch": 2, "seq_len": 4096,
-                "parallelism": lay.describe(),
+                "parallelism": (f"replicas x{world} (one independent video per GPU: SURVEY §8e upper-bound "
+                                "control, not the headline)") if replicas else lay.describe(),
                 "hipgraph": graph_ok,
             },
             "roofline": roof,
-            "step_mfma": {"algorithmic_tflop_per_step_per_gpu": round(STEP_TFLOP[cfg_name] * frames /
-                                                                     (16 if cfg_name == "full" else 4) / world, 3),
+            "step_mfma": {"algorithmic_tflop_per_step_per_gpu": round(gpu_tflop, 3),
                           "achieved": round(step_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                           "frac": round(step_tf / PEAK_BF16_TFLOPS, 4)},
             "cpu_baseline": cpu,
             "no_cfg": nocfg,
+            "replicas_control": rep,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
