@@ -118,6 +118,15 @@ typedef struct vd_gemm_desc {
    * summation order bit for bit (tests/test_gpu_dist2.py). */
   int32_t path;
   int64_t plan_m;
+  /* Output-row permutation (round 5; 0 = none): with rmap_inner > 0 the epilogue writes row m
+   * of the product — and reads its residual — at row rev3(m), where
+   *   m = ((i0*rmap_n1 + i1)*rmap_n2 + i2)*rmap_inner + j  ->  ((i2*rmap_n1 + i1)*n0 + i0)*rmap_inner + j,
+   * n0 = M / (rmap_n1*rmap_n2*rmap_inner).  The frame-sharded motion module's proj_out takes the
+   * rows of the returning all-to-all, (position chunk, frame, video, position) on a rank, and writes
+   * them straight into the rank's (video, frame, position) layout with the residual added
+   * (vdiff.dist.FrameShard.return_perm) — no separate re-shard transpose.  Not with ln_out, GEGLU
+   * or a row bias. */
+  int32_t rmap_n1, rmap_n2, rmap_inner;
 } vd_gemm_desc;
 
 int vd_gemm(const vd_gemm_desc* d, vd_stream_t stream);
@@ -148,6 +157,14 @@ int vd_gn_finalize(const float* ws, int64_t n_inst, int32_t n_split_total, int64
 int vd_gn_apply(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1,
                 int64_t C, int64_t n_inst, int64_t pix_per_inst, const float* scale_shift,
                 int32_t silu, void* y, int64_t ldy, vd_stream_t stream);
+/* vd_gn_apply writing input row m to output row rev3(m) (the vd_gemm_desc.rmap_* map: rows
+ * ((i0*n1 + i1)*n2 + i2)*inner + j -> ((i2*n1 + i1)*n0 + i0)*inner + j; n1, n2, inner powers of
+ * two, inner = 0 the identity): the frame-sharded motion module's norm writes its rows straight
+ * into the all-to-all's send order (round 5, vdiff.dist.FrameShard.send_perm). */
+int vd_gn_apply_rev3(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1,
+                     int64_t C, int64_t n_inst, int64_t pix_per_inst, const float* scale_shift,
+                     int32_t silu, void* y, int64_t ldy, int64_t n1, int64_t n2, int64_t inner,
+                     vd_stream_t stream);
 /* Two-launch GroupNorm for image instances (ResnetBlock2D / Transformer2DModel / VAE
  * norms): vd_gn_partial_g writes ONE {n, mean, M2} record per (instance, split, group)
  * (ws: n_inst*n_split*groups float4; C <= 2560, 256 % groups == 0), and vd_gn_apply_g

@@ -15,7 +15,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import unet_ref
-from vdiff.dist import FrameShard, block_transpose_reference as bt
+from vdiff.dist import FrameShard, block_transpose_reference as bt, rev3_reference
 
 
 def _free_port():
@@ -66,6 +66,25 @@ def sharded_motion_rows(sd, p, local, B, Fl, HW, heads, groups, fs):
     hp = tok.reshape(B, Pl, Ftot, C).permute(0, 2, 1, 3).reshape(-1, C)
     h = fs.to_frame_shards(hp, B, Fl, HW, bt)
     return unet_ref.linear(sd, p + ".proj_out", h) + local
+
+
+def sharded_motion_rows_fused(sd, p, local, B, Fl, HW, heads, groups, fs):
+    """The product's fused re-shard (round 5, FrameShard.send_perm / return_perm): the norm's rows
+    go out in send order, the block runs on the received (frame, video, position) rows with one
+    video of B*pl positions, and proj_out maps the returned rows into the rank's layout."""
+    C = local.shape[1]
+    ws = fs.gather_gn_partials(_gn_partial(local, B, Fl * HW))
+    a, b = _gn_finalize(ws, groups, 1e-6, sd[p + ".norm.weight"].double(), sd[p + ".norm.bias"].double())
+    hn = (local.reshape(B, Fl * HW, C) * a[:, None] + b[:, None]).reshape(-1, C)
+    recv = fs.exchange(rev3_reference(hn, *fs.send_perm(B, Fl, HW)))   # rows (f, b, j)
+    h = unet_ref.linear(sd, p + ".proj_in", recv)
+    Ftot, Pl = Fl * fs.world, HW // fs.world
+    tok = h.reshape(Ftot, B * Pl, C).permute(1, 0, 2)                   # (b*pl + j, f, C)
+    tok = unet_ref.basic_transformer_block(sd, p + ".transformer_blocks.0", tok, None, heads,
+                                           pe=unet_ref.sinusoidal_pe(32, C), double_self=True)
+    back = fs.exchange(tok.permute(1, 0, 2).reshape(-1, C))             # rows (r', f_loc, b, j)
+    y = unet_ref.linear(sd, p + ".proj_out", back)
+    return rev3_reference(y, *fs.return_perm(B, Fl, HW)) + local
 
 
 def _worker(rank, world, port, errq):
@@ -131,6 +150,16 @@ def _worker(rank, world, port, errq):
         want = ref.reshape(B, F, C, HW).permute(0, 1, 3, 2)[:, rank * Fl:(rank + 1) * Fl].reshape(-1, C)
         err = (got - want).abs().max().item()
         assert err < 1e-4, f"sharded motion module max err {err}"
+        assert fs.fused_ok(B, Fl, HW)
+        got = sharded_motion_rows_fused(sd, p, local, B, Fl, HW, 2, 32, fs)
+        err = (got - want).abs().max().item()
+        assert err < 1e-4, f"fused re-shard motion module max err {err}"
+        # the two row maps are inverse to the old transposes' composition: send order = what
+        # to_position_shards' first transpose + a frame/video swap would send
+        rows = torch.arange(B * Fl * HW, dtype=torch.float32)[:, None]
+        snd = rev3_reference(rows, *fs.send_perm(B, Fl, HW)).reshape(world, Fl, B, HW // world)
+        src = rows.reshape(B, Fl, world, HW // world)
+        assert torch.equal(snd, src.permute(2, 1, 0, 3)), "send_perm"
         # ---- 3. kt = 3 temporal conv under frame sharding: one-frame halo (all-gather) + a conv
         # over the halo'd frames with no temporal padding == the unsharded 3-D conv's frames
         Cc, Co = 8, 16

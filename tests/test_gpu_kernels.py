@@ -13,7 +13,7 @@ import torch
 import torch.nn.functional as F
 
 from vdiff import ops
-from vdiff.dist import block_transpose_reference
+from vdiff.dist import block_transpose_reference, rev3_reference
 from vdiff.models.layers import pack_conv3x3, pack_geglu
 
 pytestmark = pytest.mark.gpu
@@ -218,6 +218,69 @@ def test_gemm_v8_weight_stationary(cuda, M, N, kind):
         x = x.view(M, -1, 2, 16)
         x = x[:, :, 0].reshape(M, -1) * F.gelu(x[:, :, 1].reshape(M, -1))
     close_bf16(got, x)
+
+
+def test_gemm_v8_strided_operands(cuda):
+    """v8 on column-slice views: A with lda0 = 384, out and residual slices of wider
+    buffers (ldc = ld_res = N + 160) — v8's own A / store / residual address arithmetic — bit-equal
+    to v2 on the same views."""
+    M, N, K = 8192, 320, 320
+    abuf = rnd(M, 384)
+    a = abuf[:, 32:32 + K]
+    w = rnd(N, K, std=K ** -0.5)
+    bias = torch.randn(N, device=cuda)
+    rbuf = rnd(M, N + 160)
+    res = rbuf[:, 80:80 + N]
+    outs = []
+    for path in (8, 2):
+        obuf = torch.full((M, N + 160), 7.0, device=cuda, dtype=torch.bfloat16)
+        with ops.gemm_plan(path=path):
+            ops.gemm(a, w, bias=bias, res=res, out=obuf[:, 160:])
+        outs.append(obuf)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]), "v8 != v2 on strided views"
+    assert torch.all(outs[0][:, :160] == 7.0), "v8 wrote outside its column slice"
+    close_bf16(outs[0][:, 160:], a.float() @ w.float().T + bias + res.float())
+
+
+@pytest.mark.parametrize("path,M,N,K", [(0, 16384, 320, 320), (8, 4096, 320, 320), (0, 4096, 640, 640),
+                                        (6, 1024, 1280, 1280), (0, 256, 1280, 1280), (1, 512, 320, 192)])
+def test_gemm_row_map(cuda, path, M, N, K):
+    """vd_gemm_desc.rmap_* (round 5, the frame-sharded motion module's proj_out): product row m and
+    its residual live at row rev3(m) — rows (r', f_loc, b, j) of the returning all-to-all written
+    into a rank's (b, f_loc, r', j) layout (8 ranks, 2 frames, CFG batch 2).  The plan carries
+    the map on v8 (residual), v6 (split where forced) and v1; each case is bit-equal to the same
+    kernel without the map on pre-permuted residual rows, and within bf16 of fp32."""
+    n1, n2, world = 2, 2, 8
+    inner = M // (world * n1 * n2)
+    a = rnd(M, K)
+    w = rnd(N, K, std=K ** -0.5)
+    bias = torch.randn(N, device=cuda)
+    res = rnd(M, N)                                   # in the destination layout
+    res_src = rev3_reference(res, n1, world, inner)   # residual rows in product order
+    with ops.gemm_plan(path=path):
+        got = ops.gemm(a, w, bias=bias, res=res, rmap=(n1, n2, inner))
+        plain = ops.gemm(a, w, bias=bias, res=res_src)
+    torch.cuda.synchronize()
+    want = rev3_reference(plain, n1, n2, inner)
+    assert torch.equal(got, want), f"row map != permuted plain GEMM: max {(got.float() - want.float()).abs().max()}"
+    close_bf16(got, rev3_reference(a.float() @ w.float().T + bias, n1, n2, inner) + res.float())
+
+
+def test_gn_apply_rev3(cuda):
+    """vd_gn_apply_rev3: the motion norm writing the all-to-all's send order directly equals the
+    plain apply followed by the row permutation, bit for bit."""
+    B, Fl, HW, C, world = 2, 2, 1024, 320, 8
+    x = rnd(B * Fl * HW, C) + 0.3
+    g = 1 + 0.1 * torch.randn(C, device=cuda)
+    b = 0.1 * torch.randn(C, device=cuda)
+    ws = ops.gn_partial(x, C, B, Fl * HW, Fl * ops.gn_splits_per_frame(HW))
+    ss = ops.gn_finalize(ws, 32, 1e-6, g, b)
+    perm = (Fl, world, HW // world)
+    got = ops.gn_apply(x, ss, Fl * HW, False, rev3=perm)
+    plain = ops.gn_apply(x, ss, Fl * HW, False)
+    torch.cuda.synchronize()
+    assert torch.equal(got, rev3_reference(plain, *perm))
 
 
 @pytest.mark.parametrize("M,N,K,kind", [(256, 1280, 1280, "res"), (1024, 1280, 5120, "rowbias"), (100, 320, 2560, "silu"),

@@ -53,6 +53,39 @@ class EmulatedShard(FrameShard):
         return x
 
 
+def ab_fused(args):
+    """Both arms captured once on one model, then replayed in alternating rounds (one box, one
+    process: the guide's rule 24)."""
+    unet = materialize_synthetic("full", device="cuda", seed=0)
+    fl = args.frames // args.world
+    lat = torch.randn(1, 4, fl, 64, 64, device="cuda")
+    ehs = torch.randn(2, 77, unet.config["cross_attention_dim"], device="cuda")
+    s = DDIMScheduler(beta_schedule="linear", steps_offset=1, clip_sample=False)
+    s.set_timesteps(50)
+    ts = s.timesteps.repeat(40)
+    loops = {}
+    for arm in ("fused", "transposes"):
+        sh = EmulatedShard(args.world, 1, args.comm, args.window)
+        sh.fused = arm == "fused"
+        unet.dist = sh
+        unet.prepare()
+        loops[arm] = DenoiseLoop(unet, s, lat.clone(), ehs, 7.5, timesteps=ts, use_graph=True).prime()
+        assert loops[arm].graph is not None, loops[arm].graph_error
+        loops[arm].run(3)
+    res = {a: [] for a in loops}
+    for _ in range(args.ab_fused):
+        for arm, lp in loops.items():
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            lp.run(args.steps)
+            torch.cuda.synchronize()
+            res[arm].append(1e3 * (time.perf_counter() - t0) / args.steps)
+    for arm, v in res.items():
+        v = sorted(v)
+        print(f"world {args.world} {arm}: median {v[len(v) // 2]:.3f} ms/step, min {v[0]:.3f} (rounds {len(v)})")
+    print(json.dumps({"world": args.world, "ab": {a: sorted(v) for a, v in res.items()}}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
@@ -63,7 +96,12 @@ def main():
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--mq", default="on", choices=["on", "off", "both"],
                     help="motion-module Q/K/V projection fused into the temporal attention (A/B with both)")
+    ap.add_argument("--ab-fused", type=int, default=0,
+                    help="same-process A/B of FrameShard.fused (the round-5 re-shard without transposes) "
+                         "against the transposes: N alternating rounds of --steps steps per arm")
     args = ap.parse_args()
+    if args.ab_fused:
+        return ab_fused(args)
     unet = materialize_synthetic("full", device="cuda", seed=0)
     fl = args.frames // args.world
     lat = torch.randn(1, 4, fl, 64, 64, device="cuda")

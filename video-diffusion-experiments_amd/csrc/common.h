@@ -109,3 +109,36 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
+
+// The frame-sharded motion module's re-shard row permutation (round 5): rows
+// m = ((i0*n1 + i1)*n2 + i2)*inner + j  ->  ((i2*n1 + i1)*n0 + i0)*inner + j  ("rev3": the three
+// outer axes reversed; vdiff.dist.FrameShard.send_perm / return_perm), n1, n2, inner powers of
+// two (checked by the callers), n0 = rows / (n1*n2*inner).  Shifts and masks only, all of them
+// wave-uniform: the map costs a few VALU per row and no VGPR that outlives it.  inner == 0:
+// identity.
+struct Rev3 {
+  int n0, sh1, sh2, shi;  // shi < 0: identity
+  __host__ __device__ static int lg(int64_t v) {
+    int s = 0;
+    while (s < 62 && (int64_t{1} << s) < v) ++s;
+    return s;
+  }
+  __host__ __device__ Rev3(int64_t rows, int64_t n1, int64_t n2, int64_t inner)
+      : n0(0), sh1(0), sh2(0), shi(-1) {
+    if (inner <= 0) return;
+    sh1 = lg(n1); sh2 = lg(n2); shi = lg(inner);
+    n0 = (int)(rows >> (sh1 + sh2 + shi));
+  }
+  __host__ __device__ static bool ok(int64_t rows, int64_t n1, int64_t n2, int64_t inner) {
+    auto p2 = [](int64_t v) { return v > 0 && (v & (v - 1)) == 0; };
+    return inner == 0 || (p2(n1) && p2(n2) && p2(inner) && rows % (n1 * n2 * inner) == 0 && rows < 0x7fffffff);
+  }
+  __device__ __forceinline__ int operator()(int m) const {
+    if (shi < 0) return m;
+    const uint32_t u = (uint32_t)m;
+    const uint32_t j = u & ((1u << shi) - 1u), q = u >> shi;
+    const uint32_t i2 = q & ((1u << sh2) - 1u), q1 = q >> sh2;
+    const uint32_t i1 = q1 & ((1u << sh1) - 1u), i0 = q1 >> sh1;
+    return (int)(((((i2 << sh1) + i1) * (uint32_t)n0 + i0) << shi) + j);
+  }
+};

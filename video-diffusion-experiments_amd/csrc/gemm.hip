@@ -41,7 +41,9 @@ struct Div {
   }
 };
 
-template <int MB, int NB>
+// PERM: the vd_gemm_desc.rmap_* output-row map (instantiated only by the kernels the plan gives
+// an rmap request — v6, v1; the v2 / v3 / v5 pipelines sit at 256 VGPRs and spill with it)
+template <int MB, int NB, bool PERM = false>
 __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], int mbase,
                                               int nbase, int lane, int nodd = -1) {
   // acc[a][b][j] = C[m = mbase + b*16 + fr][n = nbase + a*16 + 4*fq + j]  (the wave's sub-tile);
@@ -50,12 +52,13 @@ __device__ __forceinline__ void gemm_epilogue(const vd_gemm_desc& d, f32x4 (&acc
   const int M = (int)d.M, N = (int)d.N;
   const int fr = lane & 15, fq = lane >> 4;
   const int nw = nbase;
+  const Rev3 perm = PERM ? Rev3(d.M, d.rmap_n1, d.rmap_n2, d.rmap_inner) : Rev3(0, 0, 0, 0);
   // per-row values are recomputed inside each loop (arrays of MB row pointers kept
   // live across the whole epilogue cost 3 x MB VGPRs beside MB x NB x 4 accumulators)
 #define VD_EPI_ROW(b)                                       \
   const int m_ = mbase + (b) * 16 + fr;                     \
   const bool mok_ = m_ < M;                                 \
-  const int mrow_ = mok_ ? m_ : 0;
+  const int mrow_ = mok_ ? (PERM ? perm(m_) : m_) : 0;
   // Wide path (T21 for the 16x16 layout): v_permlane16_swap of 16-column blocks
   // (a, a+1) leaves each lane 8 CONSECUTIVE channels — lane group g of the pair
   // holds columns 16a + 16(g&1) + 8(g>>1) .. +7 — so residual loads and bf16
@@ -395,7 +398,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
     __syncthreads();
   }
 
-  gemm_epilogue<MB, NB>(d, acc, (int)m0 + wm * MB * 16, (int)n0 + wn * (BN / 2), lane);
+  if (d.rmap_inner)
+    gemm_epilogue<MB, NB, true>(d, acc, (int)m0 + wm * MB * 16, (int)n0 + wn * (BN / 2), lane);
+  else
+    gemm_epilogue<MB, NB>(d, acc, (int)m0 + wm * MB * 16, (int)n0 + wn * (BN / 2), lane);
 }
 
 // ============================================================================ v2
@@ -1277,7 +1283,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
   const int hgrid = d.upsample ? 2 * d.h_in : d.h_in;
   const int wgrid = d.upsample ? 2 * d.w_in : d.w_in;
   // load-free epilogue (epi_fast) for plain bf16 outputs
-  const bool fast = !LN && split == 1 && !d.res && !d.rowbias && !d.out_f32 && (N % 8) == 0 &&
+  const bool fast = !LN && split == 1 && !d.res && !d.rowbias && !d.out_f32 && !d.rmap_inner && (N % 8) == 0 &&
                     (d.ldc % 8) == 0 && (((uintptr_t)d.out) & 15) == 0;
   const __amdgpu_buffer_rsrc_t rbias = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(d.bias ? d.bias : (const float*)d.a0), 0, d.bias ? (uint32_t)(N * 4) : 0u, 0x00020000);
@@ -1677,7 +1683,10 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
   }
   const int mbase = (int)m0 + wm * 32, nbase = (int)n0 + wn * 32;
   if (split == 1) {
-    gemm_epilogue<MB, NB>(d, acc, mbase, nbase, lane);
+    if (d.rmap_inner)
+      gemm_epilogue<MB, NB, true>(d, acc, mbase, nbase, lane);
+    else
+      gemm_epilogue<MB, NB>(d, acc, mbase, nbase, lane);
     return;
   }
   // ---- split K: slab, arrival counter, last arriver reduces.  Round 2: the hand-off is the
@@ -1749,6 +1758,7 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
     }
     const int64_t o = n0 + c4;
     if (o >= N) continue;
+    const int64_t mo = Rev3(d.M, d.rmap_n1, d.rmap_n2, d.rmap_inner)((int)m);  // output / residual row
     float v[4] = {0, 0, 0, 0};
     for (int s2 = 0; s2 < split; ++s2) {
       const float4 a4 = slab4(s2, m, o);
@@ -1765,13 +1775,13 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
     if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU)
       for (int j = 0; j < 4; ++j) v[j] = act_pw(d.act, v[j]);
     if (d.res) {
-      const uint2 r2 = *(const uint2*)((const bf16_t*)d.res + m * d.ld_res + o);
+      const uint2 r2 = *(const uint2*)((const bf16_t*)d.res + mo * d.ld_res + o);
       v[0] += bf_lo(r2.x); v[1] += bf_hi(r2.x); v[2] += bf_lo(r2.y); v[3] += bf_hi(r2.y);
     }
     if (d.out_f32)
-      *(float4*)((float*)d.out + m * d.ldc + o) = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)((float*)d.out + mo * d.ldc + o) = make_float4(v[0], v[1], v[2], v[3]);
     else
-      *(uint2*)((bf16_t*)d.out + m * d.ldc + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      *(uint2*)((bf16_t*)d.out + mo * d.ldc + o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
   }
 }
 
@@ -1785,9 +1795,10 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
   const int total = (int)(M * (nout / 4));
   const Div dq((int)(nout / 4)), drb(d.rowbias ? (int)d.rb_div : 1);
   const float* ws = (const float*)d.ws;
+  const Rev3 perm(d.M, d.rmap_n1, d.rmap_n2, d.rmap_inner);
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     const int m32 = dq(i);
-    const int64_t m = m32;
+    const int64_t m = m32, mo = perm(m32);  // slab row, output / residual row
     const int64_t o = (int64_t)(i - m32 * (int)(nout / 4)) * 4;
     float o4[4];
     if (geglu) {
@@ -1823,15 +1834,15 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
       if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU)
         for (int j = 0; j < 4; ++j) v[j] = act_pw(d.act, v[j]);
       if (d.res) {
-        const uint2 r = *(const uint2*)((const bf16_t*)d.res + m * d.ld_res + o);
+        const uint2 r = *(const uint2*)((const bf16_t*)d.res + mo * d.ld_res + o);
         v[0] += bf_lo(r.x); v[1] += bf_hi(r.x); v[2] += bf_lo(r.y); v[3] += bf_hi(r.y);
       }
       for (int j = 0; j < 4; ++j) o4[j] = v[j];
     }
     if (d.out_f32)
-      *(float4*)((float*)d.out + m * d.ldc + o) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+      *(float4*)((float*)d.out + mo * d.ldc + o) = make_float4(o4[0], o4[1], o4[2], o4[3]);
     else
-      *(uint2*)((bf16_t*)d.out + m * d.ldc + o) = make_uint2(pack2(o4[0], o4[1]), pack2(o4[2], o4[3]));
+      *(uint2*)((bf16_t*)d.out + mo * d.ldc + o) = make_uint2(pack2(o4[0], o4[1]), pack2(o4[2], o4[3]));
   }
 }
 
@@ -1864,7 +1875,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
 constexpr int G8_BN = 160, G8_KMAX = 320, G8_NW = 8;
 constexpr int G8_SUB = G8_BN * BK * 2;  // one 64-deep W sub-tile: 20 KiB
 
-template <bool RES, bool GEGLU>
+template <bool RES, bool GEGLU, bool PERM = false>
 __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                              uint32_t w_bytes, uint32_t c_bytes, int tiles_n,
                                                              int groups) {
@@ -1908,6 +1919,7 @@ __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc
                                         0x00020000);
   const int fr = lane & 15, fq = lane >> 4;
   const int wcol = 16 * (fq & 1) + 8 * (fq >> 1);  // lane's column offset inside a swapped pair
+  const Rev3 perm = PERM ? Rev3(d.M, d.rmap_n1, d.rmap_n2, d.rmap_inner) : Rev3(0, 0, 0, 0);  // row map
   // this lane's A fragments of row block rb: past the buffer (read as zeros, no traffic) for
   // rows >= M and for row blocks past the XCD's range
   auto load_a = [&](bf16x8 (&x)[KS], int rb) {
@@ -1922,7 +1934,7 @@ __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc
     const int m = rb * 16 + fr;
 #pragma unroll
     for (int pr = 0; pr < NB / 2; ++pr) {
-      const uint32_t off = m < M ? (uint32_t)(m * (int)d.ld_res + n0 + pr * 32 + wcol) * 2u : G2_OOB;
+      const uint32_t off = m < M ? (uint32_t)((PERM ? perm(m) : m) * (int)d.ld_res + n0 + pr * 32 + wcol) * 2u : G2_OOB;
       rsv[pr] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
     }
   };
@@ -2015,7 +2027,7 @@ __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc
       const int q = it * 64 + lane, row = q / 20, ch = q - row * 20;
       const uint4 v = *(const uint4*)(obuf + row * OROW + ch * 16);
       const int m = rb * 16 + row;
-      const uint32_t off = m < M ? (uint32_t)(m * (int)d.ldc + n0 + ch * 8) * 2u : G2_OOB;
+      const uint32_t off = m < M ? (uint32_t)((PERM ? perm(m) : m) * (int)d.ldc + n0 + ch * 8) * 2u : G2_OOB;
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rc, off, 0, 0);
     }
   };
@@ -2121,6 +2133,8 @@ int launch8(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t wb) {
   const dim3 grid((unsigned)(8 * per_xcd)), block(G8_NW * 64);
   if (d.act == VD_ACT_GEGLU)
     hipLaunchKernelGGL((gemm8_kernel<false, true>), grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
+  else if (d.res && d.rmap_inner)
+    hipLaunchKernelGGL((gemm8_kernel<true, false, true>), grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
   else if (d.res)
     hipLaunchKernelGGL((gemm8_kernel<true, false>), grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
   else
@@ -2134,7 +2148,7 @@ int launch3(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   // persistent: one workgroup per CU, ceil(units / CUs) units each, balanced grid
   const int64_t rounds = (units + g_num_cus - 1) / g_num_cus;
   const int64_t grid = (units + rounds - 1) / rounds;
-  const int fast = split == 1 && !d.res && !d.rowbias && !d.out_f32 && d.N % 8 == 0 &&
+  const int fast = split == 1 && !d.res && !d.rowbias && !d.out_f32 && !d.rmap_inner && d.N % 8 == 0 &&
                    d.N <= G3_BIAS_N && d.ldc % 8 == 0 && ((uintptr_t)d.out & 15) == 0 &&
                    d.M * d.ldc * 2 < (int64_t)G2_OOB;
   hipLaunchKernelGGL((gemm3_kernel<VD_A_DENSE>), dim3((unsigned)grid), dim3(G3_NT), 0, s, d, a0b, a1b, wb, split,
@@ -2161,6 +2175,8 @@ struct Plan {
 // workgroups: 66 -> 38 us, 41 -> 30 us against a cap of 8; neutral elsewhere —
 // profiles/r01_gemm_paths.txt)
 constexpr int SPLIT_CAP = 32;
+
+inline int64_t nk_of(const vd_gemm_desc& d) { return d.K / BK; }
 
 inline int split_for(int64_t tiles, int64_t nk) {
   if (tiles >= 192 || nk < 16) return 1;
@@ -2219,6 +2235,25 @@ Plan plan(const vd_gemm_desc& d) {
   // the LayerNorm unfused there as well the 4-frame step went 17.47 -> 17.04 ms,
   // profiles/r04_gemm_v8.txt)
   const bool v8auto = v8ok && M >= 16384;
+  // an output-row map (rmap; no ln_out, GEGLU or row bias — checked) is carried by v8 (with a
+  // residual), v6 and v1 only: the v2 / v3 / v5 pipelines sit at their register limit and spill
+  // with it (tests/test_kernel_resources.py).  v6 splits K only where forced (path 6).
+  if (d.rmap_inner) {
+    if (v8ok && d.res && (path == 0 || path == 8)) {
+      p.ver = 8;
+      p.bn = G8_BN;
+    } else if (k64 && d.N >= 64 && d.kt <= 1 && d.ks != 1 && (path == 0 || path == 6)) {
+      p.ver = 6;
+      p.bn = 64;
+      const int64_t tiles6 = ((M + G6_BM - 1) / G6_BM) * ((d.N + G6_BN - 1) / G6_BN);
+      int64_t sp = 1;
+      while (path == 6 && tiles6 * sp < 2 * g_num_cus && nk_of(d) / (sp * 2) >= 4 && sp < 16) sp *= 2;
+      p.split = (int)sp;
+      const int64_t rtiles6 = ((d.M + G6_BM - 1) / G6_BM) * ((d.N + G6_BN - 1) / G6_BN);
+      p.ws_bytes = p.split > 1 ? (int64_t)p.split * d.M * d.N * 4 + ((rtiles6 * 4 + 255) / 256) * 256 : 0;
+    }
+    return p;
+  }
   // fused LayerNorm epilogue: one 256 x 320 tile owns whole rows (v5, unsplit; >= 128 tiles so
   // the unsplit grid fills half the chip — smaller M runs the GEMM + vd_layernorm instead)
   if (d.ln_out) {
@@ -2401,6 +2436,10 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
     if (d.k0 < d.K) VD_CHECK_ARG(d.a1 != nullptr);
   }
   if (d.act == VD_ACT_GEGLU) VD_CHECK_ARG(d.N % 32 == 0 && !d.res && !d.rowbias && !d.out_f32);
+  VD_CHECK_ARG(d.rmap_inner >= 0);
+  if (d.rmap_inner > 0)
+    VD_CHECK_ARG(Rev3::ok(d.M, d.rmap_n1, d.rmap_n2, d.rmap_inner) && !d.ln_out && !d.rowbias &&
+                 d.act != VD_ACT_GEGLU);
   if (d.ln_out) {
     VD_CHECK_ARG(!d.out_f32 && d.act != VD_ACT_GEGLU && d.ln_gamma && d.ln_beta && al16(d.ln_gamma) &&
                  al16(d.ln_beta) && d.ld_ln % 4 == 0 && al8(d.ln_out) && d.N % 4 == 0);

@@ -227,7 +227,7 @@ __global__ __launch_bounds__(NT) void gn_apply_kernel(const bf16_t* x0, int64_t 
                                                       const bf16_t* x1, int64_t ldx1, int64_t C,
                                                       int64_t rows, int64_t pix_per_inst,
                                                       const float2* ss, int silu, bf16_t* y,
-                                                      int64_t ldy) {
+                                                      int64_t ldy, Rev3 perm) {
   const int64_t nch = C / 8;
   const int64_t total = rows * nch;
   // 32-bit row / chunk split (the common case; an int64 division per chunk otherwise)
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(NT) void gn_apply_kernel(const bf16_t* x0, int64_t 
 #pragma unroll
       for (int e = 0; e < 8; ++e) f[e] = silu_f(f[e]);
     }
-    *(uint4*)(y + row * ldy + c) = pack8(f);
+    *(uint4*)(y + (int64_t)perm((int)row) * ldy + c) = pack8(f);
   }
 }
 
@@ -538,21 +538,30 @@ extern "C" int vd_gn_finalize(const float* ws, int64_t n_inst, int32_t n_split_t
   return vd_launch_status();
 }
 
-extern "C" int vd_gn_apply(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1,
-                           int64_t C, int64_t n_inst, int64_t pix_per_inst,
-                           const float* scale_shift, int32_t silu, void* y, int64_t ldy,
-                           vd_stream_t stream) {
+extern "C" int vd_gn_apply_rev3(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1,
+                                int64_t C, int64_t n_inst, int64_t pix_per_inst, const float* scale_shift,
+                                int32_t silu, void* y, int64_t ldy, int64_t n1, int64_t n2, int64_t inner,
+                                vd_stream_t stream) {
   VD_CHECK_ARG(x0 && y && scale_shift && C > 0 && C % 8 == 0 && c0 % 8 == 0 && c0 > 0 && c0 <= C);
   VD_CHECK_ARG(ldx0 % 8 == 0 && ldy % 8 == 0 && al16(x0) && al16(y) && al16(scale_shift));
   if (c0 < C) VD_CHECK_ARG(x1 && ldx1 % 8 == 0 && al16(x1));
   const int64_t rows = n_inst * pix_per_inst;
+  VD_CHECK_ARG(rows < 0x7fffffff && inner >= 0 && Rev3::ok(rows, n1, n2, inner));
   const int64_t total = rows * (C / 8);
   const int64_t blocks = (total + NT - 1) / NT;
   const unsigned grid = (unsigned)(blocks < 8192 ? blocks : 8192);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream,
                      (const bf16_t*)x0, ldx0, c0, (const bf16_t*)x1, ldx1, C, rows, pix_per_inst,
-                     (const float2*)scale_shift, silu, (bf16_t*)y, ldy);
+                     (const float2*)scale_shift, silu, (bf16_t*)y, ldy, Rev3(rows, n1, n2, inner));
   return vd_launch_status();
+}
+
+extern "C" int vd_gn_apply(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1,
+                           int64_t C, int64_t n_inst, int64_t pix_per_inst,
+                           const float* scale_shift, int32_t silu, void* y, int64_t ldy,
+                           vd_stream_t stream) {
+  return vd_gn_apply_rev3(x0, ldx0, c0, x1, ldx1, C, n_inst, pix_per_inst, scale_shift, silu, y, ldy, 1, 1, 0,
+                          stream);
 }
 
 extern "C" int vd_layernorm(const void* x, int64_t ldx, int64_t rows, int64_t C, const float* gamma,

@@ -30,6 +30,8 @@ SIGNATURES = {
     "vd_gn_partial": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp], c_i32),
     "vd_gn_finalize": ([c_vp, c_i64, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp], c_i32),
     "vd_gn_apply": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_i64, c_vp], c_i32),
+    "vd_gn_apply_rev3": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_i64,
+                          c_i64, c_i64, c_i64, c_vp], c_i32),
     "vd_gn_partial_g": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp], c_i32),
     "vd_gn_apply_g": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64, c_i64, c_vp], c_i32),
     "vd_layernorm": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
@@ -90,6 +92,7 @@ class GemmDesc(C.Structure):
         ("ln_pe", c_vp), ("ln_pe_div", c_i64), ("ln_pe_period", c_i64),
         ("ln_out", c_vp), ("ld_ln", c_i64),
         ("path", c_i32), ("plan_m", c_i64),
+        ("rmap_n1", c_i32), ("rmap_n2", c_i32), ("rmap_inner", c_i32),
     ]
 
 

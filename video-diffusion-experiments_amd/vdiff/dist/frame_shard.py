@@ -55,6 +55,7 @@ class FrameShard:
             raise ValueError(f"window must be one of {self.WINDOWS}")
         self.chunks = overlap_chunks
         self.window = window
+        self.fused = True  # the fused re-shard where it applies (fused_ok); False: the transposes (A/B)
         self._side = {}  # device -> compute stream of the overlapped temporal window
 
     def frames_local(self, frames: int) -> int:
@@ -105,6 +106,38 @@ class FrameShard:
         send = transpose(hp, batch, W, frames_local * pl)           # (r', b, f_loc, pl)
         recv = self._a2a(send)                                      # (r,  b, f_loc, pl)  r = position chunk
         return transpose(recv, W, batch * frames_local, pl)         # (b, f_loc, r, pl) = (b, f_loc, p)
+
+    # -- the fused re-shard (round 5): no transposes around the all-to-alls ---------------
+    # The frame-sharded rows of a rank are (b, f_loc, p) with p = (r', j), r' the position chunk
+    # rank r' takes, j < pl = hw / world.  The motion norm writes them straight into the send
+    # order (r', f_loc, b, j) (vd_gn_apply_rev3 with send_perm), so what a rank receives is
+    # (r, f_loc, b, j) = (f, b, j): frame-major rows of ALL frames of its pl positions of both
+    # videos — the temporal attention's layout with one "video" and b*pl + j as the position
+    # (frame stride batch*pl), so the transformer block runs on the received rows as they are.
+    # Its output rows (f, b, j) are already in the returning all-to-all's send order (chunk r =
+    # rank r's frames), and the rows that come back, (r', f_loc, b, j), are mapped into the
+    # rank's (b, f_loc, r', j) layout by proj_out's epilogue (vd_gemm_desc.rmap_*, return_perm),
+    # which also reads the residual there.  Four vd_block_transpose launches per motion module
+    # fewer than to_position_shards / to_frame_shards, the same bytes on the wire.
+    def fused_ok(self, batch: int, frames_local: int, hw: int) -> bool:
+        """The fused re-shard applies: a2a window, no chunked overlap, power-of-two axes (the
+        rev3 row maps are shifts)."""
+        def p2(v):
+            return v > 0 and v & (v - 1) == 0
+        return (getattr(self, "fused", True) and self.window == "a2a" and self.chunks == 1 and hw % self.world == 0
+                and all(p2(v) for v in (hw // self.world, self.world, batch, frames_local)))
+
+    def send_perm(self, batch: int, frames_local: int, hw: int):
+        """rev3 (n1, n2, inner) taking rows (b, f_loc, r', j) to the send order (r', f_loc, b, j)."""
+        return (frames_local, self.world, hw // self.world)
+
+    def return_perm(self, batch: int, frames_local: int, hw: int):
+        """rev3 (n1, n2, inner) taking the returned rows (r', f_loc, b, j) to (b, f_loc, r', j)."""
+        return (frames_local, batch, hw // self.world)
+
+    def exchange(self, x: torch.Tensor) -> torch.Tensor:
+        """One all-to-all of equal row chunks (chunk r to rank r), on the current stream."""
+        return self._a2a(x)
 
     def _side_stream(self, device):
         if device not in self._side:
@@ -187,6 +220,14 @@ class FrameShard:
         parts = torch.empty(self.world * x.numel(), device=x.device, dtype=x.dtype)
         dist.all_gather_into_tensor(parts, x.contiguous().reshape(-1), group=self.group)
         return torch.cat(list(parts.reshape((self.world,) + tuple(x.shape)).unbind(0)), dim=2)
+
+
+def rev3_reference(src: torch.Tensor, n1: int, n2: int, inner: int) -> torch.Tensor:
+    """torch statement of the rev3 row map (vd_gn_apply_rev3, vd_gemm_desc.rmap_*): input row
+    ((i0*n1 + i1)*n2 + i2)*inner + j goes to output row ((i2*n1 + i1)*n0 + i0)*inner + j."""
+    w = src.shape[1]
+    n0 = src.shape[0] // (n1 * n2 * inner)
+    return src.reshape(n0, n1, n2, inner, w).permute(2, 1, 0, 3, 4).reshape(-1, w).contiguous()
 
 
 def block_transpose_reference(src: torch.Tensor, nb: int, na: int, nc: int) -> torch.Tensor:

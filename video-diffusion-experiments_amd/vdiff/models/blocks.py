@@ -258,9 +258,26 @@ class AnimateDiffTransformer3D(nn.Module):
         B, Fl = ctx.batch, ctx.frames
         dist = ctx.dist
         gather = dist.gather_gn_partials if dist is not None else None
+        blk = self.transformer_blocks[0]
+        if dist is not None and dist.fused_ok(B, Fl, hw):
+            # the fused re-shard (FrameShard.send_perm): norm -> send order, one all-to-all, the
+            # block on the received (frame, video, position) rows, one all-to-all back, proj_out
+            # writing the returned rows into this rank's layout with the residual
+            pl = hw // dist.world
+            F = Fl * dist.world
+            hn = ops.group_norm(x.t, B, Fl * hw, self.groups, 1e-6, self.norm._g, self.norm._b, gather=gather,
+                                two_pass=False, n_split=Fl * ops.gn_splits_per_frame(hw),
+                                rev3=dist.send_perm(B, Fl, hw))
+            recv = dist.exchange(hn)                                   # rows (f, b, j)
+            h, n = ops.gemm_ln(recv, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b, pe=blk.pos_embed._pe,
+                               pe_div=B * pl, pe_period=F)
+            h = blk.run_temporal(h, 1, F, B * pl, n=n)
+            back = dist.exchange(h)                                    # rows (r', f_loc, b, j)
+            out = ops.gemm(back, self.proj_out._w, bias=self.proj_out._b, res=x.t,
+                           rmap=dist.return_perm(B, Fl, hw))
+            return Act(out, x.n, x.h, x.w)
         hn = ops.group_norm(x.t, B, Fl * hw, self.groups, 1e-6, self.norm._g, self.norm._b, gather=gather,
                             two_pass=False, n_split=Fl * ops.gn_splits_per_frame(hw))
-        blk = self.transformer_blocks[0]
         if dist is None:  # norm1 (+ PE by frame) fused into proj_in's epilogue
             h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b, pe=blk.pos_embed._pe,
                                pe_div=hw, pe_period=Fl)

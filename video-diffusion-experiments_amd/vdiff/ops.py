@@ -82,8 +82,10 @@ def _run_gemm(d, device, what):
 
 
 def gemm(a, w, *, a1=None, bias=None, rowbias=None, rb_div=1, res=None, act=ACT_NONE,
-         out=None, out_f32=False):
-    """out[m, n] = epi(sum_k cat(a, a1)[m, k] * w[n, k]); a/a1/w bf16, bias/rowbias fp32."""
+         out=None, out_f32=False, rmap=None):
+    """out[m, n] = epi(sum_k cat(a, a1)[m, k] * w[n, k]); a/a1/w bf16, bias/rowbias fp32.
+    rmap = (n1, n2, inner): product row m is written (and its residual read) at row rev3(m)
+    (vd_gemm_desc.rmap_*, vdiff.dist.frame_shard.rev3_reference)."""
     _dev(a, w, a1, bias, rowbias, res, out)
     M = a.shape[0]
     N, K = w.shape
@@ -104,6 +106,8 @@ def gemm(a, w, *, a1=None, bias=None, rowbias=None, rb_div=1, res=None, act=ACT_
                  res=_p(res), ld_res=_rows(res) if res is not None else 0, act=act,
                  out=_p(out), ldc=_rows(out, torch.float32 if out_f32 else BF16),
                  out_f32=int(out_f32))
+    if rmap is not None:
+        d.rmap_n1, d.rmap_n2, d.rmap_inner = (int(v) for v in rmap)
     _run_gemm(d, a.device, "vd_gemm")
     return out
 
@@ -228,19 +232,21 @@ def gn_finalize(ws, groups, eps, gamma, beta):
     return ss
 
 
-def gn_apply(x, ss, pix, silu, x1=None, out=None):
+def gn_apply(x, ss, pix, silu, x1=None, out=None, rev3=None):
+    """rev3 = (n1, n2, inner): input row m lands at output row rev3(m) (vd_gn_apply_rev3)."""
     _dev(x, x1, ss)
     n_inst, C, _ = ss.shape
     if out is None:
         out = torch.empty(x.shape[0], C, device=x.device, dtype=BF16)
-    check(lib().vd_gn_apply(_p(x), _rows(x), x.shape[1], _p(x1), _rows(x1) if x1 is not None else 0,
-                            C, n_inst, pix, _p(ss), int(silu), _p(out), _rows(out), _stream()),
-          "vd_gn_apply")
+    n1, n2, inner = rev3 if rev3 is not None else (1, 1, 0)
+    check(lib().vd_gn_apply_rev3(_p(x), _rows(x), x.shape[1], _p(x1), _rows(x1) if x1 is not None else 0,
+                                 C, n_inst, pix, _p(ss), int(silu), _p(out), _rows(out), n1, n2, inner,
+                                 _stream()), "vd_gn_apply_rev3")
     return out
 
 
 def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, gather=None, two_pass=True,
-               n_split=None):
+               n_split=None, rev3=None):
     """GroupNorm(+SiLU) over NHWC rows; instance = `pix` consecutive rows.
     Image-instance norms (two_pass): per-group partial records, and an apply that finalizes
     them itself (two launches).  The motion-module norm (two_pass=False: its instance is a
@@ -253,13 +259,13 @@ def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, ga
     blocks on an arrival counter) was slower at every image norm of the step and is gone
     (round 4, profiles/r04_gn_one_launch_refuted.txt)."""
     C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
-    if two_pass and gather is None and C <= 2560 and 256 % groups == 0:
+    if two_pass and gather is None and rev3 is None and C <= 2560 and 256 % groups == 0:
         return group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=silu, x1=x1)
     ws = gn_partial(x, C, n_inst, pix, n_split or gn_splits(n_inst, pix), x1=x1)
     if gather is not None:
         ws = gather(ws)
     ss = gn_finalize(ws, groups, eps, gamma, beta)
-    return gn_apply(x, ss, pix, silu, x1=x1)
+    return gn_apply(x, ss, pix, silu, x1=x1, rev3=rev3)
 
 
 def group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, out=None, n_split=None):
