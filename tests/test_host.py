@@ -85,9 +85,14 @@ def test_prepare_latents_follows_randn_tensor_cpu_fp16():
     with torch.device("meta"):
         unet = UNetMotionModel("tiny")
     pipe = AnimateDiffPipeline(unet.to_empty(device="cpu"))
+    pipe.torch_dtype = torch.float16  # from_pretrained(..., torch_dtype=torch.float16), as 05:130-134
     x = pipe.prepare_latents(1, 16, 64, 64, generator=torch.manual_seed(42))
     want = torch.randn((1, 4, 16, 64, 64), generator=torch.manual_seed(42), dtype=torch.float16)
     assert x.dtype == torch.float32 and torch.equal(x, want.float())
+    # torch_dtype=None: diffusers draws in prompt_embeds.dtype = fp32
+    pipe.torch_dtype = None
+    x = pipe.prepare_latents(1, 16, 64, 64, generator=torch.manual_seed(42))
+    assert torch.equal(x, torch.randn((1, 4, 16, 64, 64), generator=torch.manual_seed(42)))
 
 
 def test_randn_tensor_generator_devices():

@@ -19,10 +19,11 @@ LLVM = Path("/opt/rocm/lib/llvm/bin")
 LIB = Path(__file__).resolve().parents[1] / "video-diffusion-experiments_amd" / "vdiff" / "libvdiff_hip.so"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
-# kernels allowed to spill, with their ceiling; everything else must not spill at all
-# (all three at these counts since round 3; 256 VGPRs at their occupancy)
-#  flash40: 5-6 spilled (outside the MFMA segments); flash512 (VAE mid-block attention, d=512): 4; gemm4's conv instance: 2
-ALLOWED = {"flash40_kernel": 6, "flash512_kernel": 4, "gemm4_kernelILi320ELi4ELi2ELi4ELi1E": 2}
+# kernels allowed to spill, with their ceiling (their real counts); everything else must not spill
+# at all.  flash512 (VAE mid-block attention, d = 512, 512 registers): 3-4; gemm4's conv instance
+# (256 VGPRs): 2.  flash40 has spilled nothing since round 4's fragment-read interleave and is held
+# to 0 like every other kernel (VERDICT r04 housekeeping).
+ALLOWED = {"flash512_kernel": 4, "gemm4_kernelILi320ELi4ELi2ELi4ELi1E": 2}
 
 
 def _kernels(tmp_path):
@@ -36,15 +37,22 @@ def _kernels(tmp_path):
                    check=True, capture_output=True)
     blob = fat.read_bytes()
     starts = [m.start() for m in re.finditer(re.escape(MAGIC), blob)]
-    assert starts, "no offload bundle in .hip_fatbin"
+    if not starts:
+        pytest.skip("no uncompressed offload bundle in .hip_fatbin (compressed bundles are not read here)")
+    # the device target the library was built for (VDIFF_ARCH, default gfx950), from the bundle ids
+    targets = sorted(set(re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob)))
+    if not targets:
+        pytest.skip("no hipv4 amdgcn target id in the offload bundles")
+    target = f"hipv4-amdgcn-amd-amdhsa--{targets[0].decode()}"
     out = {}
     for i, s in enumerate(starts):
         chunk = tmp_path / f"b{i}"
         chunk.write_bytes(blob[s:starts[i + 1] if i + 1 < len(starts) else len(blob)])
         co = tmp_path / f"b{i}.co"
-        subprocess.run([str(LLVM / "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={chunk}",
-                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True,
-                       capture_output=True)
+        r = subprocess.run([str(LLVM / "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={chunk}",
+                            f"--targets={target}", f"--output={co}"], capture_output=True)
+        if r.returncode != 0 or not co.exists():
+            pytest.skip(f"cannot unbundle {target} from bundle {i}: {r.stderr.decode()[-200:]}")
         notes = subprocess.run([str(LLVM / "llvm-readelf"), "--notes", str(co)], check=True,
                                capture_output=True, text=True).stdout
         cur = None

@@ -2209,7 +2209,7 @@ void read_num_cus() {  // once per process: the plan (and the workspace size) de
 Plan plan(const vd_gemm_desc& d) {
   read_num_cus();
   Plan p;
-  const int path = d.path;
+  int path = d.path;
   const int64_t M = d.plan_m > 0 ? d.plan_m : d.M;  // the row count the plan is made for
   if (path == 1 || d.K % G4_BK || d.k0 % G4_BK || M < G6_BM || (d.N < 64 && d.N > 32)) return p;
   const int64_t a_rows = d.a_mode == VD_A_CONV3X3
@@ -2235,6 +2235,7 @@ Plan plan(const vd_gemm_desc& d) {
   // the LayerNorm unfused there as well the 4-frame step went 17.47 -> 17.04 ms,
   // profiles/r04_gemm_v8.txt)
   const bool v8auto = v8ok && M >= 16384;
+  if (path == 8 && !v8ok) path = 0;  // forced v8 on a shape it does not take: the product plan
   // an output-row map (rmap; no ln_out, GEGLU or row bias — checked) is carried by v8 (with a
   // residual), v6 and v1 only: the v2 / v3 / v5 pipelines sit at their register limit and spill
   // with it (tests/test_kernel_resources.py).  v6 splits K only where forced (path 6).

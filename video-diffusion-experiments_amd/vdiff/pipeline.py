@@ -223,6 +223,9 @@ class AnimateDiffPipeline:
         self.vae = vae
         self.dist = dist
         self.unet.dist = dist
+        # the dtype the initial noise is drawn in (diffusers: prompt_embeds.dtype, i.e. the
+        # pipeline's torch_dtype, fp32 when none is given); from_config keeps the reference's fp16
+        self.torch_dtype = None
 
     @classmethod
     def from_config(cls, config="full", device="cuda", seed=0, scheduler=None, dist=None, vae="auto"):
@@ -239,7 +242,9 @@ class AnimateDiffPipeline:
                                                        clip_sample=False)
         if isinstance(vae, str):
             vae = init_synthetic_(AutoencoderKL(vae), seed).to(device=device, dtype=torch.bfloat16).prepare()
-        return cls(unet, sched, dist=dist, vae=vae)
+        pipe = cls(unet, sched, dist=dist, vae=vae)
+        pipe.torch_dtype = cls.latent_draw_dtype  # the reference's torch_dtype=torch.float16 (05:35)
+        return pipe
 
     @classmethod
     def from_pretrained(cls, pretrained_model_name_or_path, motion_adapter=None, torch_dtype=None, variant=None,
@@ -307,10 +312,11 @@ class AnimateDiffPipeline:
         """diffusers AnimateDiffPipeline.prepare_latents -> fp32 on the GPU, x init_noise_sigma.
         The draw follows randn_tensor: on the generator's device (a CPU generator from 05:156's
         torch.manual_seed, a CUDA one from 01:103's torch.Generator("cuda")), in the pipeline's
-        torch_dtype (float16 in the reference, 01:21 / 05:35), then moved."""
+        torch_dtype (float16 in the reference, 01:21 / 05:35; fp32 when the pipeline was loaded
+        with torch_dtype=None, as diffusers draws in prompt_embeds.dtype), then moved."""
         if latents is None:
             shape = (batch, self.unet.config["in_channels"], num_frames, h, w)
-            dtype = getattr(self, "torch_dtype", None) or self.latent_draw_dtype
+            dtype = self.torch_dtype or torch.float32
             latents = randn_tensor(shape, generator=generator, device=self.unet.device, dtype=dtype)
         return latents.to(self.unet.device, torch.float32) * self.scheduler.init_noise_sigma
 
