@@ -396,19 +396,23 @@ int vd_res_ln_mod(const void* x, int64_t ldx, const void* y, int64_t ldy, const 
  *   q8/k8 fp8 rows [batch*s][ld8] (ld8 >= heads*64, % 16) with one E8M0 scale byte per
  *   (row, head) in qs/ks [batch*s][heads]; vt8 = V^T fp8 [batch*heads][64][skv] with the keys
  *   of every 64-key tile in the MFMA's k-slot order, vs = one E8M0 per (image, head, tile).
- * vd_attention_fp8: softmax(scale * Q K^T) V from those operands -> bf16 rows o (column h*64
- *   of head h).  sq % 32 == 0, skv % 64 == 0.
+ *   q_scale multiplies q before it is quantized (round 5): pass scale * log2(e) and call
+ *   vd_attention_fp8 with scale = 1 / log2(e) to fold the softmax scale into q8 (the kernel then
+ *   applies no per-score multiply and takes its exp2 argument straight from the MFMA); 1.0 keeps q.
+ * vd_attention_fp8: softmax(scale * Q K^T) V from those operands (Q the dequantized q8) ->
+ *   bf16 rows o (column h*64 of head h).  sq % 32 == 0, skv % 64 == 0.
  * vd_attention_fp8_quant_rope: vd_attention_fp8_quant for the DiT's spatial blocks with
  *   vd_rope_qk mode 0 (s = Hp*Wp tokens per image) applied to q and k in fp32 inside the
  *   quantization pass (q/k are read un-rotated and left unchanged). */
 int vd_attention_fp8_quant(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                            int64_t ldv, int64_t batch, int32_t heads, int64_t sq, int64_t skv,
                            int32_t d, void* q8, void* k8, int64_t ld8, void* vt8, void* qs, void* ks,
-                           void* vs, vd_stream_t stream);
+                           void* vs, float q_scale, vd_stream_t stream);
 int vd_attention_fp8_quant_rope(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                                 int64_t ldv, int64_t batch, int32_t heads, int64_t s, int32_t d,
                                 int64_t Hp, int64_t Wp, float theta, void* q8, void* k8, int64_t ld8,
-                                void* vt8, void* qs, void* ks, void* vs, vd_stream_t stream);
+                                void* vt8, void* qs, void* ks, void* vs, float q_scale,
+                                vd_stream_t stream);
 int vd_attention_fp8(const void* q8, const void* k8, int64_t ld8, const void* qs, const void* ks,
                      const void* vt8, const void* vs, void* o, int64_t ldo, int64_t batch,
                      int32_t heads, int64_t sq, int64_t skv, int32_t d, float scale,

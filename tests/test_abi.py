@@ -101,15 +101,15 @@ def test_dit_entry_points_validate_before_launch():
     p = ctypes.addressof(buf)
     # d = 80 is not an fp8 kernel variant; skv must be a multiple of 64
     assert h.vd_attention_fp8(p, p, 64, p, p, p, p, p, 64, 1, 1, 64, 64, 80, 0.1, None) == 1000
-    assert h.vd_attention_fp8_quant(p, 64, p, 64, p, 64, 1, 1, 64, 70, 64, p, p, 64, p, p, p, p, None) == 1000
+    assert h.vd_attention_fp8_quant(p, 64, p, 64, p, 64, 1, 1, 64, 70, 64, p, p, 64, p, p, p, p, 1.0, None) == 1000
     # fused temporal RoPE: 17..32 frames and d = 64 only
     assert h.vd_temporal_attention_rope(p, p, p, 192, p, 192, 1, 16, 4, 3, 64, 0.125, 10000.0, None) == 1000
     assert h.vd_temporal_attention_rope(p, p, p, 120, p, 120, 1, 32, 4, 3, 40, 0.125, 10000.0, None) == 1000
     # fused RoPE quantization: s must equal Hp*Wp; null operands
     assert h.vd_attention_fp8_quant_rope(p, 64, p, 64, p, 64, 1, 1, 64, 64, 8, 9, 10000.0, p, p, 64, p, p, p, p,
-                                         None) == 1000
+                                         1.0, None) == 1000
     assert h.vd_attention_fp8_quant_rope(None, 64, None, 64, None, 64, 1, 1, 64, 64, 8, 8, 10000.0, None, None,
-                                         64, None, None, None, None, None) == 1000
+                                         64, None, None, None, None, 1.0, None) == 1000
 
 
 def test_dit_ops_refuse_cpu_tensors():

@@ -261,13 +261,15 @@ def test_attention_fp8_quant_rope_fused(cuda):
     assert err_f < 0.10 and err_f <= 1.1 * err_u + 0.005, (err_f, err_u)
 
 
-def _fp8_emulated_attention(qkv, B, heads, S, d, lazy=True):
+def _fp8_emulated_attention(qkv, B, heads, S, d, lazy=True, folded=True):
     """fp32 torch restatement of vd_attention_fp8's arithmetic: Q/K rounded to e4m3 with
     per-(token, head) power-of-two scales, V per (image, head, 64-key tile); per 64-key tile,
-    P = exp2(s - m) rounded to e4m3 (unit scale) against the running offset m, O and the fp32
-    row sum of the unrounded P rescaled when m moves.  lazy: m moves only when some row of a
-    32-query group (one wave) has a tile max above its m + 8 (the default kernel); else every
-    row whose tile max passes m (round 1's kernel)."""
+    P = exp2(s - m) rounded to e4m3 (unit scale) against the running offset m, O and the row sum
+    of the ROUNDED P (round 5: the fifth MFMA, ones against P^T) rescaled when m moves.  lazy: m
+    moves only when some row of a 32-query group (one wave) has a tile max above its m + 8 (the
+    default kernel); else every row whose tile max passes m (round 1's kernel).  folded
+    (ops.attention_fp8, round 5): q is multiplied by d^-1/2 log2 e BEFORE its e4m3 rounding and the
+    scores are used as they come; else the scores of the rounded q are scaled."""
     f8 = torch.float8_e4m3fn
     D = heads * d
     x = qkv.float().reshape(B, S, 3, heads, d).permute(2, 0, 3, 1, 4)  # qkv b h s d
@@ -278,10 +280,11 @@ def _fp8_emulated_attention(qkv, B, heads, S, d, lazy=True):
         sc = torch.exp2(e)
         return (t / sc).clamp(-448, 448).to(f8).float() * sc
 
-    q, k = q8(x[0], (-1,)), q8(x[1], (-1,))
+    c = d ** -0.5 * 1.4426950408889634
+    q, k = q8(x[0] * (c if folded else 1.0), (-1,)), q8(x[1], (-1,))
     v = x[2].reshape(B, heads, S // 64, 64, d)
     v = q8(v, (-2, -1)).reshape(B, heads, S, d)
-    s = (q @ k.transpose(-1, -2)) * (d ** -0.5 * 1.4426950408889634)
+    s = (q @ k.transpose(-1, -2)) * (1.0 if folded else c)
     m = torch.full((B, heads, S, 1), -math.inf)
     o = torch.zeros(B, heads, S, d)
     lsum = torch.zeros(B, heads, S, 1)
@@ -296,8 +299,8 @@ def _fp8_emulated_attention(qkv, B, heads, S, d, lazy=True):
         mn = torch.where(up, torch.maximum(m, mt), m)
         alpha = torch.where(up, torch.exp2(m - mn), torch.ones_like(m))
         m = mn
-        p = torch.exp2(st - m)
-        o = o * alpha + p.to(f8).float() @ v[..., 64 * t:64 * t + 64, :]
+        p = torch.exp2(st - m).to(f8).float()
+        o = o * alpha + p @ v[..., 64 * t:64 * t + 64, :]
         lsum = lsum * alpha + p.sum(-1, keepdim=True)
     return (o / lsum).permute(0, 2, 1, 3).reshape(B * S, D)
 
@@ -325,6 +328,25 @@ def test_attention_fp8_matches_fp32(cuda, S):
     assert torch.isfinite(got).all()
     assert err_emu < 0.01, err_emu
     assert err < 0.10, err
+
+
+def test_attention_fp8_unfolded_scale(cuda):
+    """The kernel's other form: q quantized as it is (q_scale 1) and the softmax scale applied to
+    every score in the kernel (vd_attention_fp8 with scale = d^-1/2) — against the emulation of
+    that rounding, and close to the folded form ops.attention_fp8 uses."""
+    g = torch.Generator().manual_seed(5)
+    B, heads, S, d = 2, 3, 256, 64
+    D = heads * d
+    qkv = (torch.randn(B * S, 3 * D, generator=g) * 1.5).to(torch.bfloat16)
+    c = qkv.cuda()
+    ws = ops.attention_fp8_quant(c[:, :D], c[:, D:2 * D], c[:, 2 * D:], B, heads, S, S, d)
+    out = torch.empty(B * S, D, device=cuda, dtype=torch.bfloat16)
+    got = ops.attention_fp8_run(ws, out).float().cpu()
+    folded = ops.attention_fp8(c[:, :D], c[:, D:2 * D], c[:, 2 * D:], B, heads, S, S, d).float().cpu()
+    emu = _fp8_emulated_attention(qkv, B, heads, S, d, folded=False)
+    err_emu, err_f = rel_l2(got, emu), rel_l2(got, folded)
+    print(f"unfolded fp8 vs its emulation {err_emu:.4f}, vs the folded form {err_f:.4f}")
+    assert err_emu < 0.01 and err_f < 0.1, (err_emu, err_f)
 
 
 def test_tiny_dit_fp8_attention_matches_oracle(cuda, gold):

@@ -24,14 +24,16 @@ D = heads * d
 qkv = torch.randn(n * S, 3 * D, device="cuda").to(torch.bfloat16)
 q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
 o = torch.empty(n * S, D, device="cuda", dtype=torch.bfloat16)
-ws = ops.attention_fp8_quant(q, k, v, n, heads, S, S, d)
-st = torch.cuda.current_stream().cuda_stream
+ws = ops.attention_fp8_quant(q, k, v, n, heads, S, S, d, q_scale=d ** -0.5 * ops.LOG2E)  # ops.attention_fp8's fold
+ws1 = ops.attention_fp8_quant(q, k, v, n, heads, S, S, d)                                # unfolded operands
 
 
 def fp8():
-    lib().vd_attention_fp8(ws["q8"].data_ptr(), ws["k8"].data_ptr(), ws["ld8"], ws["qs"].data_ptr(), ws["ks"].data_ptr(),
-                           ws["vt8"].data_ptr(), ws["vs"].data_ptr(), o.data_ptr(), o.stride(0), n, heads, S, S, d,
-                           d ** -0.5, st)
+    ops.attention_fp8_run(ws, o)
+
+
+def fp8_unfolded():  # the kernel's per-score-multiply form (scale not folded into q8)
+    ops.attention_fp8_run(ws1, o)
 
 
 def bf16():
@@ -41,7 +43,8 @@ def bf16():
 flop = 4.0 * n * heads * S * S * d
 
 
-for name, fn in (("warm-up", fp8), ("fp8", fp8), ("bf16", bf16), ("fp8", fp8), ("bf16", bf16)):  # the first case pays the clock ramp
+for name, fn in (("warm-up", fp8), ("fp8", fp8), ("fp8 unfolded", fp8_unfolded), ("bf16", bf16), ("fp8", fp8),
+                 ("fp8 unfolded", fp8_unfolded), ("bf16", bf16)):  # the first case pays the clock ramp
     fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()

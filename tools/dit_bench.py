@@ -112,12 +112,8 @@ def main():
     torch.cuda.synchronize()
     at = ev[0].elapsed_time(ev[1]) / 5
     # the fp8 kernel on the same data: operand quantization and the attention launch apart
-    ws = ops.attention_fp8_quant(q, k, v, 2 * F, cfg["num_heads"], S, S, d)
-    from vdiff._lib import lib
-    fp8_call = lambda: lib().vd_attention_fp8(ws["q8"].data_ptr(), ws["k8"].data_ptr(), ws["ld8"], ws["qs"].data_ptr(),  # noqa: E731
-                                              ws["ks"].data_ptr(), ws["vt8"].data_ptr(), ws["vs"].data_ptr(),
-                                              o.data_ptr(), o.stride(0), 2 * F, cfg["num_heads"], S, S, d, d ** -0.5,
-                                              torch.cuda.current_stream().cuda_stream)
+    ws = ops.attention_fp8_quant(q, k, v, 2 * F, cfg["num_heads"], S, S, d, q_scale=d ** -0.5 * ops.LOG2E)
+    fp8_call = lambda: ops.attention_fp8_run(ws, o)  # noqa: E731  (the folded form, as ops.attention_fp8)
     fp8_call()
     ev[0].record()
     for _ in range(5):
@@ -127,7 +123,7 @@ def main():
     at8 = ev[0].elapsed_time(ev[1]) / 5
     ev[0].record()
     for _ in range(5):
-        ops.attention_fp8_quant(q, k, v, 2 * F, cfg["num_heads"], S, S, d)
+        ops.attention_fp8_quant(q, k, v, 2 * F, cfg["num_heads"], S, S, d, q_scale=d ** -0.5 * ops.LOG2E)
     ev[1].record()
     torch.cuda.synchronize()
     qt8 = ev[0].elapsed_time(ev[1]) / 5

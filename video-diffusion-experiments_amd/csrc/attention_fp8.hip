@@ -61,7 +61,7 @@ __device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d
 
 // Q or K rows: one thread per (row, head): 64 bf16 -> 64 fp8 + one E8M0 byte.
 __global__ void quant_rows_kernel(const bf16_t* __restrict__ x, int64_t ldx, int64_t rows, int heads,
-                                  uint8_t* __restrict__ x8, int64_t ld8, uint8_t* __restrict__ sc) {
+                                  uint8_t* __restrict__ x8, int64_t ld8, uint8_t* __restrict__ sc, float mul) {
   const int64_t total = rows * heads;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
     const int64_t r = i / heads;
@@ -73,7 +73,10 @@ __global__ void quant_rows_kernel(const bf16_t* __restrict__ x, int64_t ldx, int
     for (int c = 0; c < FD / 8; ++c) {
       unpack8(*(const uint4*)(src + 8 * c), v + 8 * c);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[8 * c + j]));
+      for (int j = 0; j < 8; ++j) {
+        v[8 * c + j] *= mul;
+        amax = fmaxf(amax, fabsf(v[8 * c + j]));
+      }
     }
     const int e = e8m0_for(amax);
     const float inv = e8m0_inv(e);
@@ -101,7 +104,7 @@ __global__ void quant_rows_kernel(const bf16_t* __restrict__ x, int64_t ldx, int
 __global__ __launch_bounds__(NT) void quant_rows_rope_kernel(const bf16_t* __restrict__ x, int64_t ldx,
                                                              int64_t rows, int heads, uint8_t* __restrict__ x8,
                                                              int64_t ld8, uint8_t* __restrict__ sc, int64_t Hp,
-                                                             int64_t Wp, float log2_theta) {
+                                                             int64_t Wp, float log2_theta, float mul) {
   // 32-bit index math (the host checks rows * heads * 8 < 2^31): 64-bit divisions by heads,
   // Wp and Hp would dominate this HBM pass.  total is a multiple of 8, so a lane group never
   // straddles the grid stride.
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(NT) void quant_rows_rope_kernel(const bf16_t* __res
       const float inv_freq = exp2f(-log2_theta * (float)(2 * (j0 + j)) * (1.0f / (FD / 2)));
       float sn, cs;
       __sincosf(pos * inv_freq, &sn, &cs);
-      v[j] = lo ? own[j] * cs - par[j] * sn : own[j] * cs + par[j] * sn;
+      v[j] = (lo ? own[j] * cs - par[j] * sn : own[j] * cs + par[j] * sn) * mul;
       amax = fmaxf(amax, fabsf(v[j]));
     }
     amax = fmaxf(amax, __shfl_xor(amax, 1, 8));
@@ -377,6 +380,15 @@ __device__ __forceinline__ void f8_wait(int n) {  // s_waitcnt vmcnt(n), n in {0
 // physical 16-byte chunk of logical chunk c in a 64-byte row r of a K / V^T tile image
 __device__ __forceinline__ uint32_t f8_chunk(uint32_t r, uint32_t c) { return c ^ ((r >> 2) & 3); }
 
+// FOLDED (round 5): the softmax scale x log2 e is folded into q8 by the quantization
+// (vd_attention_fp8_quant's q_scale) and the running offset into the S MFMA's accumulator input
+// (C = -m), so the MFMA emits the exp2 argument itself: no scale FMA per score.  The row sum is a
+// fifth MFMA, an all-ones e4m3 A operand against P^T (the sum of the rounded P the numerator uses),
+// instead of 32 VALU adds; the V scales of all tiles are read once (a per-tile global load made
+// hipcc drain the whole LDS-DMA ring with vmcnt(0) before every PV MFMA); the fp8 packs write
+// over the previous tile's registers (no zeroing moves).  The tile is VALU-issue bound (32 exp,
+// 16 packs, the max pass against 5 MFMAs), so every VALU instruction removed is time.
+template <bool FOLDED>
 __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
     const uint8_t* __restrict__ q8, const uint8_t* __restrict__ k8, int64_t ld8,
     const uint8_t* __restrict__ qs, const uint8_t* __restrict__ ks, const uint8_t* __restrict__ vt8,
@@ -398,6 +410,14 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
   const int64_t qrow = b * sq + (qvalid ? q0 + r : 0);
   const int ntiles = (int)(skv / KT8);
 
+  // Q^T fragment (d = 32 hh + j of this lane's query), its scale, and the V scales of the first
+  // 64 tiles — all landed before the first ring DMA goes out (a plain load waited for later
+  // would drain the ring: vmcnt counts the DMAs too)
+  const i32x8 qf = *(const i32x8*)(q8 + qrow * ld8 + h * FD + 32 * hh);
+  const int qsc = qs[qrow * heads + h];
+  int vsr = lane < ntiles ? vs[bh * ntiles + lane] : 127;
+  asm volatile("" ::"v"(qf[0]), "v"(qf[7]), "v"(qsc), "v"(vsr));
+
   // ---- ring: wave w moves K rows and V^T rows 16w .. 16w + 15 of each tile, wave 0 the scales
   const u32x4f rk = f8_rsrc(k8 + b * skv * ld8 + h * FD, (uint32_t)((skv - 1) * ld8 + FD));
   const u32x4f rv = f8_rsrc(vt8 + bh * FD * skv, (uint32_t)(FD * skv));
@@ -415,9 +435,6 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
   };
   for (int t = 0; t < F8S - 1 && t < ntiles; ++t) issue(t);
 
-  // Q^T fragment: d = 32 hh + j of this lane's query, and its scale
-  const i32x8 qf = *(const i32x8*)(q8 + qrow * ld8 + h * FD + 32 * hh);
-  const int qsc = qs[qrow * heads + h];
   // per-lane LDS read offsets: K row 32 kb + r and V^T row 32 a + r, logical chunks 2 hh, 2 hh + 1
   uint32_t kro[2][2], vro[2][2];
 #pragma unroll
@@ -428,11 +445,14 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
       kro[x][j] = F8_K + row * 64 + 16u * f8_chunk(row, (uint32_t)(2 * hh + j));
       vro[x][j] = F8_V + row * 64 + 16u * f8_chunk(row, (uint32_t)(2 * hh + j));
     }
+  const i32x8 ones = {0x38383838, 0x38383838, 0x38383838, 0x38383838,   // e4m3 1.0 in every k-slot
+                      0x38383838, 0x38383838, 0x38383838, 0x38383838};
 
-  f32x16 ot[2];
+  f32x16 ot[2], ls, nm;  // O^T, the row sums (every register of a lane holds its query's sum), -m
 #pragma unroll
-  for (int i = 0; i < 16; ++i) { ot[0][i] = 0.f; ot[1][i] = 0.f; }
-  float m = -INFINITY, lsum = 0.f;
+  for (int i = 0; i < 16; ++i) { ot[0][i] = 0.f; ot[1][i] = 0.f; ls[i] = 0.f; nm[i] = 0.f; }
+  float m = FOLDED ? 0.f : -INFINITY;
+  uint32_t pw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int t = 0; t < ntiles; ++t) {
     const int ahead = (ntiles - 1 - t) < (F8S - 2) ? (ntiles - 1 - t) : (F8S - 2);
     f8_wait(ahead * npc);                               // this wave's pieces of tile t landed
@@ -447,10 +467,14 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
       const uint4 k0 = *(const uint4*)(st + kro[kb][0]), k1 = *(const uint4*)(st + kro[kb][1]);
       const i32x8 kf = {(int)k0.x, (int)k0.y, (int)k0.z, (int)k0.w, (int)k1.x, (int)k1.y, (int)k1.z, (int)k1.w};
       const int ksc = st[F8_KS + 4 * (32 * kb + r)];  // sub-dword LDS-DMA writes one dword per lane
-      f32x16 z;
+      if constexpr (FOLDED) {
+        s[kb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, nm, 0, 0, 0, ksc, 0, qsc);  // = s' - m
+      } else {
+        f32x16 z;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) z[i] = 0.f;
-      s[kb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, z, 0, 0, 0, ksc, 0, qsc);
+        for (int i = 0; i < 16; ++i) z[i] = 0.f;
+        s[kb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, z, 0, 0, 0, ksc, 0, qsc);
+      }
     }
     i32x8 vf[2];
 #pragma unroll
@@ -458,42 +482,46 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
       const uint4 v0 = *(const uint4*)(st + vro[a][0]), v1 = *(const uint4*)(st + vro[a][1]);
       vf[a] = i32x8{(int)v0.x, (int)v0.y, (int)v0.z, (int)v0.w, (int)v1.x, (int)v1.y, (int)v1.z, (int)v1.w};
     }
-    const int vsc = vs[bh * ntiles + t];
-    // ---- softmax against the lazily moved offset m (P <= 2^8)
+    if (t > 0 && (t & 63) == 0) vsr = t + lane < ntiles ? vs[bh * ntiles + t + lane] : 127;
+    const int vsc = __builtin_amdgcn_readlane(vsr, t & 63);
+    // ---- softmax against the lazily moved offset m (P <= 2^8); always moved on the first tile
     float mt = s[0][0];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kb][i]);
-    mt = fmaxf(mt, partner32f(mt)) * c;
-    if (__any(mt > m + 8.f)) {  // lazy, wave-uniform; always on the first tile (m = -inf)
-      const float mn = fmaxf(m, mt);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      m = mn;
-      lsum *= alpha;
+    mt = fmaxf(mt, partner32f(mt));
+    const float mab = FOLDED ? mt + m : mt * c;  // the tile's row max, log2 units
+    if (t == 0 || __any(mab > m + 8.f)) {         // wave-uniform
+      const float mn = t == 0 ? mab : fmaxf(m, mab);
+      const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(m - mn);
+      if constexpr (FOLDED) {
+        const float dl = mn - m;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { ot[0][i] *= alpha; ot[1][i] *= alpha; }
+        for (int i = 0; i < 16; ++i) { s[0][i] -= dl; s[1][i] -= dl; nm[i] = -mn; }
+      }
+      m = mn;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { ot[0][i] *= alpha; ot[1][i] *= alpha; ls[i] *= alpha; }
     }
-    uint32_t pw[8];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const float p0 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 0], c, -m));
-        const float p1 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 1], c, -m));
-        const float p2 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 2], c, -m));
-        const float p3 = __builtin_amdgcn_exp2f(fmaf(s[kb][4 * g + 3], c, -m));
-        lsum += (p0 + p1) + (p2 + p3);
-        int w = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, 0, false);
-        pw[4 * kb + g] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(p2, p3, w, true);
+        float p[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          p[e] = __builtin_amdgcn_exp2f(FOLDED ? s[kb][4 * g + e] : fmaf(s[kb][4 * g + e], c, -m));
+        const int w = __builtin_amdgcn_cvt_pk_fp8_f32(p[0], p[1], (int)pw[4 * kb + g], false);
+        pw[4 * kb + g] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(p[2], p[3], w, true);
       }
     const i32x8 pf = {(int)pw[0], (int)pw[1], (int)pw[2], (int)pw[3], (int)pw[4], (int)pw[5], (int)pw[6], (int)pw[7]};
 #pragma unroll
     for (int a = 0; a < 2; ++a)
       ot[a] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf[a], pf, ot[a], 0, 0, 0, vsc, 0, 127);
+    ls = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones, pf, ls, 0, 0, 0, 127, 0, 127);
   }
-  // the lane's fp32 partial over its 32 unrounded scores plus its partner's
-  const float inv = 1.0f / (lsum + partner32f(lsum));
+  const float inv = 1.0f / ls[0];
   if (qvalid) {
     bf16_t* orow = o + (b * sq + q0 + r) * ldo + h * FD;
 #pragma unroll
@@ -512,11 +540,11 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 int quant_operands(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                    int64_t batch, int32_t heads, int64_t sq, int64_t skv, int32_t d, bool rope, int64_t Hp,
                    int64_t Wp, float theta, void* q8, void* k8, int64_t ld8, void* vt8, void* qs, void* ks,
-                   void* vs, vd_stream_t stream) {
+                   void* vs, float q_scale, vd_stream_t stream) {
   VD_CHECK_ARG(d == FD && heads > 0 && batch > 0 && sq > 0 && skv > 0 && skv % KT8 == 0);
   VD_CHECK_ARG(q && k && v && q8 && k8 && vt8 && qs && ks && vs && al16(q) && al16(k) && al16(v));
   VD_CHECK_ARG(al16(q8) && al16(k8) && al16(vt8) && ld8 % 16 == 0 && ld8 >= (int64_t)heads * FD);
-  VD_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0);
+  VD_CHECK_ARG(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && q_scale > 0.f);
   if (rope) {
     VD_CHECK_ARG(Hp > 0 && Wp > 0 && sq == Hp * Wp && skv == sq && theta > 1.f);
     VD_CHECK_ARG(batch * sq * heads * 8 < 0x7fffffff);
@@ -526,14 +554,16 @@ int quant_operands(const void* q, int64_t ldq, const void* k, int64_t ldk, const
   if (rope) {
     const float l2t = log2f(theta);
     hipLaunchKernelGGL(quant_rows_rope_kernel, dim3(grid(batch * sq * heads * 8)), dim3(NT), 0, s,
-                       (const bf16_t*)q, ldq, batch * sq, (int)heads, (uint8_t*)q8, ld8, (uint8_t*)qs, Hp, Wp, l2t);
+                       (const bf16_t*)q, ldq, batch * sq, (int)heads, (uint8_t*)q8, ld8, (uint8_t*)qs, Hp, Wp, l2t,
+                       q_scale);
     hipLaunchKernelGGL(quant_rows_rope_kernel, dim3(grid(batch * skv * heads * 8)), dim3(NT), 0, s,
-                       (const bf16_t*)k, ldk, batch * skv, (int)heads, (uint8_t*)k8, ld8, (uint8_t*)ks, Hp, Wp, l2t);
+                       (const bf16_t*)k, ldk, batch * skv, (int)heads, (uint8_t*)k8, ld8, (uint8_t*)ks, Hp, Wp, l2t,
+                       1.0f);
   } else {
     hipLaunchKernelGGL(quant_rows_kernel, dim3(grid(batch * sq * heads)), dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                       batch * sq, (int)heads, (uint8_t*)q8, ld8, (uint8_t*)qs);
+                       batch * sq, (int)heads, (uint8_t*)q8, ld8, (uint8_t*)qs, q_scale);
     hipLaunchKernelGGL(quant_rows_kernel, dim3(grid(batch * skv * heads)), dim3(NT), 0, s, (const bf16_t*)k, ldk,
-                       batch * skv, (int)heads, (uint8_t*)k8, ld8, (uint8_t*)ks);
+                       batch * skv, (int)heads, (uint8_t*)k8, ld8, (uint8_t*)ks, 1.0f);
   }
   const int64_t nblk = batch * heads * (skv / KT8);
   VD_CHECK_ARG(nblk < 0x7fffffff);
@@ -547,18 +577,18 @@ int quant_operands(const void* q, int64_t ldq, const void* k, int64_t ldk, const
 extern "C" int vd_attention_fp8_quant(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                                       int64_t ldv, int64_t batch, int32_t heads, int64_t sq, int64_t skv,
                                       int32_t d, void* q8, void* k8, int64_t ld8, void* vt8, void* qs,
-                                      void* ks, void* vs, vd_stream_t stream) {
+                                      void* ks, void* vs, float q_scale, vd_stream_t stream) {
   return quant_operands(q, ldq, k, ldk, v, ldv, batch, heads, sq, skv, d, false, 0, 0, 0.f, q8, k8, ld8, vt8,
-                        qs, ks, vs, stream);
+                        qs, ks, vs, q_scale, stream);
 }
 
 extern "C" int vd_attention_fp8_quant_rope(const void* q, int64_t ldq, const void* k, int64_t ldk,
                                            const void* v, int64_t ldv, int64_t batch, int32_t heads,
                                            int64_t s, int32_t d, int64_t Hp, int64_t Wp, float theta, void* q8,
                                            void* k8, int64_t ld8, void* vt8, void* qs, void* ks, void* vs,
-                                           vd_stream_t stream) {
+                                           float q_scale, vd_stream_t stream) {
   return quant_operands(q, ldq, k, ldk, v, ldv, batch, heads, s, s, d, true, Hp, Wp, theta, q8, k8, ld8, vt8, qs,
-                        ks, vs, stream);
+                        ks, vs, q_scale, stream);
 }
 
 extern "C" int vd_attention_fp8(const void* q8, const void* k8, int64_t ld8, const void* qs, const void* ks,
@@ -571,9 +601,14 @@ extern "C" int vd_attention_fp8(const void* q8, const void* k8, int64_t ld8, con
   const int64_t nblk = (sq + 127) / 128 * heads * batch;
   VD_CHECK_ARG(nblk < 0x7fffffff);
   const float c = scale * 1.4426950408889634f;
+  const bool folded = fabsf(c - 1.0f) < 1e-6f;  // vd_attention_fp8_quant folded scale x log2 e into q8
   const bool v2ok = skv * ld8 < 0x7fffffff && skv * FD < 0x7fffffff && skv * heads < 0x7fffffff;
-  if (v2ok)
-    hipLaunchKernelGGL(flash_fp8_v2_kernel, dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream,
+  if (v2ok && folded)
+    hipLaunchKernelGGL(flash_fp8_v2_kernel<true>, dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream,
+                       (const uint8_t*)q8, (const uint8_t*)k8, ld8, (const uint8_t*)qs, (const uint8_t*)ks,
+                       (const uint8_t*)vt8, (const uint8_t*)vs, (bf16_t*)o, ldo, (int)heads, sq, skv, 1.0f);
+  else if (v2ok)
+    hipLaunchKernelGGL(flash_fp8_v2_kernel<false>, dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream,
                        (const uint8_t*)q8, (const uint8_t*)k8, ld8, (const uint8_t*)qs, (const uint8_t*)ks,
                        (const uint8_t*)vt8, (const uint8_t*)vs, (bf16_t*)o, ldo, (int)heads, sq, skv, c);
   else

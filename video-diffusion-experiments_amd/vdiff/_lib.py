@@ -61,8 +61,8 @@ SIGNATURES = {
     "vd_patchify": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp, c_i64, c_vp], c_i32),
     "vd_unpatchify": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp], c_i32),
     "vd_rope_qk": ([c_vp, c_i64, c_i64, c_i32, c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_vp], c_i32),
-    "vd_attention_fp8_quant": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
-    "vd_attention_fp8_quant_rope": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i64, c_i64, c_f32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp], c_i32),
+    "vd_attention_fp8_quant": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp], c_i32),
+    "vd_attention_fp8_quant_rope": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i64, c_i64, c_f32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp], c_i32),
     "vd_attention_fp8": ([c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i64, c_i64, c_i32, c_f32, c_vp], c_i32),
     "vd_rows_eltwise": ([c_i32, c_vp, c_i64, c_vp, c_i64, c_i32, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
     "vd_upsample_nearest2x": ([c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),

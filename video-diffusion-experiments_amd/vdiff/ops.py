@@ -555,10 +555,12 @@ def res_ln_mod(x, *, y=None, gate=None, shift=None, scale=None, rows_per_b=None,
     return out
 
 
-def attention_fp8_quant(q, k, v, batch, heads, sq, skv, d=64, rope=None):
+def attention_fp8_quant(q, k, v, batch, heads, sq, skv, d=64, rope=None, q_scale=1.0):
     """bf16 q/k/v row views -> the fp8 operands of vd_attention_fp8 (a dict of buffers).
     rope=(Hp, Wp, theta): apply the spatial 2-D RoPE (rope_qk mode 0) to q and k inside the
-    quantization pass (vd_attention_fp8_quant_rope); q and k are read un-rotated."""
+    quantization pass (vd_attention_fp8_quant_rope); q and k are read un-rotated.
+    q_scale: q is multiplied by it before quantization (attention_fp8 folds the softmax scale x
+    log2 e there); ws["q_scale"] records it."""
     _dev(q, k, v)
     dev = q.device
     ld8 = (heads * d + 15) // 16 * 16
@@ -569,31 +571,45 @@ def attention_fp8_quant(q, k, v, batch, heads, sq, skv, d=64, rope=None):
           "qs": torch.empty(batch * sq, heads, device=dev, dtype=u8),
           "ks": torch.empty(batch * skv, heads, device=dev, dtype=u8),
           "vs": torch.empty(batch * heads, max(1, skv // 64), device=dev, dtype=u8),
-          "ld8": ld8, "batch": batch, "heads": heads, "sq": sq, "skv": skv, "d": d}
+          "ld8": ld8, "batch": batch, "heads": heads, "sq": sq, "skv": skv, "d": d, "q_scale": float(q_scale)}
     if rope is not None:
         if sq != skv:
             raise ValueError("fused RoPE quantization needs sq == skv (self-attention)")
         Hp, Wp, theta = rope
         check(lib().vd_attention_fp8_quant_rope(
             _p(q), q.stride(0), _p(k), k.stride(0), _p(v), v.stride(0), batch, heads, sq, d, Hp, Wp, theta,
-            _p(ws["q8"]), _p(ws["k8"]), ld8, _p(ws["vt8"]), _p(ws["qs"]), _p(ws["ks"]), _p(ws["vs"]), _stream()),
-            "vd_attention_fp8_quant_rope")
+            _p(ws["q8"]), _p(ws["k8"]), ld8, _p(ws["vt8"]), _p(ws["qs"]), _p(ws["ks"]), _p(ws["vs"]), float(q_scale),
+            _stream()), "vd_attention_fp8_quant_rope")
         return ws
     check(lib().vd_attention_fp8_quant(_p(q), q.stride(0), _p(k), k.stride(0), _p(v), v.stride(0), batch, heads,
                                        sq, skv, d, _p(ws["q8"]), _p(ws["k8"]), ld8, _p(ws["vt8"]), _p(ws["qs"]),
-                                       _p(ws["ks"]), _p(ws["vs"]), _stream()), "vd_attention_fp8_quant")
+                                       _p(ws["ks"]), _p(ws["vs"]), float(q_scale), _stream()), "vd_attention_fp8_quant")
     return ws
+
+
+LOG2E = 1.4426950408889634
+
+
+def attention_fp8_run(ws, out, scale=None):
+    """vd_attention_fp8 on operands from attention_fp8_quant.  `scale` multiplies the scores of
+    the dequantized q8 (default d^-1/2 / ws["q_scale"]: the softmax scale q_scale did not fold;
+    1 / log2 e after attention_fp8's full fold selects the kernel's folded form)."""
+    d = ws["d"]
+    if scale is None:
+        scale = d ** -0.5 / ws["q_scale"]
+    check(lib().vd_attention_fp8(_p(ws["q8"]), _p(ws["k8"]), ws["ld8"], _p(ws["qs"]), _p(ws["ks"]), _p(ws["vt8"]),
+                                 _p(ws["vs"]), _p(out), out.stride(0), ws["batch"], ws["heads"], ws["sq"], ws["skv"],
+                                 d, scale, _stream()), "vd_attention_fp8")
+    return out
 
 
 def attention_fp8(q, k, v, batch, heads, sq, skv, d=64, scale=None, out=None, rope=None):
     """fp8 (e4m3, block-scaled MFMA) self-attention, d = 64: quantize (optionally with the
-    spatial RoPE fused, see attention_fp8_quant), then attend."""
-    ws = attention_fp8_quant(q, k, v, batch, heads, sq, skv, d, rope=rope)
+    spatial RoPE fused, see attention_fp8_quant) with the softmax scale x log2 e folded into q,
+    then attend (the kernel's folded form: no per-score multiply)."""
+    scale = d ** -0.5 if scale is None else scale
+    ws = attention_fp8_quant(q, k, v, batch, heads, sq, skv, d, rope=rope, q_scale=scale * LOG2E)
     if out is None:
         out = torch.empty(batch * sq, heads * d, device=q.device, dtype=BF16)
     _dev(out)
-    scale = d ** -0.5 if scale is None else scale
-    check(lib().vd_attention_fp8(_p(ws["q8"]), _p(ws["k8"]), ws["ld8"], _p(ws["qs"]), _p(ws["ks"]), _p(ws["vt8"]),
-                                 _p(ws["vs"]), _p(out), out.stride(0), batch, heads, sq, skv, d, scale, _stream()),
-          "vd_attention_fp8")
-    return out
+    return attention_fp8_run(ws, out, scale=1.0 / LOG2E)
