@@ -127,9 +127,25 @@ typedef struct vd_gemm_desc {
    * (vdiff.dist.FrameShard.return_perm) — no separate re-shard transpose.  Not with ln_out, GEGLU
    * or a row bias. */
   int32_t rmap_n1, rmap_n2, rmap_inner;
+  /* LayerNorm folded into the consuming GEMM (round 5; NULL = none).  With ln_fold_s != NULL
+   * the A rows are the UN-normalised LayerNorm input x (K = its row length), w = W∘gamma (each
+   * column k of the Linear's W scaled by gamma[k], rounded to bf16 once), bias = b + W·beta
+   * (fp32), and ln_fold_s[n] = Σ_k w[n][k] in fp32 (of the bf16 w).  The kernel takes each row's
+   * mean and rstd = 1/sqrt(var + ln_fold_eps) from A itself (Σx and Σx² as two extra MFMAs per
+   * k-step over the A fragments it holds) and its epilogue forms
+   *   rstd·(Σ_k w[n][k] x[m][k] − mean·ln_fold_s[n]) + bias[n]   (then act / GEGLU as usual)
+   * = Linear(LayerNorm(x)) without the normalised rows being written or read.  Only the
+   * weight-stationary v8 path carries it (dense, K = 320, no residual / row bias / rmap):
+   * vd_gemm_plan reports kernel 0 and vd_gemm returns VD_EUNSUPPORTED for any other plan. */
+  const float* ln_fold_s; float ln_fold_eps;
 } vd_gemm_desc;
 
 int vd_gemm(const vd_gemm_desc* d, vd_stream_t stream);
+/* The plan vd_gemm would run for this descriptor (its path / plan_m controls included):
+ * *kernel = 1, 2, 3, 5, 6 or 8 (v1 .. v8; 0: no kernel takes it, vd_gemm would refuse it) and
+ * *split = its K slices.  Lets a caller choose between a folded and an unfolded form (ln_fold_s)
+ * and lets tools label their timings; no launch, no state. */
+int vd_gemm_plan(const vd_gemm_desc* d, int32_t* kernel, int32_t* split);
 /* Workspace bytes vd_gemm needs for this descriptor (0 = none): shapes with too
  * few output tiles to fill 256 CUs are split along K into fp32 slabs that a
  * second kernel reduces (deterministic, no atomics) while applying the epilogue. */

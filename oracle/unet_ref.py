@@ -92,18 +92,43 @@ def layer_norm(sd, p, x, eps=1e-5):
     return F.layer_norm(x, (x.shape[-1],), sd[p + ".weight"], sd[p + ".bias"], eps)
 
 
-def attention(sd, p, x, ctx, heads, rnd=_ident):
+def folded_linear(sd, norm_p, x, w, b=None, eps=1e-5):
+    """The device's folded LayerNorm -> Linear ("dev" mode; vdiff.models.layers.LnFold and
+    vd_gemm_desc.ln_fold_s): W' = bf16(W∘gamma), s = Σ_k W'[n][k], b' = W·beta + b and
+    rstd·(x·W'^T − mean·s) + b' over the UN-normalised rows x — the same function as
+    Linear(LayerNorm(x)) up to the rounding of W' (the normalised rows are never rounded)."""
+    g, be = sd[norm_p + ".weight"].double(), sd[norm_p + ".bias"].double()
+    wd = w.double()
+    wf = (wd * g[None, :]).to(torch.bfloat16).double()
+    bp = wd @ be + (b.double() if b is not None else 0.0)
+    xd = x.double()
+    mean = xd.mean(-1, keepdim=True)
+    rstd = (xd.var(-1, unbiased=False, keepdim=True) + eps).rsqrt()
+    return (rstd * (xd @ wf.T - mean * wf.sum(1)) + bp).float()
+
+
+def attention(sd, p, x, ctx, heads, rnd=_ident, fold_norm=None):
     """diffusers:Attention + AttnProcessor2_0 (App. A.5): q/k/v without bias,
-    softmax(q k^T / sqrt(d)) v, to_out.0 with bias, no residual inside."""
+    softmax(q k^T / sqrt(d)) v, to_out.0 with bias, no residual inside.  fold_norm ("dev" mode):
+    x is the un-normalised input of that LayerNorm, folded into q (and k / v of a
+    self-attention) as the device does (folded_linear)."""
     ctx = x if ctx is None else ctx
     dev = getattr(rnd, "device_attention", False)
     wq = sd[p + ".to_q.weight"]
     d = wq.shape[0] // heads
-    if dev:  # vdiff Attention.prepare: bf16(W_q * d^-1/2 * log2 e); scores in log2 units
-        wq = _bf16_round(wq * (d ** -0.5 * math.log2(math.e)))
-    q = rnd(F.linear(x, wq))
-    k = rnd(linear(sd, p + ".to_k", ctx, bias=False))
-    v = rnd(linear(sd, p + ".to_v", ctx, bias=False))
+    if fold_norm is not None:  # vdiff BasicTransformerBlock.prepare: LnFold of the scaled q rows
+        q = rnd(folded_linear(sd, fold_norm, x, wq.float() * (d ** -0.5 * math.log2(math.e))))
+        self_attn = ctx is x
+        k = rnd(folded_linear(sd, fold_norm, x, sd[p + ".to_k.weight"]) if self_attn
+                else linear(sd, p + ".to_k", ctx, bias=False))
+        v = rnd(folded_linear(sd, fold_norm, x, sd[p + ".to_v.weight"]) if self_attn
+                else linear(sd, p + ".to_v", ctx, bias=False))
+    else:
+        if dev:  # vdiff Attention.prepare: bf16(W_q * d^-1/2 * log2 e); scores in log2 units
+            wq = _bf16_round(wq * (d ** -0.5 * math.log2(math.e)))
+        q = rnd(F.linear(x, wq))
+        k = rnd(linear(sd, p + ".to_k", ctx, bias=False))
+        v = rnd(linear(sd, p + ".to_v", ctx, bias=False))
     b, s, c = q.shape
     q = q.view(b, s, heads, d).transpose(1, 2)
     k = k.view(b, -1, heads, d).transpose(1, 2)
@@ -124,27 +149,49 @@ def attention(sd, p, x, ctx, heads, rnd=_ident):
     return linear(sd, p + ".to_out.0", rnd(o))
 
 
-def feed_forward(sd, p, x, rnd=_ident):
-    """diffusers:FeedForward(activation_fn='geglu'): GEGLU(C->4C) -> Linear(4C->C) (App. A.5)."""
-    hg = linear(sd, p + ".net.0.proj", x)
+def feed_forward(sd, p, x, rnd=_ident, fold_norm=None):
+    """diffusers:FeedForward(activation_fn='geglu'): GEGLU(C->4C) -> Linear(4C->C) (App. A.5).
+    fold_norm: x un-normalised, that LayerNorm folded into the GEGLU projection (folded_linear)."""
+    if fold_norm is not None:
+        hg = folded_linear(sd, fold_norm, x, sd[p + ".net.0.proj.weight"], sd[p + ".net.0.proj.bias"])
+    else:
+        hg = linear(sd, p + ".net.0.proj", x)
     h, g = hg.chunk(2, dim=-1)
     a = rnd(h * F.gelu(g, approximate="none"))
     return linear(sd, p + ".net.2", a)
 
 
 def basic_transformer_block(sd, p, x, ehs, heads, pe=None, double_self=False, rnd=_ident):
-    """diffusers:BasicTransformerBlock, norm_type='layer_norm' (App. A.3 / A.4)."""
-    n = layer_norm(sd, p + ".norm1", x)
-    if pe is not None:
-        n = n + pe[:, : x.shape[1]]
-    x = rnd(attention(sd, p + ".attn1", rnd(n), None, heads, rnd) + x)
-    n = layer_norm(sd, p + ".norm2", x)
-    if pe is not None:
-        n = n + pe[:, : x.shape[1]]
+    """diffusers:BasicTransformerBlock, norm_type='layer_norm' (App. A.3 / A.4).  A "dev"-mode
+    rounder may carry ln_fold(i, C, rows, motion) -> bool, the device's choice of folding norm i
+    into its consuming GEMM (vdiff BasicTransformerBlock.fold); those norms then follow the
+    device's folded arithmetic (folded_linear)."""
+    fold = getattr(rnd, "ln_fold", None)
+    rows = x.shape[0] * x.shape[1]
+
+    def folds(i):
+        return fold is not None and fold(i, x.shape[-1], rows, pe is not None)
+
+    if folds(1):
+        x = rnd(attention(sd, p + ".attn1", x, None, heads, rnd, fold_norm=p + ".norm1") + x)
+    else:
+        n = layer_norm(sd, p + ".norm1", x)
+        if pe is not None:
+            n = n + pe[:, : x.shape[1]]
+        x = rnd(attention(sd, p + ".attn1", rnd(n), None, heads, rnd) + x)
     ctx = None if double_self else ehs
-    x = rnd(attention(sd, p + ".attn2", rnd(n), ctx, heads, rnd) + x)
-    n = layer_norm(sd, p + ".norm3", x)
-    x = rnd(feed_forward(sd, p + ".ff", rnd(n), rnd) + x)
+    if folds(2):
+        x = rnd(attention(sd, p + ".attn2", x, ctx, heads, rnd, fold_norm=p + ".norm2") + x)
+    else:
+        n = layer_norm(sd, p + ".norm2", x)
+        if pe is not None:
+            n = n + pe[:, : x.shape[1]]
+        x = rnd(attention(sd, p + ".attn2", rnd(n), ctx, heads, rnd) + x)
+    if folds(3):
+        x = rnd(feed_forward(sd, p + ".ff", x, rnd, fold_norm=p + ".norm3") + x)
+    else:
+        n = layer_norm(sd, p + ".norm3", x)
+        x = rnd(feed_forward(sd, p + ".ff", rnd(n), rnd) + x)
     return x
 
 

@@ -26,6 +26,29 @@ def nchw(act: Act):
     return act.t.float().cpu().reshape(act.n, act.h, act.w, -1).permute(0, 3, 1, 2)
 
 
+def device_rounder(unet):
+    """The oracle's "dev" rounder plus the device's LayerNorm-fold decisions (ln_fold hook of
+    unet_ref.basic_transformer_block): norm i of a block with C channels over `rows` rows folds
+    exactly when the device's block of that kind would fold it (BasicTransformerBlock.fold,
+    i.e. the library's own plan)."""
+    from vdiff.models.blocks import BasicTransformerBlock
+    blocks = {}
+    for m in unet.modules():
+        if isinstance(m, BasicTransformerBlock):
+            blocks.setdefault((m.norm1.normalized_shape[0], m.pos_embed is not None), m)
+
+    def dev(x):
+        return unet_ref.ROUNDERS["dev"](x)
+
+    def ln_fold(i, C, rows, motion):
+        b = blocks.get((C, motion))
+        return b is not None and b.fold(i, rows) is not None
+
+    dev.device_attention = True
+    dev.ln_fold = ln_fold
+    return dev
+
+
 def block_errors(unet, lat, ehs, t=961, log=None):
     """-> [(block name, rel-L2 vs fp32 oracle, rel-L2 vs device-emulating oracle)]."""
     rows_out = []
@@ -37,7 +60,7 @@ def block_errors(unet, lat, ehs, t=961, log=None):
     B, _, F, H, W = x_in.shape
     g, eps = cfg["norm_num_groups"], cfg["norm_eps"]
     heads, mheads, mlen = cfg["num_attention_heads"], cfg["motion_num_attention_heads"], cfg["motion_max_seq_length"]
-    R = {m: unet_ref.ROUNDERS[m] for m in ("fp32", "dev")}
+    R = {"fp32": unet_ref.ROUNDERS["fp32"], "dev": device_rounder(unet)}
     # device context
     tt = torch.full((B,), float(t), device="cuda")
     te = ops.timestep_embed(tt, unet.time_proj.num_channels)

@@ -159,4 +159,4 @@ def test_product_library_has_no_selector_state():
     data = [name for _, kind, name in syms if kind in "BDGRSV" and not name.startswith("__hip_cuid_")]
     assert data == [], data
     fields = [f for f, _ in L.GemmDesc._fields_]
-    assert fields[-5:] == ["path", "plan_m", "rmap_n1", "rmap_n2", "rmap_inner"]
+    assert fields[-7:] == ["path", "plan_m", "rmap_n1", "rmap_n2", "rmap_inner", "ln_fold_s", "ln_fold_eps"]

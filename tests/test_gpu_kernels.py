@@ -14,7 +14,7 @@ import torch.nn.functional as F
 
 from vdiff import ops
 from vdiff.dist import block_transpose_reference, rev3_reference
-from vdiff.models.layers import pack_conv3x3, pack_geglu
+from vdiff.models.layers import LnFold, pack_conv3x3, pack_geglu
 
 pytestmark = pytest.mark.gpu
 BF = torch.bfloat16
@@ -241,6 +241,68 @@ def test_gemm_v8_strided_operands(cuda):
     assert torch.equal(outs[0], outs[1]), "v8 != v2 on strided views"
     assert torch.all(outs[0][:, :160] == 7.0), "v8 wrote outside its column slice"
     close_bf16(outs[0][:, 160:], a.float() @ w.float().T + bias + res.float())
+
+
+@pytest.mark.parametrize("M,N,kind,offset", [(16384, 960, "plain", 0.0), (16384 + 37, 320, "plain", 30.0),
+                                              (65536 + 16 * 5 + 3, 2560, "geglu", 0.0), (20000, 2560, "geglu", 30.0),
+                                              (131072, 960, "plain", 0.0)])
+def test_gemm_ln_fold(cuda, M, N, kind, offset):
+    """vd_gemm_desc.ln_fold_s (round 5): Linear(LayerNorm(x)) as ONE v8 GEMM over the un-normalised
+    rows (LnFold: W' = W∘gamma in bf16, s = its row sums, b' = b + W·beta; each row's mean / rstd
+    from the A fragments by two extra MFMAs per k-step).  Within bf16 output rounding of fp64 of the
+    same folded arithmetic; within the unfolded path's own rounding (bf16 normalised rows) of fp64
+    LayerNorm -> Linear and of the unfolded device path (vd_layernorm + GEMM); rows whose mean is 30
+    std exercise the fp32 one-pass variance; ragged M (partial row block, unequal XCD ranges)."""
+    K = 320
+    g = torch.Generator(device=cuda).manual_seed(0)
+    x = bf(1.7 * (torch.randn(M, K, device=cuda, generator=g) + offset
+                  + 0.5 * torch.randn(M, 1, device=cuda, generator=g)))
+    norm = torch.nn.LayerNorm(K).to(cuda)
+    with torch.no_grad():
+        norm.weight.copy_(1 + 0.2 * torch.randn(K, device=cuda, generator=g))
+        norm.bias.copy_(0.1 * torch.randn(K, device=cuda, generator=g))
+    w = torch.randn(N, K, device=cuda, generator=g) * K ** -0.5
+    b = 0.1 * torch.randn(N, device=cuda, generator=g)
+    geglu = kind == "geglu"
+    act = ops.ACT_GEGLU if geglu else ops.ACT_NONE
+    fold = LnFold(norm, w, b, pack=pack_geglu if geglu else None)
+    assert fold.runs(M, act), "the plan does not fold this shape"
+    got = fold.gemm(x, act=act)
+
+    def epi(y):  # packed GEGLU pairs -> h * gelu(g)
+        if not geglu:
+            return y
+        y = y.reshape(M, -1, 2, 16)
+        return y[:, :, 0].reshape(M, -1) * F.gelu(y[:, :, 1].reshape(M, -1))
+
+    xd = x.double()
+    mean = xd.mean(1, keepdim=True)
+    rstd = (xd.var(1, unbiased=False, keepdim=True) + fold.eps).rsqrt()
+    same = epi(rstd * (xd @ fold.w.double().T - mean * fold.s.double()) + fold.b.double())
+    close_bf16(got, same)
+    wp = pack_geglu(w) if geglu else w
+    bp = pack_geglu(b) if geglu else b
+    ln = F.layer_norm(xd, (K,), norm.weight.double(), norm.bias.double(), norm.eps)
+    ref = epi(ln @ wp.double().T + bp.double())
+    unfolded = ops.gemm(ops.layer_norm(x, norm.weight.detach().float().contiguous(),
+                                       norm.bias.detach().float().contiguous()), bf(wp).contiguous(), bias=bp, act=act)
+    e_ref = ((got.double() - ref).norm() / ref.norm()).item()
+    e_unf = ((unfolded.double() - ref).norm() / ref.norm()).item()
+    e_dev = ((got.double() - unfolded.double()).norm() / ref.norm()).item()
+    print(f"M={M} N={N} {kind} offset {offset}: folded vs fp64 {e_ref:.5f}, unfolded vs fp64 {e_unf:.5f}, "
+          f"folded vs unfolded {e_dev:.5f}")
+    assert e_ref < 5e-3 and e_dev < 7e-3
+    assert e_ref < 1.5 * e_unf + 1e-3  # no worse than the unfolded path's own bf16 rounding
+
+
+def test_gemm_ln_fold_refused_off_v8(cuda):
+    """A fold no kernel takes is refused (VD_EUNSUPPORTED), never run on another kernel."""
+    K, M = 320, 1024
+    norm = torch.nn.LayerNorm(K).to(cuda)
+    fold = LnFold(norm, torch.randn(320, K, device=cuda) * K ** -0.5)
+    assert not fold.runs(M)
+    with pytest.raises(Exception, match="unsupported|1001"):
+        fold.gemm(rnd(M, K))
 
 
 @pytest.mark.parametrize("path,M,N,K", [(0, 16384, 320, 320), (8, 4096, 320, 320), (0, 4096, 640, 640),

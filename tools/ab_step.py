@@ -1,0 +1,85 @@
+"""Same-process A/B of one model-side switch over the whole captured denoising step.
+
+    python tools/ab_step.py --switch ln_fold [--world 1|2|4|8] [--frames 16] [--rounds 6] [--steps 10]
+
+Both arms are captured on ONE model in one process (each its own hipGraph), then replayed in
+alternating rounds, so box-to-box clock differences cancel (MI355X_MICROARCH.md rule of same-box
+A/Bs).  --world N > 1 runs rank 0 of an N-way frame-sharded step with the collectives replaced by
+same-size device copies (tools/rank_emulate.py's EmulatedShard).
+
+Switches:
+  ln_fold  LayerNorm folded into its consuming v8 GEMM (BasicTransformerBlock._fold; round 5)
+           against the unfolded norm -> GEMM."""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "video-diffusion-experiments_amd"), str(ROOT / "tools")]
+
+import torch  # noqa: E402
+
+from vdiff import DDIMScheduler, DenoiseLoop  # noqa: E402
+from vdiff.models.blocks import BasicTransformerBlock  # noqa: E402
+from vdiff.weights import materialize_synthetic  # noqa: E402
+
+
+def set_ln_fold(unet, on, saved):
+    for m in unet.modules():
+        if isinstance(m, BasicTransformerBlock):
+            if id(m) not in saved:
+                saved[id(m)] = getattr(m, "_fold", {})
+            m._fold = saved[id(m)] if on else {}
+
+
+SWITCHES = {"ln_fold": set_ln_fold}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--switch", default="ln_fold", choices=sorted(SWITCHES))
+    ap.add_argument("--world", type=int, default=1)
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=10)
+    args = ap.parse_args()
+    unet = materialize_synthetic("full", device="cuda", seed=0)
+    if args.world > 1:
+        from rank_emulate import EmulatedShard
+        unet.dist = EmulatedShard(args.world, 1, "copy")
+    unet.prepare()
+    fl = args.frames // args.world
+    lat = torch.randn(1, 4, fl, 64, 64, device="cuda")
+    ehs = torch.randn(2, 77, unet.config["cross_attention_dim"], device="cuda")
+    s = DDIMScheduler(beta_schedule="linear", steps_offset=1, clip_sample=False)
+    s.set_timesteps(50)
+    ts = s.timesteps.repeat(1 + (args.rounds * args.steps + 10) // 50)
+    saved, loops = {}, {}
+    for arm in ("on", "off"):
+        SWITCHES[args.switch](unet, arm == "on", saved)
+        loops[arm] = DenoiseLoop(unet, s, lat.clone(), ehs, 7.5, timesteps=ts, use_graph=True).prime()
+        assert loops[arm].graph is not None, loops[arm].graph_error
+        loops[arm].run(3)
+    SWITCHES[args.switch](unet, True, saved)
+    res = {a: [] for a in loops}
+    for _ in range(args.rounds):
+        for arm, lp in loops.items():
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            lp.run(args.steps)
+            torch.cuda.synchronize()
+            res[arm].append(1e3 * (time.perf_counter() - t0) / args.steps)
+    for arm, v in res.items():
+        v = sorted(v)
+        print(f"{args.switch} {arm}: world {args.world} frames/rank {fl}: median {v[len(v) // 2]:.3f} ms/step, "
+              f"min {v[0]:.3f} (rounds {len(v)})", flush=True)
+    print(json.dumps({"switch": args.switch, "world": args.world, "frames_local": fl,
+                      "ms_per_step": {a: sorted(round(x, 3) for x in v) for a, v in res.items()}}))
+
+
+if __name__ == "__main__":
+    main()

@@ -1875,17 +1875,25 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const vd_gemm_desc d, 
 constexpr int G8_BN = 160, G8_KMAX = 320, G8_NW = 8;
 constexpr int G8_SUB = G8_BN * BK * 2;  // one 64-deep W sub-tile: 20 KiB
 
-template <bool RES, bool GEGLU, bool PERM = false>
+// LNF (round 5, vd_gemm_desc.ln_fold_s): the LayerNorm of A's rows folded in.  Per k-step two
+// more MFMAs on the A fragments the wave already holds — ones·x (every output column = the row
+// sum) and x·xᵀ (the 16 x 16 Gram block, whose diagonal is the row's sum of squares) — so the
+// statistics cost no VALU inside the loop; the epilogue forms rstd·(acc − mean·s[n]) + b'[n]
+// with s and b' in LDS next to the bias.  var = E[x²] − mean² in fp32: its relative error is
+// ≈ 1e-7·(1 + mean²/var), below bf16 rounding for |mean| / std up to ~100
+// (tests/test_gpu_kernels.py::test_gemm_ln_fold covers a row offset of 30 std).
+template <bool RES, bool GEGLU, bool PERM = false, bool LNF = false>
 __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                              uint32_t w_bytes, uint32_t c_bytes, int tiles_n,
                                                              int groups) {
   constexpr int KS = G8_KMAX / 32, NB = G8_BN / 16, NW = G8_NW;
   constexpr int OROW = G8_BN * 2 + 16;  // staged output row (bytes, padded)
-  __shared__ __attribute__((aligned(1024))) char smem[(G8_KMAX / BK) * G8_SUB + G8_BN * 4 + NW * 16 * OROW];
+  __shared__ __attribute__((aligned(1024))) char smem[(G8_KMAX / BK) * G8_SUB + G8_BN * 8 + NW * 16 * OROW];
   float* sbias = (float*)(smem + (G8_KMAX / BK) * G8_SUB);
+  float* ssum = sbias + G8_BN;  // LNF: s[n] of the tile's columns
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  char* obuf = smem + (G8_KMAX / BK) * G8_SUB + G8_BN * 4 + wid * 16 * OROW;
+  char* obuf = smem + (G8_KMAX / BK) * G8_SUB + G8_BN * 8 + wid * 16 * OROW;
   const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
   if (j >= groups * tiles_n) return;  // the XCD's workgroups beyond a whole number of W tiles
   const int nt = j % tiles_n, grp = j / tiles_n;
@@ -1905,7 +1913,10 @@ __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc
       const uint32_t n = (uint32_t)(n0 + pr * 8 + rb);
       dma16(rw, smem + s * G8_SUB + pr * 1024, n * (uint32_t)(d.ldw * 2) + (uint32_t)(s * BK * 2) + lc16);
     }
-    if (tid < G8_BN) sbias[tid] = d.bias ? d.bias[n0 + tid] : 0.f;
+    if (tid < G8_BN) {
+      sbias[tid] = d.bias ? d.bias[n0 + tid] : 0.f;
+      if constexpr (LNF) ssum[tid] = d.ln_fold_s[n0 + tid];
+    }
     wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1952,6 +1963,8 @@ __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc
 #pragma unroll
       for (int a = 0; a < NB; ++a) f[a] = *(const bf16x8*)(sb + wk + a * 16 * BK * 2);
     };
+    f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, gacc = f32x4{0.f, 0.f, 0.f, 0.f};  // LNF: ones·x, x·xᵀ
+    const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
     read_w(wf[0], 0);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -1959,7 +1972,23 @@ __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc
 #pragma unroll
       for (int a = 0; a < NB; ++a)
         acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks & 1][a], x[ks], acc[a], 0, 0, 0);
+      if constexpr (LNF) {
+        sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, x[ks], sacc, 0, 0, 0);
+        gacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[ks], x[ks], gacc, 0, 0, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);  // one k-step per region (unpinned, hipcc spilled)
+    }
+    // LNF: this lane's outputs all belong to A row rb*16 + fr.  Σx is in every entry of sacc;
+    // Σx² is the Gram block's diagonal entry (fr, fr), held by lane fr + 16 (fr >> 2) at index fr & 3
+    float nmean = 0.f, rstd = 1.f;
+    if constexpr (LNF) {
+      const int j3 = fr & 3;
+      const float gd = j3 == 0 ? gacc[0] : j3 == 1 ? gacc[1] : j3 == 2 ? gacc[2] : gacc[3];
+      const float sxx = __shfl(gd, fr + 16 * (fr >> 2), 64);
+      constexpr float RK = 1.0f / (float)G8_KMAX;
+      const float mean = sacc[0] * RK;
+      rstd = rsqrtf(fmaxf(fmaf(sxx, RK, -mean * mean), 0.f) + d.ln_fold_eps);
+      nmean = -mean;
     }
     if constexpr (GEGLU) {
       // (hidden, gate) 16-column block pairs (a, a+1) -> 16 output columns: the lane's 4 outputs
@@ -1968,12 +1997,28 @@ __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc
       for (int a = 0; a < NB; a += 2) {
         const int c = a * 16 + 4 * fq;
         const float4 th = *(const float4*)(sbias + c), tg = *(const float4*)(sbias + c + 16);
+        const float thv[4] = {th.x, th.y, th.z, th.w}, tgv[4] = {tg.x, tg.y, tg.z, tg.w};
+        float hv[4], gv[4];
+        if constexpr (LNF) {
+          const float4 sh = *(const float4*)(ssum + c), sg = *(const float4*)(ssum + c + 16);
+          const float shv[4] = {sh.x, sh.y, sh.z, sh.w}, sgv[4] = {sg.x, sg.y, sg.z, sg.w};
+#pragma unroll
+          for (int j4 = 0; j4 < 4; ++j4) {
+            hv[j4] = fmaf(rstd, fmaf(nmean, shv[j4], acc[a][j4]), thv[j4]);
+            gv[j4] = fmaf(rstd, fmaf(nmean, sgv[j4], acc[a + 1][j4]), tgv[j4]);
+          }
+        } else {
+#pragma unroll
+          for (int j4 = 0; j4 < 4; ++j4) {
+            hv[j4] = acc[a][j4] + thv[j4];
+            gv[j4] = acc[a + 1][j4] + tgv[j4];
+          }
+        }
         uint32_t pk[2];
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
-          const f32x2 go = gelu_erf2(f32x2{acc[a + 1][2 * h2], acc[a + 1][2 * h2 + 1]} +
-                                     (h2 ? f32x2{tg.z, tg.w} : f32x2{tg.x, tg.y}));
-          const f32x2 oo = (f32x2{acc[a][2 * h2], acc[a][2 * h2 + 1]} + (h2 ? f32x2{th.z, th.w} : f32x2{th.x, th.y})) * go;
+          const f32x2 go = gelu_erf2(f32x2{gv[2 * h2], gv[2 * h2 + 1]});
+          const f32x2 oo = f32x2{hv[2 * h2], hv[2 * h2 + 1]} * go;
           pk[h2] = pack2(oo[0], oo[1]);
         }
         *(uint2*)(obuf + fr * OROW + ((a / 2) * 16 + 4 * fq) * 2) = make_uint2(pk[0], pk[1]);
@@ -2003,8 +2048,17 @@ __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc
       for (int jj = 0; jj < 4; ++jj) {
         auto rp = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[a][jj]), __float_as_uint(acc[a + 1][jj]),
                                                    false, false);
-        o[jj] = __uint_as_float(rp[0]) + bv[jj];
-        o[4 + jj] = __uint_as_float(rp[1]) + bv[4 + jj];
+        o[jj] = __uint_as_float(rp[0]);
+        o[4 + jj] = __uint_as_float(rp[1]);
+      }
+      if constexpr (LNF) {
+        const float4 u0 = *(const float4*)(ssum + c), u1 = *(const float4*)(ssum + c + 4);
+        const float sv[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) o[jj] = fmaf(rstd, fmaf(nmean, sv[jj], o[jj]), bv[jj]);
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) o[jj] += bv[jj];
       }
       if (d.act == VD_ACT_SILU || d.act == VD_ACT_GELU) {
 #pragma unroll
@@ -2131,7 +2185,11 @@ int launch8(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t wb) {
   if (groups < 1) return VD_EINVAL;
   const uint32_t cb = (uint32_t)(d.M * d.ldc * 2);
   const dim3 grid((unsigned)(8 * per_xcd)), block(G8_NW * 64);
-  if (d.act == VD_ACT_GEGLU)
+  if (d.ln_fold_s && d.act == VD_ACT_GEGLU)
+    hipLaunchKernelGGL((gemm8_kernel<false, true, false, true>), grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
+  else if (d.ln_fold_s)
+    hipLaunchKernelGGL((gemm8_kernel<false, false, false, true>), grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
+  else if (d.act == VD_ACT_GEGLU)
     hipLaunchKernelGGL((gemm8_kernel<false, true>), grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
   else if (d.res && d.rmap_inner)
     hipLaunchKernelGGL((gemm8_kernel<true, false, true>), grid, block, 0, s, d, a0b, wb, cb, tiles_n, groups);
@@ -2206,7 +2264,7 @@ void read_num_cus() {  // once per process: the plan (and the workspace size) de
 // every decision (kernel, tile count, split-K, LayerNorm fusion) as if M were plan_m while the
 // launch covers all M rows: an unsharded run planned with a frame shard's M reproduces that
 // shard's arithmetic exactly (split-K fixes the summation order).
-Plan plan(const vd_gemm_desc& d) {
+Plan plan_core(const vd_gemm_desc& d) {
   read_num_cus();
   Plan p;
   int path = d.path;
@@ -2236,6 +2294,17 @@ Plan plan(const vd_gemm_desc& d) {
   // profiles/r04_gemm_v8.txt)
   const bool v8auto = v8ok && M >= 16384;
   if (path == 8 && !v8ok) path = 0;  // forced v8 on a shape it does not take: the product plan
+  // a folded LayerNorm (ln_fold_s) runs on v8 wherever v8 would run the plain GEMM (or is forced);
+  // no other kernel carries it: ver 0 = not runnable, the caller takes the unfolded form
+  if (d.ln_fold_s) {
+    if ((v8auto && path == 0) || (v8ok && path == 8)) {
+      p.ver = 8;
+      p.bn = G8_BN;
+    } else {
+      p.ver = 0;
+    }
+    return p;
+  }
   // an output-row map (rmap; no ln_out, GEGLU or row bias — checked) is carried by v8 (with a
   // residual), v6 and v1 only: the v2 / v3 / v5 pipelines sit at their register limit and spill
   // with it (tests/test_kernel_resources.py).  v6 splits K only where forced (path 6).
@@ -2378,6 +2447,18 @@ Plan plan(const vd_gemm_desc& d) {
   return p;
 }
 
+// a folded LayerNorm only ever runs on v8: every other outcome of the plan (its early exits
+// included) is "no kernel"
+Plan plan(const vd_gemm_desc& d) {
+  Plan p = plan_core(d);
+  if (d.ln_fold_s && p.ver != 8) {
+    p.ver = 0;
+    p.split = 1;
+    p.ws_bytes = 0;
+  }
+  return p;
+}
+
 }  // namespace
 
 // kt <= 1 (a plain 2-D conv or any dense GEMM): one "frame" per video, no temporal offset,
@@ -2394,6 +2475,14 @@ vd_gemm_desc normalized(const vd_gemm_desc& in) {
 }
 
 extern "C" int64_t vd_gemm_ws_bytes(const vd_gemm_desc* d) { return d ? plan(normalized(*d)).ws_bytes : 0; }
+
+extern "C" int vd_gemm_plan(const vd_gemm_desc* d, int32_t* kernel, int32_t* split) {
+  if (!d || !kernel || !split) return VD_EINVAL;
+  const Plan p = plan(normalized(*d));
+  *kernel = p.ver;
+  *split = p.split;
+  return VD_OK;
+}
 
 extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   if (!dp) return VD_EINVAL;
@@ -2441,12 +2530,17 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
   if (d.rmap_inner > 0)
     VD_CHECK_ARG(Rev3::ok(d.M, d.rmap_n1, d.rmap_n2, d.rmap_inner) && !d.ln_out && !d.rowbias &&
                  d.act != VD_ACT_GEGLU);
+  if (d.ln_fold_s) {
+    VD_CHECK_ARG(al16(d.ln_fold_s) && d.ln_fold_eps >= 0.f && !d.res && !d.rowbias && !d.ln_out && !d.rmap_inner &&
+                 d.a_mode == VD_A_DENSE && !d.a1 && d.k0 == d.K);
+  }
   if (d.ln_out) {
     VD_CHECK_ARG(!d.out_f32 && d.act != VD_ACT_GEGLU && d.ln_gamma && d.ln_beta && al16(d.ln_gamma) &&
                  al16(d.ln_beta) && d.ld_ln % 4 == 0 && al8(d.ln_out) && d.N % 4 == 0);
     if (d.ln_pe) VD_CHECK_ARG(al16(d.ln_pe) && d.ln_pe_div > 0 && d.ln_pe_period > 0);
   }
   const Plan p = plan(d);
+  if (p.ver == 0) return VD_EUNSUPPORTED;  // a folded LayerNorm no kernel takes at this shape
   if (p.ver >= 2 && p.split > 1) VD_CHECK_ARG(d.ws && al16(d.ws) && d.ws_bytes >= p.ws_bytes);
   if (d.ln_out && !p.ln_fused) {  // the GEMM, then vd_layernorm over its output
     vd_gemm_desc g = d;

@@ -27,6 +27,7 @@ SIGNATURES = {
     "vd_build_arch": ([], C.c_char_p),
     "vd_gemm": ([c_vp, c_vp], c_i32),
     "vd_gemm_ws_bytes": ([c_vp], c_i64),
+    "vd_gemm_plan": ([c_vp, c_vp, c_vp], c_i32),
     "vd_gn_partial": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp], c_i32),
     "vd_gn_finalize": ([c_vp, c_i64, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp], c_i32),
     "vd_gn_apply": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_i64, c_vp], c_i32),
@@ -93,6 +94,7 @@ class GemmDesc(C.Structure):
         ("ln_out", c_vp), ("ld_ln", c_i64),
         ("path", c_i32), ("plan_m", c_i64),
         ("rmap_n1", c_i32), ("rmap_n2", c_i32), ("rmap_inner", c_i32),
+        ("ln_fold_s", c_vp), ("ln_fold_eps", c_f32),
     ]
 
 

@@ -17,6 +17,7 @@ Every block has two entry points over the same kernels (see layers.py):
 """
 from __future__ import annotations
 
+import math
 from collections import namedtuple
 from typing import Optional
 
@@ -24,8 +25,8 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .layers import (Act, Attention, Conv2d, Downsample2D, Dropout, FeedForward, GroupNorm, LayerNorm,
-                     Linear, SiLU, SinusoidalPositionalEmbedding, Upsample2D, add, bf, f32, fmap_rows,
+from .layers import (Act, Attention, Conv2d, Downsample2D, Dropout, FeedForward, GroupNorm, LayerNorm, LnFold,
+                     Linear, pack_geglu, SiLU, SinusoidalPositionalEmbedding, Upsample2D, add, bf, f32, fmap_rows,
                      rows_fmap, token_rows)
 
 Transformer2DModelOutput = namedtuple("Transformer2DModelOutput", ["sample"])
@@ -122,19 +123,58 @@ class BasicTransformerBlock(nn.Module):
         m = getattr(self, f"norm{i}")
         return m._g, m._b
 
+    def prepare(self):
+        """LayerNorms folded into the GEMM that consumes them (LnFold, vd_gemm_desc.ln_fold_s)
+        wherever the library's plan takes the shape (the weight-stationary K = 320 GEMM): the
+        spatial block's norm1 -> fused QKV, norm2 -> to_q, norm3 -> GEGLU; the motion block's
+        norm3 -> GEGLU (its norm1 / norm2 add the positional encoding after the norm and feed
+        the fused temporal QKV kernel)."""
+        self._fold = {}
+        proj = self.ff.net[0].proj
+        cand = {3: (self.norm3, proj.weight.float(), proj.bias, pack_geglu, ops.ACT_GEGLU)}
+        if self.attn2.is_cross:
+            c = self.attn1.dim_head ** -0.5 * math.log2(math.e)  # Attention.prepare's q scale
+            a1 = self.attn1
+            cand[1] = (self.norm1, torch.cat([a1.to_q.weight.float() * c, a1.to_k.weight.float(),
+                                              a1.to_v.weight.float()], 0), None, None, ops.ACT_NONE)
+            cand[2] = (self.norm2, self.attn2.to_q.weight.float() * c, None, None, ops.ACT_NONE)
+        for i, (nrm, w, b, pack, act) in cand.items():
+            if ops.ln_fold_shape_ok(w.shape[0], w.shape[1], act=act):
+                self._fold[i] = (LnFold(nrm, w, b, pack=pack), act)
+
+    def fold(self, i, M):
+        """norm i's LnFold when its consumer GEMM runs folded over M rows, else None."""
+        f = getattr(self, "_fold", {}).get(i)
+        return f[0] if f is not None and f[0].runs(M, f[1]) else None
+
+    def _out_norm(self, a, attn, i, h, **pe):
+        """h' = to_out(a) + h and norm i of it: (h', n), or (h', None) when norm i folds into
+        its consumer (the rows are then never normalised in memory)."""
+        if pe.get("pe") is None and self.fold(i, h.shape[0]) is not None:
+            return ops.gemm(a, attn._wo, bias=attn._bo, res=h), None
+        return ops.gemm_ln(a, attn._wo, *self._nrm(i), bias=attn._bo, res=h, **pe)
+
+    def _ff(self, h, n):
+        f3 = self.fold(3, h.shape[0]) if n is None else None
+        return self.ff.forward_rows(h if n is None else n, h, fold=f3)
+
     # spatial: tokens are (image, pixel) rows
     # run_*: `n` = norm1(h) when the caller's GEMM already produced it (ops.gemm_ln: the
     # LayerNorm fused into the epilogue of the GEMM writing h, or run right after it)
     def run_spatial(self, h, n_img, hw, ctx: Ctx, n=None):
         C = h.shape[1]
         d = self.dim_head
-        if n is None:
-            n = ops.layer_norm(h, *self._nrm(1))
-        qkv = ops.gemm(n, self.attn1._wqkv)
+        f1 = self.fold(1, h.shape[0]) if n is None else None
+        if f1 is not None:
+            qkv = f1.gemm(h)
+        else:
+            if n is None:
+                n = ops.layer_norm(h, *self._nrm(1))
+            qkv = ops.gemm(n, self.attn1._wqkv)
         a = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], n_img, self.heads, hw, hw, d,
                           scale=self.attn1.attn_scale)
-        h, n = ops.gemm_ln(a, self.attn1._wo, *self._nrm(2), bias=self.attn1._bo, res=h)
-        q = ops.gemm(n, self.attn2._wq)
+        h, n = self._out_norm(a, self.attn1, 2, h)
+        q = self.fold(2, h.shape[0]).gemm(h) if n is None else ops.gemm(n, self.attn2._wq)
         kv = None if ctx.kv_cache is None else ctx.kv_cache.get(id(self.attn2))
         if kv is None:
             kv = self.attn2.project_kv(ctx.ehs_rows)
@@ -142,8 +182,8 @@ class BasicTransformerBlock(nn.Module):
                 ctx.kv_cache[id(self.attn2)] = kv
         a = ops.attention(q, kv[:, :C], kv[:, C:], n_img, self.heads, hw, ctx.ctx_len, d,
                           kv_div=ctx.frames, scale=self.attn2.attn_scale)
-        h, n = ops.gemm_ln(a, self.attn2._wo, *self._nrm(3), bias=self.attn2._bo, res=h)
-        return self.ff.forward_rows(n, h)
+        h, n = self._out_norm(a, self.attn2, 3, h)
+        return self._ff(h, n)
 
     # temporal: tokens are (video, frame, position) rows; attention over frames
     def run_temporal(self, h, batch, frames, positions, n=None):
@@ -162,9 +202,9 @@ class BasicTransformerBlock(nn.Module):
                 a = ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch, frames,
                                            positions, self.heads, d, scale=attn.attn_scale)
             # norm2 (+ PE) after attn1, norm3 after attn2
-            h, n = ops.gemm_ln(a, attn._wo, *self._nrm(i + 1), bias=attn._bo, res=h,
-                               pe=pe if i == 1 else None, pe_div=positions, pe_period=frames)
-        return self.ff.forward_rows(n, h)
+            h, n = self._out_norm(a, attn, i + 1, h, pe=pe if i == 1 else None, pe_div=positions,
+                                  pe_period=frames)
+        return self._ff(h, n)
 
     def run_temporal_gathered(self, h, batch, frames_local, positions, dist):
         """run_temporal on a frame-sharded rank's rows (b, f_loc, p) under the K/V all-gather
@@ -182,9 +222,9 @@ class BasicTransformerBlock(nn.Module):
                                        ops.block_transpose)
             a = ops.temporal_attention_kv(q, kv[:, :C], kv[:, C:], batch, frames_local, frames, positions,
                                           self.heads, d, scale=attn.attn_scale)
-            h, n = ops.gemm_ln(a, attn._wo, *self._nrm(i + 1), bias=attn._bo, res=h,
-                               pe=pe if i == 1 else None, pe_div=positions, pe_period=frames_local)
-        return self.ff.forward_rows(n, h)
+            h, n = self._out_norm(a, attn, i + 1, h, pe=pe if i == 1 else None, pe_div=positions,
+                                  pe_period=frames_local)
+        return self._ff(h, n)
 
     def forward(self, hidden_states, attention_mask=None, encoder_hidden_states=None,
                 encoder_attention_mask=None, timestep=None, cross_attention_kwargs=None,
@@ -219,8 +259,11 @@ class Transformer2DModel(nn.Module):
         hw = x.h * x.w
         hn = ops.group_norm(x.t, x.n, hw, self.groups, 1e-6, self.norm._g, self.norm._b)
         blk = self.transformer_blocks[0]
-        h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b)
-        h = blk.run_spatial(h, x.n, hw, ctx, n=n)
+        if blk.fold(1, hn.shape[0]) is not None:  # norm1 folds into the QKV GEMM
+            h = blk.run_spatial(ops.gemm(hn, self.proj_in._w, bias=self.proj_in._b), x.n, hw, ctx)
+        else:
+            h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b)
+            h = blk.run_spatial(h, x.n, hw, ctx, n=n)
         out = ops.gemm(h, self.proj_out._w, bias=self.proj_out._b, res=x.t)
         return Act(out, x.n, x.h, x.w)
 

@@ -87,6 +87,38 @@ def pack_geglu(w: torch.Tensor) -> torch.Tensor:
     return torch.stack([h.reshape(shp), g.reshape(shp)], 1).reshape(w.shape).contiguous()
 
 
+class LnFold:
+    """Linear(LayerNorm(x)) as ONE GEMM over the un-normalised rows (vd_gemm_desc.ln_fold_s):
+        W·(gamma∘(x − mean)·rstd + beta) + b = rstd·(W'x − mean·s) + b',
+    W' = W∘gamma (column k scaled by gamma[k], rounded to bf16 once), s[n] = Σ_k W'[n][k] (fp32,
+    of the bf16 W' so the mean term cancels against the MFMA's own products), b' = b + W·beta.
+    The kernel takes mean / rstd of each row from the A fragments it already holds, so the
+    normalised rows are never written.  `pack` reorders output rows (GEGLU's interleave) after
+    folding; `w` is the Linear's weight in fp32 as the unfolded path would round it (the q rows
+    already carry the softmax scale)."""
+
+    def __init__(self, norm: nn.LayerNorm, w: torch.Tensor, b: Optional[torch.Tensor] = None, pack=None):
+        g = norm.weight.detach().double()
+        be = norm.bias.detach().double()
+        wd = w.detach().double()
+        wf = wd * g[None, :]
+        bp = wd @ be
+        if b is not None:
+            bp = bp + b.detach().double()
+        if pack is not None:
+            wf, bp = pack(wf), pack(bp)
+        self.w = wf.to(torch.bfloat16).contiguous()
+        self.s = self.w.double().sum(1).float().contiguous()
+        self.b = bp.float().contiguous()
+        self.eps = float(norm.eps)
+
+    def runs(self, M: int, act: int = 0) -> bool:
+        return ops.ln_fold_runs(M, self.w, self.s, act=act)
+
+    def gemm(self, x, act: int = 0):
+        return ops.gemm(x, self.w, bias=self.b, act=act, ln_fold=(self.s, self.eps))
+
+
 # ------------------------------------------------------------------ layout helpers
 def to_bf16_cuda(x: torch.Tensor) -> torch.Tensor:
     if not x.is_cuda:
@@ -390,8 +422,13 @@ class FeedForward(nn.Module):
     def prepare(self):
         self._w2, self._b2 = bf(self.net[2].weight), f32(self.net[2].bias)
 
-    def forward_rows(self, n, res):
-        g = ops.gemm(n, self.net[0]._w, bias=self.net[0]._b, act=ops.ACT_GEGLU)
+    def forward_rows(self, n, res, fold: Optional[LnFold] = None):
+        """ff(n) + res; with `fold` (the block's norm3 folded into the GEGLU GEMM) n is the
+        un-normalised residual stream itself."""
+        if fold is not None:
+            g = fold.gemm(n, act=ops.ACT_GEGLU)
+        else:
+            g = ops.gemm(n, self.net[0]._w, bias=self.net[0]._b, act=ops.ACT_GEGLU)
         return ops.gemm(g, self._w2, bias=self._b2, res=res)
 
     def forward(self, hidden_states):

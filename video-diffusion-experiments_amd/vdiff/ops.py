@@ -67,11 +67,47 @@ def gemm_plan(path: int = 0, plan_div: int = 0):
         _PLAN.path, _PLAN.plan_div = old
 
 
-def _run_gemm(d, device, what):
-    """Attach the split-K workspace the C side asks for (if any), then launch."""
+def _plan_controls(d):
     d.path = _PLAN.path
     if _PLAN.plan_div > 1 and d.M % _PLAN.plan_div == 0:
         d.plan_m = d.M // _PLAN.plan_div
+
+
+def gemm_plan_of(d):
+    """(kernel, split) vd_gemm would run for descriptor d under the current gemm_plan controls
+    (vd_gemm_plan; kernel 0 = refused)."""
+    _plan_controls(d)
+    k, sp = C.c_int32(0), C.c_int32(0)
+    check(lib().vd_gemm_plan(C.byref(d), C.byref(k), C.byref(sp)), "vd_gemm_plan")
+    return k.value, sp.value
+
+
+def ln_fold_runs(M, w, s, *, act=ACT_NONE):
+    """True when vd_gemm runs Linear(LayerNorm(x)) over M rows of x with the norm folded into
+    the GEMM (vd_gemm_desc.ln_fold_s: w = W∘gamma, s = its row sums) — the v8 plan; the caller
+    otherwise writes the normalised rows and runs the plain GEMM.  Decided by the library's own
+    plan (with plan_div, so a frame shard and its unsharded replay decide alike)."""
+    N, K = w.shape
+    nout = N // 2 if act == ACT_GEGLU else N
+    d = GemmDesc(a0=256, lda0=K, k0=K, a_mode=A_DENSE, w=_p(w), ldw=_rows(w), M=M, N=N, K=K, bias=256,
+                 act=act, out=256, ldc=nout, ln_fold_s=_p(s), ln_fold_eps=1e-5)
+    return gemm_plan_of(d)[0] == 8
+
+
+def ln_fold_shape_ok(N, K, *, act=ACT_NONE):
+    """Whether a folded LayerNorm (ln_fold_s) can run for an N x K Linear at all (asked at a
+    row count the automatic plan folds): decides at prepare time which folded weights to build."""
+    nout = N // 2 if act == ACT_GEGLU else N
+    d = GemmDesc(a0=256, lda0=K, k0=K, a_mode=A_DENSE, w=256, ldw=K, M=32768, N=N, K=K, bias=256, act=act,
+                 out=256, ldc=nout, ln_fold_s=256, ln_fold_eps=1e-5)
+    k, sp = C.c_int32(0), C.c_int32(0)
+    check(lib().vd_gemm_plan(C.byref(d), C.byref(k), C.byref(sp)), "vd_gemm_plan")
+    return k.value == 8
+
+
+def _run_gemm(d, device, what):
+    """Attach the split-K workspace the C side asks for (if any), then launch."""
+    _plan_controls(d)
     nbytes = lib().vd_gemm_ws_bytes(C.byref(d))
     ws = None
     if nbytes > 0:
@@ -82,10 +118,13 @@ def _run_gemm(d, device, what):
 
 
 def gemm(a, w, *, a1=None, bias=None, rowbias=None, rb_div=1, res=None, act=ACT_NONE,
-         out=None, out_f32=False, rmap=None):
+         out=None, out_f32=False, rmap=None, ln_fold=None):
     """out[m, n] = epi(sum_k cat(a, a1)[m, k] * w[n, k]); a/a1/w bf16, bias/rowbias fp32.
     rmap = (n1, n2, inner): product row m is written (and its residual read) at row rev3(m)
-    (vd_gemm_desc.rmap_*, vdiff.dist.frame_shard.rev3_reference)."""
+    (vd_gemm_desc.rmap_*, vdiff.dist.frame_shard.rev3_reference).
+    ln_fold = (s, eps): a is the UN-normalised input of a LayerNorm folded into this GEMM —
+    w = W∘gamma, bias = b + W·beta, s = w's fp32 row sums (vd_gemm_desc.ln_fold_s,
+    vdiff.models.layers.LnFold); raises when the plan cannot take it (see ln_fold_runs)."""
     _dev(a, w, a1, bias, rowbias, res, out)
     M = a.shape[0]
     N, K = w.shape
@@ -108,6 +147,12 @@ def gemm(a, w, *, a1=None, bias=None, rowbias=None, rb_div=1, res=None, act=ACT_
                  out_f32=int(out_f32))
     if rmap is not None:
         d.rmap_n1, d.rmap_n2, d.rmap_inner = (int(v) for v in rmap)
+    if ln_fold is not None:
+        s, eps = ln_fold
+        _dev(s)
+        if s.dtype != torch.float32 or not s.is_contiguous() or s.numel() != N:
+            raise ValueError("ln_fold s must be a contiguous fp32 vector of N entries")
+        d.ln_fold_s, d.ln_fold_eps = _p(s), float(eps)
     _run_gemm(d, a.device, "vd_gemm")
     return out
 
