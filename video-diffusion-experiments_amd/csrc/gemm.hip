@@ -454,6 +454,18 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // after the barrier (sched_barrier), then k-step 1's reads interleave one per two of k-step 0's
 // MFMAs (sched_group_barrier), so the MFMA chain waits on counted lgkmcnt only (52.79 vs 53.50
 // ms/step for the unpinned order, 53.11 with all reads ahead; profiles/r02f_fragment_order.txt).
+#ifdef VD_G2_STAMPS
+// Diagnostic build only (tools/g2_stamps.py; never in libvdiff_hip.so): per-wave cycle sums of the
+// k-tile loop's segments — ring wait, barrier, fragment reads + MFMA issue, epilogue + DMA issue.
+__device__ unsigned long long g2_diag[4096 * 8 * 6];
+#define G2_STAMP(t)                                                                      \
+  do {                                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+  } while (0)
+#endif
+
 template <int BN, int MODE>
 __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                          uint32_t a1_bytes, uint32_t w_bytes,
@@ -630,7 +642,14 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
   unit_kr(cu, ckt, ckt1);
   const int fr = lane & 15, fq = lane >> 4;
   int stage = 0;
+#ifdef VD_G2_STAMPS
+  unsigned long long st0, st1, st2, st3, st4, sw = 0, sb = 0, sm = 0, stl = 0, tbeg;
+  G2_STAMP(tbeg);
+#endif
   for (int it = 0; it < n_it; ++it) {
+#ifdef VD_G2_STAMPS
+    G2_STAMP(st0);
+#endif
     // this wave's DMA for k-tile `it` has landed once at most k-tile it+1's remain
     // outstanding (everything issued before that, epilogue stores included, is done)
     if (it + 1 < n_it) {
@@ -639,8 +658,14 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     } else {
       wait_vm<0>();
     }
+#ifdef VD_G2_STAMPS
+    G2_STAMP(st1);
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's DMA for `it` landed; stage (it-1)%3 fully read
+#ifdef VD_G2_STAMPS
+    G2_STAMP(st2);
+#endif
     const char* sbase = smem + stage * C::STAGE;
     {
       bf16x8 wf[BK / 32][C::NB], xf[BK / 32][C::MB];
@@ -670,6 +695,9 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
         __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
       }
     }
+#ifdef VD_G2_STAMPS
+    G2_STAMP(st3);
+#endif
     if (++ckt == ckt1) {  // unit finished: epilogue (its memory ops precede the next DMA)
       const int tile = cu / split, sp = cu % split;
       const int64_t m0 = (int64_t)(tile / tiles_n) * G2_BM, n0 = (int64_t)(tile % tiles_n) * BN;
@@ -698,8 +726,30 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     }
     if (it + 2 < n_it) issue(stage == 0 ? 2 : stage - 1);
     stage = stage == 2 ? 0 : stage + 1;
+#ifdef VD_G2_STAMPS
+    G2_STAMP(st4);
+    sw += st1 - st0; sb += st2 - st1; sm += st3 - st2; stl += st4 - st3;
+#endif
   }
+#ifdef VD_G2_STAMPS
+  unsigned long long tend;
+  G2_STAMP(tend);
+  if (lane == 0 && blockIdx.x < 4096) {
+    unsigned long long* o = g2_diag + ((size_t)blockIdx.x * 8 + wid) * 6;
+    o[0] = sw; o[1] = sb; o[2] = sm; o[3] = stl; o[4] = tend - tbeg; o[5] = (unsigned long long)n_it;
+  }
+#endif
 }
+
+#ifdef VD_G2_STAMPS
+extern "C" int vd_diag_g2_read(void* host, int64_t n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g2_diag), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int vd_diag_g2_clear() {
+  static unsigned long long z[4096 * 8 * 6];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g2_diag), z, sizeof(z), 0, hipMemcpyHostToDevice);
+}
+#endif
 
 
 // Load-free epilogue (v5, split == 1, bf16 out, no residual / row bias): the bias
