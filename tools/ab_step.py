@@ -8,8 +8,9 @@ A/Bs).  --world N > 1 runs rank 0 of an N-way frame-sharded step with the collec
 same-size device copies (tools/rank_emulate.py's EmulatedShard).
 
 Switches:
-  ln_fold  LayerNorm folded into its consuming v8 GEMM (BasicTransformerBlock._fold; round 5)
-           against the unfolded norm -> GEMM."""
+  ln_fold    LayerNorm folded into its consuming v8 GEMM (BasicTransformerBlock._fold; round 5)
+             against the unfolded norm -> GEMM;
+  cfg_dedup  conv_in + down_blocks[0].resnets[0] once for both CFG halves (DenoiseLoop.cfg_dedup)."""
 from __future__ import annotations
 
 import argparse
@@ -36,7 +37,13 @@ def set_ln_fold(unet, on, saved):
             m._fold = saved[id(m)] if on else {}
 
 
-SWITCHES = {"ln_fold": set_ln_fold}
+def set_cfg_dedup(unet, on, saved):  # a hook on the loop before its capture
+    def hook(lp):
+        lp.cfg_dedup = on
+    return hook
+
+
+SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup}
 
 
 def main():
@@ -60,8 +67,11 @@ def main():
     ts = s.timesteps.repeat(1 + (args.rounds * args.steps + 10) // 50)
     saved, loops = {}, {}
     for arm in ("on", "off"):
-        SWITCHES[args.switch](unet, arm == "on", saved)
-        loops[arm] = DenoiseLoop(unet, s, lat.clone(), ehs, 7.5, timesteps=ts, use_graph=True).prime()
+        hook = SWITCHES[args.switch](unet, arm == "on", saved)
+        lp = DenoiseLoop(unet, s, lat.clone(), ehs, 7.5, timesteps=ts, use_graph=True)
+        if callable(hook):
+            hook(lp)
+        loops[arm] = lp.prime()
         assert loops[arm].graph is not None, loops[arm].graph_error
         loops[arm].run(3)
     SWITCHES[args.switch](unet, True, saved)

@@ -43,6 +43,9 @@ class Ctx:
         self.ctx_len = ctx_len
         self.dist = dist              # vdiff.dist.FrameShard or None
         self.kv_cache = kv_cache      # {id(attn): kv rows} or None
+        # the two CFG halves of the input are the same latents (DenoiseLoop): everything before
+        # the first cross-attention — conv_in and down_blocks[0].resnets[0] — runs on one half
+        self.cfg_dup = False
 
 
 def concat_channels(a, b):
@@ -364,12 +367,13 @@ class AnimateDiffTransformer3D(nn.Module):
 
 
 class _MotionBlockBase(nn.Module):
-    def _run_layers(self, x, ctx, skips_in=None):
+    def _run_layers(self, x, ctx, skips_in=None, res0=None):
+        """res0: resnets[0]'s output computed by the caller (UNetMotionModel's CFG dedup)."""
         outs = []
         attns = getattr(self, "attentions", None)
         for i, res in enumerate(self.resnets):
             skip = skips_in.pop() if skips_in is not None else None
-            x = res.run(x, ctx, skip=skip)
+            x = res0 if (i == 0 and res0 is not None) else res.run(x, ctx, skip=skip)
             if attns is not None:
                 x = attns[i].run(x, ctx)
             x = self.motion_modules[i].run(x, ctx)
@@ -405,8 +409,8 @@ class CrossAttnDownBlockMotion(_MotionBlockBase):
         self.downsamplers = (nn.ModuleList([Downsample2D(out_channels, out_channels)])
                              if add_downsample else None)
 
-    def run(self, x, ctx):
-        x, outs = self._run_layers(x, ctx)
+    def run(self, x, ctx, res0=None):
+        x, outs = self._run_layers(x, ctx, res0=res0)
         if self.downsamplers is not None:
             x = self.downsamplers[0].run(x)
             outs.append(x)

@@ -124,11 +124,24 @@ class UNetMotionModel(nn.Module):
         """Packed NHWC input rows [batch*frames*h*w, 8] -> eps rows fp32 [..., out_channels]."""
         g = self.config["norm_num_groups"]
         n_img = ctx.batch * ctx.frames
-        t, _, _ = ops.conv3x3(x_rows, n_img, h, w, self.conv_in._w, bias=self.conv_in._b)
+        blocks = list(self.down_blocks)
+        res0 = None
+        if ctx.cfg_dup and ctx.batch % 2 == 0:
+            # CFG dedup: both halves of x_rows are the same latents and the same timestep, so
+            # conv_in and down_blocks[0].resnets[0] (nothing reads the text embeddings before
+            # the first cross-attention) run on one half; their outputs are copied to the other
+            half = x_rows.shape[0] // 2
+            t = torch.empty(x_rows.shape[0], self.conv_in.out_channels, device=x_rows.device, dtype=torch.bfloat16)
+            ops.conv3x3(x_rows[:half], n_img // 2, h, w, self.conv_in._w, bias=self.conv_in._b, out=t[:half])
+            r1 = blocks[0].resnets[0].run(Act(t[:half], n_img // 2, h, w), ctx)
+            t[half:].copy_(t[:half])
+            res0 = Act(torch.cat([r1.t, r1.t]), n_img, h, w)
+        else:
+            t, _, _ = ops.conv3x3(x_rows, n_img, h, w, self.conv_in._w, bias=self.conv_in._b)
         x = Act(t, n_img, h, w)
         skips = [x]
-        for blk in self.down_blocks:
-            x, outs = blk.run(x, ctx)
+        for i, blk in enumerate(blocks):
+            x, outs = blk.run(x, ctx, res0=res0) if i == 0 else blk.run(x, ctx)
             skips.extend(outs)
         x = self.mid_block.run(x, ctx)
         for blk in self.up_blocks:

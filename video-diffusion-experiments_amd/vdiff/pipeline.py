@@ -109,6 +109,8 @@ class DenoiseLoop:
         self.x_in2 = ops.pack_latents(self.lat, dup=self.ncfg, cpad=CIN_PAD, in_div=self.in_div0)
         self.x_in = self.x_in2[:self.Bu * self.F * self.H * self.W]
         self.kv_cache = {}
+        # conv_in + down_blocks[0].resnets[0] once for both CFG halves (UNetMotionModel.forward_rows)
+        self.cfg_dedup = True
         self.use_graph = use_graph
         self.graph = None
         self.graph_error = None
@@ -127,6 +129,7 @@ class DenoiseLoop:
         u = self.unet
         te = ops.timestep_embed(self.ts, u.time_proj.num_channels, step_idx=self.step_idx, batch=self.Bu)
         ctx = u.make_ctx(te, self.ehs_rows, self.Bu, self.F, self.L, kv_cache=self.kv_cache)
+        ctx.cfg_dup = self.cfg_dedup and self.Bu == self.Bt == 2 * self.B  # x_in = [lat; lat]
         eps = u.forward_rows(self.x_in, self.H, self.W, ctx)
         if self.cfg_shard is not None:
             eps = self.cfg_shard.gather_eps(eps)
