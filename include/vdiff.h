@@ -265,7 +265,15 @@ int vd_temporal_attention_kv(const void* q, int64_t ldq, const void* k, const vo
  * the two-launch path. */
 int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* wqkv, int64_t ldw, void* o, int64_t ldo,
                             int64_t batch, int32_t frames, int64_t positions, int32_t heads, int32_t d,
-                            float scale, vd_stream_t stream);
+                            float scale, const float* ln_fold_tab, float ln_fold_eps, vd_stream_t stream);
+/* ln_fold_tab != NULL (round 5): the block's LayerNorm (+ the sinusoidal PE by frame) folded in,
+ * as vd_gemm_desc.ln_fold_s: x holds the UN-normalised rows, wqkv = W_qkv∘gamma (bf16), and
+ * ln_fold_tab is [8 heads][2048] fp32: per head h, the 120 row sums of wqkv's rows of that head
+ * (q | k | v, 40 each, in that order), then for each frame f < 16 the 120 values
+ * W·(beta + pe[f]) of the same rows (W the unfolded fp32 weight), zero-padded to 2048.
+ * vd_motion_qkv_attention_takes: 1 when the fused kernel takes the shape (else the call
+ * returns VD_EUNSUPPORTED and the caller runs GEMM + vd_temporal_attention); no launch. */
+int vd_motion_qkv_attention_takes(int64_t batch, int32_t frames, int64_t positions, int32_t heads, int32_t d);
 /* vd_temporal_attention for the DiT's temporal blocks (d = 64, 17..32 frames) with the 1-D
  * temporal RoPE (vd_rope_qk mode 1, angle by frame) applied to q/k inside the kernel as they
  * are loaded; q and k are read un-rotated and left unchanged. */

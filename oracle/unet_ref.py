@@ -92,22 +92,26 @@ def layer_norm(sd, p, x, eps=1e-5):
     return F.layer_norm(x, (x.shape[-1],), sd[p + ".weight"], sd[p + ".bias"], eps)
 
 
-def folded_linear(sd, norm_p, x, w, b=None, eps=1e-5):
+def folded_linear(sd, norm_p, x, w, b=None, eps=1e-5, pe=None):
     """The device's folded LayerNorm -> Linear ("dev" mode; vdiff.models.layers.LnFold and
     vd_gemm_desc.ln_fold_s): W' = bf16(W∘gamma), s = Σ_k W'[n][k], b' = W·beta + b and
     rstd·(x·W'^T − mean·s) + b' over the UN-normalised rows x — the same function as
-    Linear(LayerNorm(x)) up to the rounding of W' (the normalised rows are never rounded)."""
+    Linear(LayerNorm(x)) up to the rounding of W' (the normalised rows are never rounded).
+    pe (1, F, C): the motion block's PE added after the norm, folded as W·pe[f] per frame
+    (vdiff.models.layers.MotionLnFold); x is then (rows, F, C)."""
     g, be = sd[norm_p + ".weight"].double(), sd[norm_p + ".bias"].double()
     wd = w.double()
     wf = (wd * g[None, :]).to(torch.bfloat16).double()
     bp = wd @ be + (b.double() if b is not None else 0.0)
+    if pe is not None:
+        bp = bp + pe[:, : x.shape[1]].double() @ wd.T
     xd = x.double()
     mean = xd.mean(-1, keepdim=True)
     rstd = (xd.var(-1, unbiased=False, keepdim=True) + eps).rsqrt()
     return (rstd * (xd @ wf.T - mean * wf.sum(1)) + bp).float()
 
 
-def attention(sd, p, x, ctx, heads, rnd=_ident, fold_norm=None):
+def attention(sd, p, x, ctx, heads, rnd=_ident, fold_norm=None, pe=None):
     """diffusers:Attention + AttnProcessor2_0 (App. A.5): q/k/v without bias,
     softmax(q k^T / sqrt(d)) v, to_out.0 with bias, no residual inside.  fold_norm ("dev" mode):
     x is the un-normalised input of that LayerNorm, folded into q (and k / v of a
@@ -117,11 +121,11 @@ def attention(sd, p, x, ctx, heads, rnd=_ident, fold_norm=None):
     wq = sd[p + ".to_q.weight"]
     d = wq.shape[0] // heads
     if fold_norm is not None:  # vdiff BasicTransformerBlock.prepare: LnFold of the scaled q rows
-        q = rnd(folded_linear(sd, fold_norm, x, wq.float() * (d ** -0.5 * math.log2(math.e))))
+        q = rnd(folded_linear(sd, fold_norm, x, wq.float() * (d ** -0.5 * math.log2(math.e)), pe=pe))
         self_attn = ctx is x
-        k = rnd(folded_linear(sd, fold_norm, x, sd[p + ".to_k.weight"]) if self_attn
+        k = rnd(folded_linear(sd, fold_norm, x, sd[p + ".to_k.weight"], pe=pe) if self_attn
                 else linear(sd, p + ".to_k", ctx, bias=False))
-        v = rnd(folded_linear(sd, fold_norm, x, sd[p + ".to_v.weight"]) if self_attn
+        v = rnd(folded_linear(sd, fold_norm, x, sd[p + ".to_v.weight"], pe=pe) if self_attn
                 else linear(sd, p + ".to_v", ctx, bias=False))
     else:
         if dev:  # vdiff Attention.prepare: bf16(W_q * d^-1/2 * log2 e); scores in log2 units
@@ -170,10 +174,10 @@ def basic_transformer_block(sd, p, x, ehs, heads, pe=None, double_self=False, rn
     rows = x.shape[0] * x.shape[1]
 
     def folds(i):
-        return fold is not None and fold(i, x.shape[-1], rows, pe is not None)
+        return fold is not None and fold(i, x.shape[-1], rows, pe is not None, x.shape[1])
 
     if folds(1):
-        x = rnd(attention(sd, p + ".attn1", x, None, heads, rnd, fold_norm=p + ".norm1") + x)
+        x = rnd(attention(sd, p + ".attn1", x, None, heads, rnd, fold_norm=p + ".norm1", pe=pe) + x)
     else:
         n = layer_norm(sd, p + ".norm1", x)
         if pe is not None:
@@ -181,7 +185,7 @@ def basic_transformer_block(sd, p, x, ehs, heads, pe=None, double_self=False, rn
         x = rnd(attention(sd, p + ".attn1", rnd(n), None, heads, rnd) + x)
     ctx = None if double_self else ehs
     if folds(2):
-        x = rnd(attention(sd, p + ".attn2", x, ctx, heads, rnd, fold_norm=p + ".norm2") + x)
+        x = rnd(attention(sd, p + ".attn2", x, ctx, heads, rnd, fold_norm=p + ".norm2", pe=pe) + x)
     else:
         n = layer_norm(sd, p + ".norm2", x)
         if pe is not None:

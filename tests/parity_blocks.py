@@ -40,9 +40,13 @@ def device_rounder(unet):
     def dev(x):
         return unet_ref.ROUNDERS["dev"](x)
 
-    def ln_fold(i, C, rows, motion):
+    def ln_fold(i, C, rows, motion, frames=1):
         b = blocks.get((C, motion))
-        return b is not None and b.fold(i, rows) is not None
+        if b is None:
+            return False
+        if motion and i < 3:  # norm1 / norm2 + PE fold into the fused QKV attention
+            return b.mfold(i, 1, frames, rows // frames) is not None
+        return b.fold(i, rows) is not None
 
     dev.device_attention = True
     dev.ln_fold = ln_fold

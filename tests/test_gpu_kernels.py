@@ -1080,6 +1080,50 @@ def test_motion_qkv_attention(cuda, batch, positions, unit):
     close_bf16(got, ref.reshape(batch, positions, F, C).permute(0, 2, 1, 3).reshape(-1, C))
     assert ops.motion_qkv_attention(x[:, :320], w[:, :320], batch, 8, positions * 2, heads, d) is None  # 8 frames
     assert ops.motion_qkv_attention(x[:16 * 64], w, 1, F, 64, heads, d) is None  # 8 workgroups: unfused path
+    assert ops.motion_qkv_takes(batch, F, positions, heads, d) and not ops.motion_qkv_takes(1, F, 64, heads, d)
+
+
+@pytest.mark.parametrize("batch,positions,offset", [(2, 4096, 0.0), (1, 4100, 30.0), (1, 2048, 0.0)])
+def test_motion_qkv_attention_ln_fold(cuda, batch, positions, offset):
+    """vd_motion_qkv_attention with ln_fold_tab (round 5): the motion block's LayerNorm + PE by
+    frame folded into the fused QKV attention (MotionLnFold: W' = W∘gamma, per head the row sums
+    and W·(beta + pe[f])), over the UN-normalised rows — against the unfolded device path
+    (vd_layernorm with PE, then the same kernel on bf16(W)) within the two paths' bf16 roundings,
+    and against fp64 LayerNorm + PE -> QKV -> SDPA; rows offset by 30 std; both PW forms."""
+    from vdiff.models.layers import MotionLnFold
+    C, d, heads, NF = 320, 40, 8, 16
+    g = torch.Generator(device=cuda).manual_seed(3)
+    x = bf(1.3 * (torch.randn(batch * NF * positions, C, device=cuda, generator=g) + offset))
+    norm = torch.nn.LayerNorm(C).to(cuda)
+    with torch.no_grad():
+        norm.weight.copy_(1 + 0.2 * torch.randn(C, device=cuda, generator=g))
+        norm.bias.copy_(0.1 * torch.randn(C, device=cuda, generator=g))
+    pe = torch.randn(32, C, device=cuda, generator=g) * 0.5
+    w = torch.randn(3 * C, C, device=cuda, generator=g) * C ** -0.5 * 2.0
+    sc = 1.0 / math.log2(math.e)
+    mf = MotionLnFold(norm, w, pe, heads, d)
+    got = ops.motion_qkv_attention(x, mf.w, batch, NF, positions, heads, d, scale=sc, ln_fold=(mf.tab, mf.eps))
+    assert got is not None
+    gamma, beta = norm.weight.detach().float().contiguous(), norm.bias.detach().float().contiguous()
+    n = ops.layer_norm(x, gamma, beta, pe=pe.float().contiguous(), pe_div=positions, pe_period=NF)
+    unf = ops.motion_qkv_attention(n, bf(w).contiguous(), batch, NF, positions, heads, d, scale=sc)
+    xd = x.double()
+    ln = F.layer_norm(xd, (C,), norm.weight.double(), norm.bias.double(), norm.eps)
+    ln = ln + pe.double()[(torch.arange(x.shape[0], device=cuda) // positions) % NF]
+    qkv = ln @ w.double().T
+    q, k, v = qkv[:, :C] * (sc * math.sqrt(d)), qkv[:, C:2 * C], qkv[:, 2 * C:]
+
+    def tok(t):  # rows (b, f, p) -> (b*p, f, C)
+        return t.reshape(batch, NF, positions, C).permute(0, 2, 1, 3).reshape(batch * positions, NF, C)
+
+    ref = sdpa_ref(tok(q), tok(k), tok(v), batch * positions, heads, NF, NF, d)
+    ref = ref.reshape(batch, positions, NF, C).permute(0, 2, 1, 3).reshape(-1, C)
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+    e_ref, e_unf, e_dev = rel(got, ref), rel(unf, ref), rel(got, unf)
+    print(f"batch {batch} positions {positions} offset {offset}: folded vs fp64 {e_ref:.5f}, unfolded vs fp64 "
+          f"{e_unf:.5f}, folded vs unfolded {e_dev:.5f}")
+    assert e_ref < 2.5e-2 and e_dev < 3e-2  # the attention of bf16 q / k at this weight scale: ~1.5 % either way
+    assert e_ref < 1.5 * e_unf + 1e-3
 
 
 # ---------------------------------------------------------------- step glue

@@ -10,7 +10,8 @@ same-size device copies (tools/rank_emulate.py's EmulatedShard).
 Switches:
   ln_fold    LayerNorm folded into its consuming v8 GEMM (BasicTransformerBlock._fold; round 5)
              against the unfolded norm -> GEMM;
-  cfg_dedup  conv_in + down_blocks[0].resnets[0] once for both CFG halves (DenoiseLoop.cfg_dedup)."""
+  cfg_dedup  conv_in + down_blocks[0].resnets[0] once for both CFG halves (DenoiseLoop.cfg_dedup);
+  mfold      the motion block's norm1 / norm2 + PE folded into the fused QKV attention (_mfold)."""
 from __future__ import annotations
 
 import argparse
@@ -43,7 +44,16 @@ def set_cfg_dedup(unet, on, saved):  # a hook on the loop before its capture
     return hook
 
 
-SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup}
+def set_mfold(unet, on, saved):
+    for m in unet.modules():
+        if isinstance(m, BasicTransformerBlock):
+            key = ("m", id(m))
+            if key not in saved:
+                saved[key] = getattr(m, "_mfold", {})
+            m._mfold = saved[key] if on else {}
+
+
+SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup, "mfold": set_mfold}
 
 
 def main():

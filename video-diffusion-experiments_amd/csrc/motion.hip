@@ -99,13 +99,30 @@ __device__ __forceinline__ void mq_wait_vm() {
   else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
 }
 
+__device__ __forceinline__ void mq_wait_vm_rt(int n) {  // s_waitcnt vmcnt(n), n in 0..9
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+  }
+}
+
 template <int D>
 struct Mq2Cfg {
   using B = MqCfg<D>;
   static constexpr int W_BYTES = B::NWP * B::KC * 2;               // 16 KiB ring slot
   static constexpr int S_BYTES = B::S_ELEMS * 2;                   // per-wave scratch
-  static constexpr int LDS_BYTES = MQ2_S * W_BYTES + B::P * S_BYTES;
+  static constexpr int TAB_BYTES = 8192;                           // LNF: one head's s | P' table
+  static constexpr int LDS_BYTES = MQ2_S * W_BYTES + B::P * S_BYTES + 2 * TAB_BYTES;
   static_assert(B::NWP == 128 && B::KC == 64, "16 pieces of 8 ring rows x 128 B per chunk");
+  static_assert(8 * 1024 == TAB_BYTES && 3 * B::C / 8 * (1 + MF) <= TAB_BYTES / 4, "table: one KiB piece per wave");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
@@ -115,10 +132,17 @@ struct Mq2Cfg {
 // weight fragment two positions' MFMAs (half the LDS bytes per MFMA, half the weight stream per
 // token) for 40 more VGPRs of token fragments and 32 of accumulators; the heads' attention runs
 // position by position through the same per-wave scratch.
-template <int D, int PW = 1>
+// LNF (round 5): the motion block's norm1 / norm2 (+ the sinusoidal PE by frame) folded in, as
+// gemm.hip's v8 LNF: x holds the UN-normalised rows, w = W_qkv∘gamma, and `tab` per head h the
+// 120 fp32 column sums s of w's rows of that head (q | k | v, 40 each) then, per frame f < 16,
+// the 120 values P[f] = W·(beta + pe[f]) — an 8 KiB table that rides the weight ring as one 1 KiB
+// LDS-DMA piece per wave with the head's first chunk (double-buffered in LDS).  Each wave's token
+// rows (16 frames of a position) get mean / rstd from two extra MFMAs per k-step over the
+// fragments it already holds; the head epilogue writes rstd (acc - mean s) + P[frame] to the scratch.
+template <int D, int PW = 1, bool LNF = false>
 __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw, bf16_t* __restrict__ o,
-    int64_t ldo, int64_t batch, int64_t positions, float c) {
+    int64_t ldo, int64_t batch, int64_t positions, float c, const float* __restrict__ tab, float eps) {
   using Cf = MqCfg<D>;
   using C2 = Mq2Cfg<D>;
   constexpr int PWG = Cf::P * PW;  // positions per workgroup
@@ -131,6 +155,7 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
   bf16_t* q_s = s_l;                                     // [16][DPAD]
   bf16_t* k_s = s_l + MF * Cf::DPAD;                     // [16][DPAD]
   bf16_t* v_s = s_l + 2 * MF * Cf::DPAD;                 // V image [16][VS]
+  const uint32_t tab0 = (uint32_t)(MQ2_S * C2::W_BYTES + Cf::P * C2::S_BYTES);  // LNF tables (byte offset)
 
   const int64_t nblk_p = (positions + PWG - 1) / PWG;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
@@ -141,9 +166,13 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
   // 2w + 1 = ring rows 8g .. 8g + 7; ring row n < 3D is W row (n / D) * C + h * D + n % D
   const u32x4m rw = mq_rsrc(w, (uint32_t)(3 * Cf::C * ldw * 2));
   const uint32_t rsub = (uint32_t)lane >> 3, pch = (uint32_t)lane & 7;  // row in the piece, physical chunk
+  const u32x4m rt = mq_rsrc(LNF ? (const void*)tab : (const void*)w, LNF ? 8u * C2::TAB_BYTES : 0u);
   auto issue = [&](int t) {
     const int h = t / Cf::NCH, kc = t % Cf::NCH;
     const uint32_t slot = lds0 + (uint32_t)(t % MQ2_S) * C2::W_BYTES;
+    if (LNF && kc == 0)  // head h's table: this wave's KiB, with the head's first chunk
+      mq_dma(rt, lds0 + tab0 + (uint32_t)(h & 1) * C2::TAB_BYTES + (uint32_t)wave * 1024,
+             (uint32_t)h * C2::TAB_BYTES + (uint32_t)wave * 1024 + (uint32_t)lane * 16);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int g = 2 * wave + i;
@@ -174,6 +203,31 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
 #pragma unroll
     for (int kk = 0; kk < Cf::C / 32; ++kk) xf[pw][kk] = __builtin_bit_cast(bf16x8, *(const u32x4*)(xr + 32 * kk));
   }
+  // LNF: each token row's mean and rstd (lane (fr, fq) holds row fr's channels 32 kk + 8 fq ..):
+  // ones·x gives the row sum in every entry, x·x^T the Gram block whose diagonal (fr, fr) sits in
+  // lane fr + 16 (fr >> 2), register fr & 3
+  float nmean[PW], rstd[PW];
+#pragma unroll
+  for (int pw = 0; pw < PW; ++pw) {
+    nmean[pw] = 0.f;
+    rstd[pw] = 1.f;
+    if constexpr (LNF) {
+      const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
+      f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, gacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < Cf::C / 32; ++kk) {
+        sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, xf[pw][kk], sacc, 0, 0, 0);
+        gacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[pw][kk], xf[pw][kk], gacc, 0, 0, 0);
+      }
+      const int j3 = fr & 3;
+      const float gd = j3 == 0 ? gacc[0] : j3 == 1 ? gacc[1] : j3 == 2 ? gacc[2] : gacc[3];
+      const float sxx = __shfl(gd, fr + 16 * (fr >> 2), 64);
+      constexpr float RK = 1.0f / (float)Cf::C;
+      const float mean = sacc[0] * RK;
+      rstd[pw] = rsqrtf(fmaxf(fmaf(sxx, RK, -mean * mean), 0.f) + eps);
+      nmean[pw] = -mean;
+    }
+  }
 
   const bool unitc = c == 1.0f;
   const int vtr = (4 * fq + (fr >> 2)) * Cf::VS + 4 * (fr & 3);  // tr-read lane offset (temporal_mfma_kernel)
@@ -188,7 +242,11 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
     const int t = h * Cf::NCH + kc;
     // this wave's pieces of chunk t landed: the younger ones are chunks t+1 .. min(t+S-2, T-1)
     const int ahead = (T - 1 - t) < (MQ2_S - 2) ? (T - 1 - t) : (MQ2_S - 2);
-    if (ahead >= 4) mq_wait_vm<8>();
+    if constexpr (LNF) {  // + one table piece for every head-first chunk among them
+      int younger = 2 * ahead;
+      for (int u = t + 1; u <= t + ahead; ++u) younger += (u % Cf::NCH) == 0;
+      mq_wait_vm_rt(younger);
+    } else if (ahead >= 4) mq_wait_vm<8>();
     else if (ahead == 3) mq_wait_vm<6>();
     else if (ahead == 2) mq_wait_vm<4>();
     else if (ahead == 1) mq_wait_vm<2>();
@@ -238,7 +296,16 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
         if (ch < 3 * D) {
           const int part = ch / D, cd = ch - part * D;
           bf16_t* dst = part == 0 ? q_s + fr * Cf::DPAD + cd : (part == 1 ? k_s + fr * Cf::DPAD + cd : v_s + fr * Cf::VS + cd);
-          *(uint2*)dst = make_uint2(pack2(acc[pw][a][0], acc[pw][a][1]), pack2(acc[pw][a][2], acc[pw][a][3]));
+          f32x4 v = acc[pw][a];
+          if constexpr (LNF) {
+            const float* tb = (const float*)(lds2 + tab0 + (h & 1) * C2::TAB_BYTES);
+            const float4 sv = *(const float4*)(tb + ch), pv = *(const float4*)(tb + 3 * D + fr * 3 * D + ch);
+            v[0] = fmaf(rstd[pw], fmaf(nmean[pw], sv.x, v[0]), pv.x);
+            v[1] = fmaf(rstd[pw], fmaf(nmean[pw], sv.y, v[1]), pv.y);
+            v[2] = fmaf(rstd[pw], fmaf(nmean[pw], sv.z, v[2]), pv.z);
+            v[3] = fmaf(rstd[pw], fmaf(nmean[pw], sv.w, v[3]), pv.w);
+          }
+          *(uint2*)dst = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         }
         acc[pw][a] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
@@ -293,47 +360,67 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
-extern "C" int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* wqkv, int64_t ldw, void* o,
-                                       int64_t ldo, int64_t batch, int32_t frames, int64_t positions,
-                                       int32_t heads, int32_t d, float scale, vd_stream_t stream) {
-  VD_CHECK_ARG(x && wqkv && o && al16(x) && al16(wqkv) && ((uintptr_t)o & 7) == 0);
-  VD_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldo % 4 == 0 && batch > 0 && positions > 0);
-  if (frames != MF || heads != 8 || d != 40) return VD_EUNSUPPORTED;
-  using Cf = MqCfg<40>;
-  VD_CHECK_ARG(ldx >= Cf::C && ldw >= Cf::C && ldo >= Cf::C);
-  const int64_t nwg = batch * ((positions + Cf::P - 1) / Cf::P);
-  VD_CHECK_ARG(nwg < 0x7fffffff && batch * MF * positions < 0x7fffffff);
-  // one workgroup per CU: below one round of the chip (v2; two rounds for v1) the unfused GEMM +
-  // attention is faster (tools/motion_qkv_bench.py: 2-frame rank, 128 workgroups: v2 39.1 vs
-  // unfused 34.8 us; 4-frame rank, 256: v2 42.4 vs 56.8 us; the full step, 1024: v2 157 vs 250)
+namespace {
+// the shapes the fused kernel takes: frames 16, 8 heads, d 40, and at least one round of the chip
+// (one workgroup per CU: below it the unfused GEMM + attention is faster — tools/motion_qkv_bench.py:
+// 2-frame rank, 128 workgroups: v2 39.1 vs unfused 34.8 us; 4-frame rank, 256: v2 42.4 vs 56.8 us;
+// the full step, 1024: v2 157 vs 250)
+bool mq_takes(int64_t batch, int32_t frames, int64_t positions, int32_t heads, int32_t d) {
+  if (frames != MF || heads != 8 || d != 40 || batch <= 0 || positions <= 0) return false;
+  const int64_t nwg = batch * ((positions + MqCfg<40>::P - 1) / MqCfg<40>::P);
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess &&
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
-  if (nwg < (int64_t)cus) return VD_EUNSUPPORTED;
-  {
-    using C2 = Mq2Cfg<40>;
-    static bool attr2_set = false;
-    if (!attr2_set) {
-      if (hipFuncSetAttribute((const void*)motion_qkv_attn2_kernel<40, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              C2::LDS_BYTES) != hipSuccess ||
-          hipFuncSetAttribute((const void*)motion_qkv_attn2_kernel<40, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              C2::LDS_BYTES) != hipSuccess)
-        return vd_launch_status();
-      attr2_set = true;
-    }
-    // two positions per wave where that still gives one round of the chip (156 -> 128 us per
-    // level-1 layer, profiles/r03s_motion_pw2.txt)
-    const int64_t nwg2 = batch * ((positions + 2 * Cf::P - 1) / (2 * Cf::P));
-    if (nwg2 >= (int64_t)cus) {
-      hipLaunchKernelGGL((motion_qkv_attn2_kernel<40, 2>), dim3((unsigned)nwg2), dim3(Cf::NT), C2::LDS_BYTES,
-                         (hipStream_t)stream, (const bf16_t*)x, ldx, (const bf16_t*)wqkv, ldw, (bf16_t*)o, ldo, batch,
-                         positions, scale * 1.4426950408889634f);
+  return nwg >= (int64_t)cus;
+}
+
+template <int PW, bool LNF>
+int mq_launch(const void* x, int64_t ldx, const void* wqkv, int64_t ldw, void* o, int64_t ldo, int64_t batch,
+              int64_t positions, float scale, const float* tab, float eps, int64_t nwg, hipStream_t stream) {
+  using C2 = Mq2Cfg<40>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)motion_qkv_attn2_kernel<40, PW, LNF>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, C2::LDS_BYTES) != hipSuccess)
       return vd_launch_status();
-    }
-    hipLaunchKernelGGL((motion_qkv_attn2_kernel<40, 1>), dim3((unsigned)nwg), dim3(Cf::NT), C2::LDS_BYTES,
-                       (hipStream_t)stream, (const bf16_t*)x, ldx, (const bf16_t*)wqkv, ldw, (bf16_t*)o, ldo, batch,
-                       positions, scale * 1.4426950408889634f);
-    return vd_launch_status();
+    attr_set = true;
   }
+  hipLaunchKernelGGL((motion_qkv_attn2_kernel<40, PW, LNF>), dim3((unsigned)nwg), dim3(MqCfg<40>::NT), C2::LDS_BYTES,
+                     stream, (const bf16_t*)x, ldx, (const bf16_t*)wqkv, ldw, (bf16_t*)o, ldo, batch, positions,
+                     scale * 1.4426950408889634f, tab, eps);
+  return vd_launch_status();
+}
+}  // namespace
+
+extern "C" int vd_motion_qkv_attention_takes(int64_t batch, int32_t frames, int64_t positions, int32_t heads,
+                                             int32_t d) {
+  return mq_takes(batch, frames, positions, heads, d) ? 1 : 0;
+}
+
+extern "C" int vd_motion_qkv_attention(const void* x, int64_t ldx, const void* wqkv, int64_t ldw, void* o,
+                                       int64_t ldo, int64_t batch, int32_t frames, int64_t positions,
+                                       int32_t heads, int32_t d, float scale, const float* ln_fold_tab,
+                                       float ln_fold_eps, vd_stream_t stream) {
+  VD_CHECK_ARG(x && wqkv && o && al16(x) && al16(wqkv) && ((uintptr_t)o & 7) == 0);
+  VD_CHECK_ARG(ldx % 8 == 0 && ldw % 8 == 0 && ldo % 4 == 0 && batch > 0 && positions > 0);
+  if (ln_fold_tab) VD_CHECK_ARG(al16(ln_fold_tab) && ln_fold_eps >= 0.f);
+  if (!mq_takes(batch, frames, positions, heads, d)) return VD_EUNSUPPORTED;
+  using Cf = MqCfg<40>;
+  VD_CHECK_ARG(ldx >= Cf::C && ldw >= Cf::C && ldo >= Cf::C);
+  const int64_t nwg = batch * ((positions + Cf::P - 1) / Cf::P);
+  VD_CHECK_ARG(nwg < 0x7fffffff && batch * MF * positions < 0x7fffffff);
+  hipStream_t s = (hipStream_t)stream;
+  // two positions per wave where that still gives one round of the chip (156 -> 128 us per
+  // level-1 layer, profiles/r03s_motion_pw2.txt)
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  const int64_t nwg2 = batch * ((positions + 2 * Cf::P - 1) / (2 * Cf::P));
+  if (nwg2 >= (int64_t)cus)
+    return ln_fold_tab ? mq_launch<2, true>(x, ldx, wqkv, ldw, o, ldo, batch, positions, scale, ln_fold_tab, ln_fold_eps, nwg2, s)
+                       : mq_launch<2, false>(x, ldx, wqkv, ldw, o, ldo, batch, positions, scale, nullptr, 0.f, nwg2, s);
+  return ln_fold_tab ? mq_launch<1, true>(x, ldx, wqkv, ldw, o, ldo, batch, positions, scale, ln_fold_tab, ln_fold_eps, nwg, s)
+                     : mq_launch<1, false>(x, ldx, wqkv, ldw, o, ldo, batch, positions, scale, nullptr, 0.f, nwg, s);
 }

@@ -43,7 +43,9 @@ SIGNATURES = {
     "vd_temporal_attention": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
     "vd_temporal_attention_valu": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
     "vd_temporal_attention_kv": ([c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
-    "vd_motion_qkv_attention": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_vp], c_i32),
+    "vd_motion_qkv_attention": ([c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32,
+                                 c_vp, c_f32, c_vp], c_i32),
+    "vd_motion_qkv_attention_takes": ([c_i64, c_i32, c_i64, c_i32, c_i32], c_i32),
     "vd_temporal_attention_rope": ([c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, c_i32, c_i32, c_f32, c_f32, c_vp], c_i32),
     "vd_softmax_rows": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp], c_i32),
     "vd_frame_metrics": ([c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp], c_i32),

@@ -26,7 +26,7 @@ import torch.nn as nn
 
 from .. import ops
 from .layers import (Act, Attention, Conv2d, Downsample2D, Dropout, FeedForward, GroupNorm, LayerNorm, LnFold,
-                     Linear, pack_geglu, SiLU, SinusoidalPositionalEmbedding, Upsample2D, add, bf, f32, fmap_rows,
+                     Linear, MotionLnFold, pack_geglu, SiLU, SinusoidalPositionalEmbedding, Upsample2D, add, bf, f32, fmap_rows,
                      rows_fmap, token_rows)
 
 Transformer2DModelOutput = namedtuple("Transformer2DModelOutput", ["sample"])
@@ -144,16 +144,34 @@ class BasicTransformerBlock(nn.Module):
         for i, (nrm, w, b, pack, act) in cand.items():
             if ops.ln_fold_shape_ok(w.shape[0], w.shape[1], act=act):
                 self._fold[i] = (LnFold(nrm, w, b, pack=pack), act)
+        # the motion block's norm1 / norm2 + PE folded into the fused temporal QKV attention
+        # (level 1: 8 heads of d = 40, 16 frames)
+        self._mfold = {}
+        if self.pos_embed is not None and self.heads * self.dim_head == 320 and self.dim_head == 40:
+            c = self.attn1.dim_head ** -0.5 * math.log2(math.e)
+            for i, (nrm, attn) in ((1, (self.norm1, self.attn1)), (2, (self.norm2, self.attn2))):
+                w = torch.cat([attn.to_q.weight.float() * c, attn.to_k.weight.float(), attn.to_v.weight.float()], 0)
+                self._mfold[i] = MotionLnFold(nrm, w, self.pos_embed.pe[0], self.heads, self.dim_head)
+
+    def mfold(self, i, batch, frames, positions):
+        """norm i's MotionLnFold when the fused temporal QKV attention takes this shape, else None."""
+        f = getattr(self, "_mfold", {}).get(i)
+        if f is None or not self.fuse_qkv_attention or frames != MotionLnFold.FRAMES:
+            return None
+        return f if ops.motion_qkv_takes(batch, frames, positions, self.heads, self.dim_head) else None
 
     def fold(self, i, M):
         """norm i's LnFold when its consumer GEMM runs folded over M rows, else None."""
         f = getattr(self, "_fold", {}).get(i)
         return f[0] if f is not None and f[0].runs(M, f[1]) else None
 
-    def _out_norm(self, a, attn, i, h, **pe):
+    def _out_norm(self, a, attn, i, h, mshape=None, **pe):
         """h' = to_out(a) + h and norm i of it: (h', n), or (h', None) when norm i folds into
-        its consumer (the rows are then never normalised in memory)."""
-        if pe.get("pe") is None and self.fold(i, h.shape[0]) is not None:
+        its consumer (the rows are then never normalised in memory).  mshape = (batch, frames,
+        positions) of a temporal block: norm i (+ PE) may fold into the fused QKV attention."""
+        folded = (self.fold(i, h.shape[0]) is not None if pe.get("pe") is None
+                  else mshape is not None and self.mfold(i, *mshape) is not None)
+        if folded:
             return ops.gemm(a, attn._wo, bias=attn._bo, res=h), None
         return ops.gemm_ln(a, attn._wo, *self._nrm(i), bias=attn._bo, res=h, **pe)
 
@@ -193,19 +211,29 @@ class BasicTransformerBlock(nn.Module):
         C = h.shape[1]
         d = self.dim_head
         pe = self.pos_embed._pe
-        if n is None:
-            n = ops.layer_norm(h, *self._nrm(1), pe=pe, pe_div=positions, pe_period=frames)
+        mshape = (batch, frames, positions)
         for attn, i in ((self.attn1, 1), (self.attn2, 2)):
             # Q/K/V projection fused into the attention where the kernel takes the shape
-            # (level 1: 16 frames, d 40), else the QKV GEMM + the attention kernel
-            a = (ops.motion_qkv_attention(n, attn._wqkv, batch, frames, positions, self.heads, d,
-                                          scale=attn.attn_scale) if self.fuse_qkv_attention else None)
+            # (level 1: 16 frames, d 40), with norm i + PE folded in when the caller left the rows
+            # un-normalised; else the norm, the QKV GEMM and the attention kernel
+            mf = self.mfold(i, *mshape) if n is None else None
+            a = None
+            if mf is not None:
+                a = ops.motion_qkv_attention(h, mf.w, batch, frames, positions, self.heads, d,
+                                             scale=attn.attn_scale, ln_fold=(mf.tab, mf.eps))
+            elif self.fuse_qkv_attention:
+                if n is None:
+                    n = ops.layer_norm(h, *self._nrm(i), pe=pe, pe_div=positions, pe_period=frames)
+                a = ops.motion_qkv_attention(n, attn._wqkv, batch, frames, positions, self.heads, d,
+                                             scale=attn.attn_scale)
             if a is None:
+                if n is None:
+                    n = ops.layer_norm(h, *self._nrm(i), pe=pe, pe_div=positions, pe_period=frames)
                 qkv = ops.gemm(n, attn._wqkv)
                 a = ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch, frames,
                                            positions, self.heads, d, scale=attn.attn_scale)
             # norm2 (+ PE) after attn1, norm3 after attn2
-            h, n = self._out_norm(a, attn, i + 1, h, pe=pe if i == 1 else None, pe_div=positions,
+            h, n = self._out_norm(a, attn, i + 1, h, mshape=mshape, pe=pe if i == 1 else None, pe_div=positions,
                                   pe_period=frames)
         return self._ff(h, n)
 
@@ -315,8 +343,11 @@ class AnimateDiffTransformer3D(nn.Module):
                                 two_pass=False, n_split=Fl * ops.gn_splits_per_frame(hw),
                                 rev3=dist.send_perm(B, Fl, hw))
             recv = dist.exchange(hn)                                   # rows (f, b, j)
-            h, n = ops.gemm_ln(recv, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b, pe=blk.pos_embed._pe,
-                               pe_div=B * pl, pe_period=F)
+            if blk.mfold(1, 1, F, B * pl) is not None:  # norm1 + PE fold into the QKV attention
+                h, n = ops.gemm(recv, self.proj_in._w, bias=self.proj_in._b), None
+            else:
+                h, n = ops.gemm_ln(recv, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b, pe=blk.pos_embed._pe,
+                                   pe_div=B * pl, pe_period=F)
             h = blk.run_temporal(h, 1, F, B * pl, n=n)
             back = dist.exchange(h)                                    # rows (r', f_loc, b, j)
             out = ops.gemm(back, self.proj_out._w, bias=self.proj_out._b, res=x.t,
@@ -324,9 +355,12 @@ class AnimateDiffTransformer3D(nn.Module):
             return Act(out, x.n, x.h, x.w)
         hn = ops.group_norm(x.t, B, Fl * hw, self.groups, 1e-6, self.norm._g, self.norm._b, gather=gather,
                             two_pass=False, n_split=Fl * ops.gn_splits_per_frame(hw))
-        if dist is None:  # norm1 (+ PE by frame) fused into proj_in's epilogue
-            h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b, pe=blk.pos_embed._pe,
-                               pe_div=hw, pe_period=Fl)
+        if dist is None:  # norm1 (+ PE by frame) fused into proj_in's epilogue, or folded into the QKV attention
+            if blk.mfold(1, B, Fl, hw) is not None:
+                h, n = ops.gemm(hn, self.proj_in._w, bias=self.proj_in._b), None
+            else:
+                h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b, pe=blk.pos_embed._pe,
+                                   pe_div=hw, pe_period=Fl)
             h = blk.run_temporal(h, B, Fl, hw, n=n)
         else:
             h = ops.gemm(hn, self.proj_in._w, bias=self.proj_in._b)

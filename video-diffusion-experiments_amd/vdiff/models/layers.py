@@ -119,6 +119,31 @@ class LnFold:
         return ops.gemm(x, self.w, bias=self.b, act=act, ln_fold=(self.s, self.eps))
 
 
+class MotionLnFold:
+    """The motion block's norm1 / norm2 (+ the sinusoidal PE by frame) folded into the fused
+    temporal QKV attention (vd_motion_qkv_attention's ln_fold_tab): W' = W_qkv∘gamma in bf16 and
+    the [8 heads][2048] fp32 table — per head the 120 row sums of W' (q | k | v rows of the head)
+    and, per frame f < 16, W·(beta + pe[f]) of the same rows."""
+
+    FRAMES = 16
+
+    def __init__(self, norm: nn.LayerNorm, w: torch.Tensor, pe: torch.Tensor, heads: int, d: int):
+        C = heads * d
+        g = norm.weight.detach().double()
+        wd = w.detach().double()
+        self.w = (wd * g[None, :]).to(torch.bfloat16).contiguous()
+        s = self.w.double().sum(1)
+        p = (norm.bias.detach().double()[None, :] + pe[:self.FRAMES].detach().double().to(wd.device)) @ wd.T  # [16][3C]
+        tab = torch.zeros(heads, 2048, dtype=torch.float64, device=wd.device)
+        cols = torch.arange(3 * d, device=wd.device)
+        for h in range(heads):
+            n = (cols // d) * C + h * d + cols % d
+            tab[h, :3 * d] = s[n]
+            tab[h, 3 * d:3 * d * (1 + self.FRAMES)] = p[:, n].reshape(-1)
+        self.tab = tab.float().contiguous()
+        self.eps = float(norm.eps)
+
+
 # ------------------------------------------------------------------ layout helpers
 def to_bf16_cuda(x: torch.Tensor) -> torch.Tensor:
     if not x.is_cuda:

@@ -399,17 +399,33 @@ def temporal_attention(q, k, v, batch, frames, positions, heads, d, scale=None, 
     return out
 
 
-def motion_qkv_attention(x, wqkv, batch, frames, positions, heads, d, scale=None, out=None):
+def motion_qkv_takes(batch, frames, positions, heads, d):
+    """Whether vd_motion_qkv_attention takes this shape (vd_motion_qkv_attention_takes; no launch).
+    Under gemm_plan(plan_div=N) the question is asked for one of N frame shards (batch 1, the
+    positions divided by N), so an unsharded replay folds the motion norms exactly where a shard would."""
+    if _PLAN.plan_div > 1 and (batch * positions) % _PLAN.plan_div == 0:
+        batch, positions = 1, batch * positions // _PLAN.plan_div
+    return bool(lib().vd_motion_qkv_attention_takes(batch, frames, positions, heads, d))
+
+
+def motion_qkv_attention(x, wqkv, batch, frames, positions, heads, d, scale=None, out=None, ln_fold=None):
     """Temporal attention over frames with the fused Q/K/V projection folded in
     (vd_motion_qkv_attention): x = normed rows (b, f, p), wqkv = [3C][C].  Returns None where
-    the fused kernel does not take the shape (the caller runs gemm + temporal_attention)."""
+    the fused kernel does not take the shape (the caller runs gemm + temporal_attention).
+    ln_fold = (table, eps): x holds the UN-normalised rows and the block's LayerNorm + PE are
+    folded in (wqkv = W∘gamma; vdiff.models.blocks.MotionLnFold builds the table)."""
     _dev(x, wqkv, out)
     C = heads * d
     if out is None:
         out = torch.empty(x.shape[0], C, device=x.device, dtype=BF16)
     scale = d ** -0.5 if scale is None else scale
+    tab, eps = (None, 0.0) if ln_fold is None else ln_fold
+    if tab is not None:
+        _dev(tab)
+        if tab.dtype != torch.float32 or not tab.is_contiguous() or tab.numel() != 8 * 2048:
+            raise ValueError("ln_fold table must be a contiguous fp32 [8][2048]")
     rc = lib().vd_motion_qkv_attention(_p(x), _rows(x), _p(wqkv), _rows(wqkv), _p(out), _rows(out), batch, frames,
-                                       positions, heads, d, scale, _stream())
+                                       positions, heads, d, scale, _p(tab), float(eps), _stream())
     if rc == VD_EUNSUPPORTED:
         return None
     check(rc, "vd_motion_qkv_attention")
