@@ -44,8 +44,8 @@ def device_rounder(unet):
         b = blocks.get((C, motion))
         if b is None:
             return False
-        if motion and i < 3:  # norm1 / norm2 + PE fold into the fused QKV attention
-            return b.mfold(i, 1, frames, rows // frames) is not None
+        if motion and i < 3:  # norm1 / norm2 + PE fold into the fused QKV attention or the QKV GEMM
+            return b.temporal_fold(i, 1, frames, rows // frames) is not None
         return b.fold(i, rows) is not None
 
     dev.device_attention = True

@@ -11,8 +11,10 @@ import math
 import pytest
 import torch
 import torch.nn.functional as F
+import torch.nn.functional as F_
 
 from vdiff import ops
+from vdiff._lib import GemmDesc
 from vdiff.dist import block_transpose_reference, rev3_reference
 from vdiff.models.layers import LnFold, pack_conv3x3, pack_geglu
 
@@ -243,17 +245,24 @@ def test_gemm_v8_strided_operands(cuda):
     close_bf16(outs[0][:, 160:], a.float() @ w.float().T + bias + res.float())
 
 
-@pytest.mark.parametrize("M,N,kind,offset", [(16384, 960, "plain", 0.0), (16384 + 37, 320, "plain", 30.0),
-                                              (65536 + 16 * 5 + 3, 2560, "geglu", 0.0), (20000, 2560, "geglu", 30.0),
-                                              (131072, 960, "plain", 0.0)])
-def test_gemm_ln_fold(cuda, M, N, kind, offset):
-    """vd_gemm_desc.ln_fold_s (round 5): Linear(LayerNorm(x)) as ONE v8 GEMM over the un-normalised
+@pytest.mark.parametrize("M,N,K,kind,offset,kern", [
+    (16384, 960, 320, "plain", 0.0, 8), (16384 + 37, 320, 320, "plain", 30.0, 8),
+    (65536 + 16 * 5 + 3, 2560, 320, "geglu", 0.0, 8), (20000, 2560, 320, "geglu", 30.0, 8),
+    (131072, 960, 320, "plain", 0.0, 8),
+    # the unsplit v6 of a frame shard's small M (L2-L4 at 4 images per rank)
+    (1024, 3840, 1280, "plain", 0.0, 6), (4096 + 37, 640, 640, "plain", 30.0, 6),
+    (256, 10240, 1280, "geglu", 0.0, 6), (700, 2560, 640, "geglu", 30.0, 6), (256, 1280, 1280, "plain", 0.0, 6),
+    # the unsplit persistent v2 (BN 160 with the odd column block, BN 128 for GEGLU)
+    (4096, 1920, 640, "plain", 0.0, 2), (32768 + 37, 640, 640, "plain", 30.0, 2),
+    (4096 + 37, 5120, 640, "geglu", 30.0, 2), (1024, 10240, 1280, "geglu", 0.0, 2)])
+def test_gemm_ln_fold(cuda, M, N, K, kind, offset, kern):
+    """vd_gemm_desc.ln_fold_s (round 5): Linear(LayerNorm(x)) as ONE GEMM over the un-normalised
     rows (LnFold: W' = W∘gamma in bf16, s = its row sums, b' = b + W·beta; each row's mean / rstd
-    from the A fragments by two extra MFMAs per k-step).  Within bf16 output rounding of fp64 of the
-    same folded arithmetic; within the unfolded path's own rounding (bf16 normalised rows) of fp64
-    LayerNorm -> Linear and of the unfolded device path (vd_layernorm + GEMM); rows whose mean is 30
-    std exercise the fp32 one-pass variance; ragged M (partial row block, unequal XCD ranges)."""
-    K = 320
+    from the A fragments — two extra MFMAs per k-step on v8, dot-2 VALU on v6).  Within bf16 output
+    rounding of fp64 of the same folded arithmetic; within the unfolded path's own rounding (bf16
+    normalised rows) of fp64 LayerNorm -> Linear and of the unfolded device path (vd_layernorm +
+    GEMM); rows whose mean is 30 std exercise the fp32 one-pass variance; ragged M (partial row
+    block, unequal XCD ranges / a partial 64-row tile)."""
     g = torch.Generator(device=cuda).manual_seed(0)
     x = bf(1.7 * (torch.randn(M, K, device=cuda, generator=g) + offset
                   + 0.5 * torch.randn(M, 1, device=cuda, generator=g)))
@@ -267,6 +276,10 @@ def test_gemm_ln_fold(cuda, M, N, kind, offset):
     act = ops.ACT_GEGLU if geglu else ops.ACT_NONE
     fold = LnFold(norm, w, b, pack=pack_geglu if geglu else None)
     assert fold.runs(M, act), "the plan does not fold this shape"
+    nout = N // 2 if geglu else N
+    assert ops.gemm_plan_of(GemmDesc(a0=256, lda0=K, k0=K, a_mode=0, w=fold.w.data_ptr(), ldw=K, M=M, N=N, K=K,
+                                     bias=256, act=act, out=256, ldc=nout, ln_fold_s=fold.s.data_ptr(),
+                                     ln_fold_eps=1e-5)) == (kern, 1)
     got = fold.gemm(x, act=act)
 
     def epi(y):  # packed GEGLU pairs -> h * gelu(g)
@@ -295,11 +308,47 @@ def test_gemm_ln_fold(cuda, M, N, kind, offset):
     assert e_ref < 1.5 * e_unf + 1e-3  # no worse than the unfolded path's own bf16 rounding
 
 
-def test_gemm_ln_fold_refused_off_v8(cuda):
-    """A fold no kernel takes is refused (VD_EUNSUPPORTED), never run on another kernel."""
-    K, M = 320, 1024
+@pytest.mark.parametrize("B,F,P,C,kern", [(2, 16, 128, 640, 2), (2, 16, 32, 1280, 6), (2, 16, 8, 1280, 6),
+                                          (1, 16, 37, 1280, 6)])
+def test_gemm_ln_fold_pe_rowbias(cuda, B, F, P, C, kern):
+    """The motion block's norm + sinusoidal PE folded into its levels-2-4 QKV GEMM (LnFold(pe=...)):
+    rows (video, frame, position), PE[frame] added after the norm = the row bias W·pe[(m / P) % F]
+    after the fold (v2 at the rank's level 2, v6 at levels 3-4).  Within bf16 output rounding of
+    fp64 LayerNorm + PE -> Linear, no worse than the unfolded device path."""
+    g = torch.Generator(device=cuda).manual_seed(1)
+    M, N, K = B * F * P, 3 * C, C
+    x = bf(1.3 * torch.randn(M, K, device=cuda, generator=g) + 0.4 * torch.randn(M, 1, device=cuda, generator=g))
     norm = torch.nn.LayerNorm(K).to(cuda)
-    fold = LnFold(norm, torch.randn(320, K, device=cuda) * K ** -0.5)
+    with torch.no_grad():
+        norm.weight.copy_(1 + 0.2 * torch.randn(K, device=cuda, generator=g))
+        norm.bias.copy_(0.1 * torch.randn(K, device=cuda, generator=g))
+    pe = 0.5 * torch.randn(32, K, device=cuda, generator=g)
+    w = torch.randn(N, K, device=cuda, generator=g) * K ** -0.5
+    fold = LnFold(norm, w, pe=pe)
+    assert fold.runs(M), "the plan does not fold this shape"
+    assert ops.gemm_plan_of(GemmDesc(a0=256, lda0=K, k0=K, a_mode=0, w=fold.w.data_ptr(), ldw=K, M=M, N=N, K=K,
+                                     bias=256, rowbias=256, ld_rb=N, rb_div=P, out=256, ldc=N,
+                                     ln_fold_s=fold.s.data_ptr(), ln_fold_eps=1e-5)) == (kern, 1)
+    got = fold.gemm(x, pe_div=P, pe_period=F)
+    xd = x.double()
+    frame = (torch.arange(M, device=cuda) // P) % F
+    ln = F_.layer_norm(xd, (K,), norm.weight.double(), norm.bias.double(), norm.eps) + pe.double()[frame]
+    ref = ln @ w.double().T
+    unfolded = ops.gemm(ops.layer_norm(x, norm.weight.detach().float().contiguous(),
+                                       norm.bias.detach().float().contiguous(), pe=pe.float().contiguous(),
+                                       pe_div=P, pe_period=F), bf(w).contiguous())
+    e_ref = ((got.double() - ref).norm() / ref.norm()).item()
+    e_unf = ((unfolded.double() - ref).norm() / ref.norm()).item()
+    print(f"B={B} F={F} P={P} C={C}: folded vs fp64 {e_ref:.5f}, unfolded vs fp64 {e_unf:.5f}")
+    assert e_ref < 5e-3 and e_ref < 1.5 * e_unf + 1e-3
+
+
+def test_gemm_ln_fold_refused_off_plan(cuda):
+    """A fold no kernel takes (here the v3 plan of M 32768 x N 1920 x K 640) is refused
+    (VD_EUNSUPPORTED), never run on another kernel."""
+    K, M = 640, 32768
+    norm = torch.nn.LayerNorm(K).to(cuda)
+    fold = LnFold(norm, torch.randn(1920, K, device=cuda) * K ** -0.5)
     assert not fold.runs(M)
     with pytest.raises(Exception, match="unsupported|1001"):
         fold.gemm(rnd(M, K))

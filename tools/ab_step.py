@@ -11,7 +11,8 @@ Switches:
   ln_fold    LayerNorm folded into its consuming v8 GEMM (BasicTransformerBlock._fold; round 5)
              against the unfolded norm -> GEMM;
   cfg_dedup  conv_in + down_blocks[0].resnets[0] once for both CFG halves (DenoiseLoop.cfg_dedup);
-  mfold      the motion block's norm1 / norm2 + PE folded into the fused QKV attention (_mfold)."""
+  mfold      the motion block's norm1 / norm2 + PE folded into the fused QKV attention (_mfold);
+  pfold      the same norms + PE folded into the levels-2-4 QKV GEMM, PE as a row bias (_pfold)."""
 from __future__ import annotations
 
 import argparse
@@ -53,7 +54,16 @@ def set_mfold(unet, on, saved):
             m._mfold = saved[key] if on else {}
 
 
-SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup, "mfold": set_mfold}
+def set_pfold(unet, on, saved):
+    for m in unet.modules():
+        if isinstance(m, BasicTransformerBlock):
+            key = ("p", id(m))
+            if key not in saved:
+                saved[key] = getattr(m, "_pfold", {})
+            m._pfold = saved[key] if on else {}
+
+
+SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup, "mfold": set_mfold, "pfold": set_pfold}
 
 
 def main():

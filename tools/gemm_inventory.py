@@ -64,17 +64,21 @@ def main():
         e1.record()
         e1.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / args.reps
-        kind = KIND[d.a_mode] + ("+res" if d.res else "") + ACT.get(d.act, "") + ("+ln" if d.ln_out else "")
-        key = (kind, d.M, d.N, d.K)
+        kind = KIND[d.a_mode] + ("+res" if d.res else "") + ACT.get(d.act, "") + ("+ln" if d.ln_out else "") + \
+            ("+fold" if d.ln_fold_s else "")
+        kv, sp = C.c_int32(), C.c_int32()
+        check(lib().vd_gemm_plan(C.byref(d), C.byref(kv), C.byref(sp)), "vd_gemm_plan")
+        key = (kind, d.M, d.N, d.K, f"v{kv.value}" + (f"/s{sp.value}" if sp.value > 1 else ""))
         a = agg[key]
         a[0] += 1
         a[1] += us
         a[2] += 2.0 * d.M * d.N * d.K
     tot = sum(v[1] for v in agg.values())
     print(f"{len(calls)} vd_gemm calls, {tot / 1e3:.2f} ms per forward (launch-by-launch), frames {args.frames}")
-    print(f"{'kind':18s} {'M':>7s} {'N':>5s} {'K':>6s} {'calls':>5s} {'us/call':>8s} {'ms/step':>8s} {'TF/s':>7s}")
+    print(f"{'kind':18s} {'M':>7s} {'N':>5s} {'K':>6s} {'plan':>7s} {'calls':>5s} {'us/call':>8s} {'ms/step':>8s} "
+          f"{'TF/s':>7s}")
     for key, (n, us, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-        print(f"{key[0]:18s} {key[1]:7d} {key[2]:5d} {key[3]:6d} {n:5d} {us / n:8.1f} {us / 1e3:8.3f} "
+        print(f"{key[0]:18s} {key[1]:7d} {key[2]:5d} {key[3]:6d} {key[4]:>7s} {n:5d} {us / n:8.1f} {us / 1e3:8.3f} "
               f"{fl / (us * 1e-6) / 1e12:7.1f}")
 
 

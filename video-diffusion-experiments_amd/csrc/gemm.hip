@@ -466,7 +466,51 @@ __device__ unsigned long long g2_diag[4096 * 8 * 6];
   } while (0)
 #endif
 
-template <int BN, int MODE>
+// Σ over a bf16x8 fragment of x and of x² (fp32 dot-2 accumulation; every bf16 product is exact)
+__device__ __forceinline__ void frag_stats(const bf16x8& f, float& s, float& q) {
+  const u32x4 u = __builtin_bit_cast(u32x4, f);
+  const bf16x2_t one2 = __builtin_bit_cast(bf16x2_t, 0x3F803F80u);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bf16x2_t p = __builtin_bit_cast(bf16x2_t, u[j]);
+    s = __builtin_amdgcn_fdot2_f32_bf16(p, one2, s, false);
+    q = __builtin_amdgcn_fdot2_f32_bf16(p, p, q, false);
+  }
+}
+
+// acc[a][b] -> rstd_b·(acc − mean_b·s[n]) for the lane's rows from its per-k-quarter sums (LNF)
+template <int MB, int NB>
+__device__ __forceinline__ void ln_fold_acc(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], float (&ls)[MB],
+                                            float (&lq)[MB], int nbase, int lane, int nodd = -1) {
+  const int fq = lane >> 4;
+  const float rk = 1.0f / (float)d.K;
+  float nmean[MB], rstd[MB];
+#pragma unroll
+  for (int b = 0; b < MB; ++b) {
+    float s = ls[b], q = lq[b];
+    s += __shfl_xor(s, 16, 64);
+    q += __shfl_xor(q, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    q += __shfl_xor(q, 32, 64);
+    const float mean = s * rk;
+    rstd[b] = rsqrtf(fmaxf(fmaf(q, rk, -mean * mean), 0.f) + d.ln_fold_eps);
+    nmean[b] = -mean;
+  }
+#pragma unroll
+  for (int a = 0; a < NB; ++a) {
+    const int n = (nodd >= 0 && a == NB - 1 ? nodd : nbase + a * 16) + 4 * fq;  // gemm_epilogue's columns
+    const float4 t = n < (int)d.N ? *(const float4*)(d.ln_fold_s + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float sv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int b = 0; b < MB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[a][b][j] = rstd[b] * fmaf(nmean[b], sv[j], acc[a][b][j]);
+  }
+}
+
+// LNF (round 5): the folded LayerNorm on v2 as on v6 (dense, unsplit units only — the plan): the
+// row statistics from dot-2 VALU on the X fragments of each k-step, reset with the accumulators
+template <int BN, int MODE, bool LNF = false>
 __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                          uint32_t a1_bytes, uint32_t w_bytes,
                                                          int split) {
@@ -641,6 +685,7 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
   int cu = u_begin, ckt, ckt1;
   unit_kr(cu, ckt, ckt1);
   const int fr = lane & 15, fq = lane >> 4;
+  float ls[C::MB] = {}, lq[C::MB] = {};  // LNF: this lane's k-quarter sums of Σx, Σx² per row block
   int stage = 0;
 #ifdef VD_G2_STAMPS
   unsigned long long st0, st1, st2, st3, st4, sw = 0, sb = 0, sm = 0, stl = 0, tbeg;
@@ -694,6 +739,12 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
         }
         __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
       }
+      if constexpr (LNF) {
+#pragma unroll
+        for (int ks = 0; ks < BK / 32; ++ks)
+#pragma unroll
+          for (int b = 0; b < C::MB; ++b) frag_stats(xf[ks][b], ls[b], lq[b]);
+      }
     }
 #ifdef VD_G2_STAMPS
     G2_STAMP(st3);
@@ -702,6 +753,11 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
       const int tile = cu / split, sp = cu % split;
       const int64_t m0 = (int64_t)(tile / tiles_n) * G2_BM, n0 = (int64_t)(tile % tiles_n) * BN;
       if (split == 1) {
+        if constexpr (LNF) {
+          ln_fold_acc<C::MB, C::NB>(d, acc, ls, lq, (int)n0 + wcb, lane, ODDMAP ? (int)n0 + wodd : -1);
+#pragma unroll
+          for (int b = 0; b < C::MB; ++b) ls[b] = lq[b] = 0.f;
+        }
         gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::MB * 16, (int)n0 + wcb, lane,
                                     ODDMAP ? (int)n0 + wodd : -1);
       } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
@@ -1591,10 +1647,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
 // The ring depth S is picked per launch: 3 stages (48 KiB, three workgroups per CU) when
 // the grid oversubscribes the CUs, 4 / 6 stages (2 / 1 per CU) on small grids, where
 // each workgroup's k-loop is latency-bound and more tiles in flight pay directly.
+// LNF (round 5, vd_gemm_desc.ln_fold_s; dense, unsplit): the LayerNorm of A's rows folded in, as
+// v8's — but here the row statistics come from VALU dot products on the X fragments the wave already
+// holds (v_dot2_f32_bf16: 2 x 4 per fragment, Σx against ones and Σx² against itself), which fill the
+// gaps of a loop that runs far below the MFMA pipe's rate at these M; the lane's four k-quarters are
+// summed by two cross-lane adds after the loop, and the accumulators become rstd·(acc − mean·s[n])
+// before the common epilogue adds b' (the folded bias).
 constexpr int G6_BM = 64, G6_BN = 64, G6_NT = 256;
 constexpr int G6_A = G6_BM * BK * 2, G6_W = G6_BN * BK * 2, G6_STAGE = G6_A + G6_W;  // 8 + 8 KiB
 
-template <int MODE, int G6_S>  // all fragment reads of a K-tile ahead of its MFMAs (as gemm2)
+template <int MODE, int G6_S, bool LNF = false>  // all fragment reads of a K-tile ahead of its MFMAs (as gemm2)
 __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void gemm6_kernel(
     const vd_gemm_desc d, uint32_t a0_bytes, uint32_t a1_bytes, uint32_t w_bytes, int split) {
   constexpr int MB = 2, NB = 2;
@@ -1696,6 +1758,7 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
   for (int j = 0; j < G6_S - 1; ++j)
     if (j < nk) issue(j);
   const int fr = lane & 15, fq = lane >> 4;
+  float ls[MB] = {}, lq[MB] = {};  // LNF: this lane's k-quarter sums of Σx, Σx² per row block
   int stage = 0;
   for (int it = 0; it < nk; ++it) {
     // k-steps it+1 .. it+S-2 (4 pieces each) may stay in flight
@@ -1728,10 +1791,21 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
 #pragma unroll
           for (int b = 0; b < MB; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][a], xf[ks][b], acc[a][b], 0, 0, 0);
+      if constexpr (LNF) {
+#pragma unroll
+        for (int ks = 0; ks < BK / 32; ++ks)
+#pragma unroll
+          for (int b = 0; b < MB; ++b) frag_stats(xf[ks][b], ls[b], lq[b]);
+      }
     }
     stage = stage == G6_S - 1 ? 0 : stage + 1;
   }
   const int mbase = (int)m0 + wm * 32, nbase = (int)n0 + wn * 32;
+  if constexpr (LNF) {  // dense, unsplit (plan): the whole row went through this wave
+    ln_fold_acc<MB, NB>(d, acc, ls, lq, nbase, lane);
+    gemm_epilogue<MB, NB>(d, acc, mbase, nbase, lane);
+    return;
+  }
   if (split == 1) {
     if (d.rmap_inner)
       gemm_epilogue<MB, NB, true>(d, acc, mbase, nbase, lane);
@@ -2157,7 +2231,13 @@ int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   const int64_t grid = (units + rounds - 1) / rounds;
   if (d.a_mode == VD_A_CONV3X3)
     hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
-  else
+  else if constexpr (BN != 32) {
+    if (d.ln_fold_s)
+      hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE, true>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb,
+                         split);
+    else
+      hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
+  } else
     hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
   int rc = vd_launch_status();
   if (rc != VD_OK || split == 1) return rc;
@@ -2213,7 +2293,9 @@ int launch6(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   const int64_t wgs = tiles * split;
   const dim3 grid((unsigned)wgs);
 #define G6_LAUNCH(S)                                                                                    \
-  if (d.a_mode == VD_A_CONV3X3)                                                                         \
+  if (d.ln_fold_s)                                                                                      \
+    hipLaunchKernelGGL((gemm6_kernel<VD_A_DENSE, S, true>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split); \
+  else if (d.a_mode == VD_A_CONV3X3)                                                                    \
     hipLaunchKernelGGL((gemm6_kernel<VD_A_CONV3X3, S>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split); \
   else                                                                                                  \
     hipLaunchKernelGGL((gemm6_kernel<VD_A_DENSE, S>), grid, dim3(G6_NT), 0, s, d, a0b, a1b, wb, split);
@@ -2344,15 +2426,20 @@ Plan plan_core(const vd_gemm_desc& d) {
   // profiles/r04_gemm_v8.txt)
   const bool v8auto = v8ok && M >= 16384;
   if (path == 8 && !v8ok) path = 0;  // forced v8 on a shape it does not take: the product plan
-  // a folded LayerNorm (ln_fold_s) runs on v8 wherever v8 would run the plain GEMM (or is forced);
-  // no other kernel carries it: ver 0 = not runnable, the caller takes the unfolded form
+  // a folded LayerNorm (ln_fold_s) runs on v8 wherever v8 would run the plain GEMM (or is forced),
+  // and on v2 / v6 wherever the plain GEMM's plan is an unsplit v2 / v6 (levels 2-4, the small M
+  // of a frame-sharded rank); no other kernel carries it: ver 0 = not runnable, the caller takes the unfolded form
   if (d.ln_fold_s) {
     if ((v8auto && path == 0) || (v8ok && path == 8)) {
       p.ver = 8;
       p.bn = G8_BN;
-    } else {
-      p.ver = 0;
+      return p;
     }
+    vd_gemm_desc g = d;
+    g.ln_fold_s = nullptr;
+    const Plan q = plan_core(g);
+    if ((q.ver == 6 || (q.ver == 2 && q.bn != 32)) && q.split == 1 && d.a_mode == VD_A_DENSE) return q;
+    p.ver = 0;
     return p;
   }
   // an output-row map (rmap; no ln_out, GEGLU or row bias — checked) is carried by v8 (with a
@@ -2497,11 +2584,11 @@ Plan plan_core(const vd_gemm_desc& d) {
   return p;
 }
 
-// a folded LayerNorm only ever runs on v8: every other outcome of the plan (its early exits
-// included) is "no kernel"
+// a folded LayerNorm only ever runs on v8 or an unsplit v2 / v6: every other outcome of the plan (its
+// early exits included) is "no kernel"
 Plan plan(const vd_gemm_desc& d) {
   Plan p = plan_core(d);
-  if (d.ln_fold_s && p.ver != 8) {
+  if (d.ln_fold_s && p.ver != 8 && !((p.ver == 6 || (p.ver == 2 && p.bn != 32)) && p.split == 1)) {
     p.ver = 0;
     p.split = 1;
     p.ws_bytes = 0;
@@ -2581,7 +2668,7 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
     VD_CHECK_ARG(Rev3::ok(d.M, d.rmap_n1, d.rmap_n2, d.rmap_inner) && !d.ln_out && !d.rowbias &&
                  d.act != VD_ACT_GEGLU);
   if (d.ln_fold_s) {
-    VD_CHECK_ARG(al16(d.ln_fold_s) && d.ln_fold_eps >= 0.f && !d.res && !d.rowbias && !d.ln_out && !d.rmap_inner &&
+    VD_CHECK_ARG(al16(d.ln_fold_s) && d.ln_fold_eps >= 0.f && !d.res && !d.ln_out && !d.rmap_inner &&
                  d.a_mode == VD_A_DENSE && !d.a1 && d.k0 == d.K);
   }
   if (d.ln_out) {

@@ -152,6 +152,28 @@ class BasicTransformerBlock(nn.Module):
             for i, (nrm, attn) in ((1, (self.norm1, self.attn1)), (2, (self.norm2, self.attn2))):
                 w = torch.cat([attn.to_q.weight.float() * c, attn.to_k.weight.float(), attn.to_v.weight.float()], 0)
                 self._mfold[i] = MotionLnFold(nrm, w, self.pos_embed.pe[0], self.heads, self.dim_head)
+        # elsewhere (levels 2-4: d = 80 / 160, no fused QKV attention) norm1 / norm2 + PE fold into
+        # the QKV GEMM, the PE as the row bias W·pe[frame] (LnFold(pe=...), v2 / v6 plans)
+        self._pfold = {}
+        if self.pos_embed is not None:
+            c = self.attn1.dim_head ** -0.5 * math.log2(math.e)
+            for i, (nrm, attn) in ((1, (self.norm1, self.attn1)), (2, (self.norm2, self.attn2))):
+                w = torch.cat([attn.to_q.weight.float() * c, attn.to_k.weight.float(), attn.to_v.weight.float()], 0)
+                if ops.ln_fold_shape_ok(w.shape[0], w.shape[1], rowbias=True):
+                    self._pfold[i] = LnFold(nrm, w, pe=self.pos_embed.pe[0])
+
+    def temporal_fold(self, i, batch, frames, positions):
+        """How norm i (+ PE) of a temporal block over (batch, frames, positions) rows folds: ("m", f)
+        into the fused QKV attention, ("p", f) into the QKV GEMM with the PE as a row bias, or None
+        (the norm is written) — one decision for the producer (_out_norm, the motion module's
+        proj_in) and the consumer (run_temporal)."""
+        mf = self.mfold(i, batch, frames, positions)
+        if mf is not None:
+            return "m", mf
+        if self.fuse_qkv_attention and ops.motion_qkv_takes(batch, frames, positions, self.heads, self.dim_head):
+            return None  # the fused attention runs on normalised rows
+        f = getattr(self, "_pfold", {}).get(i)
+        return ("p", f) if f is not None and f.runs(batch * frames * positions) else None
 
     def mfold(self, i, batch, frames, positions):
         """norm i's MotionLnFold when the fused temporal QKV attention takes this shape, else None."""
@@ -170,7 +192,7 @@ class BasicTransformerBlock(nn.Module):
         its consumer (the rows are then never normalised in memory).  mshape = (batch, frames,
         positions) of a temporal block: norm i (+ PE) may fold into the fused QKV attention."""
         folded = (self.fold(i, h.shape[0]) is not None if pe.get("pe") is None
-                  else mshape is not None and self.mfold(i, *mshape) is not None)
+                  else mshape is not None and self.temporal_fold(i, *mshape) is not None)
         if folded:
             return ops.gemm(a, attn._wo, bias=attn._bo, res=h), None
         return ops.gemm_ln(a, attn._wo, *self._nrm(i), bias=attn._bo, res=h, **pe)
@@ -216,20 +238,24 @@ class BasicTransformerBlock(nn.Module):
             # Q/K/V projection fused into the attention where the kernel takes the shape
             # (level 1: 16 frames, d 40), with norm i + PE folded in when the caller left the rows
             # un-normalised; else the norm, the QKV GEMM and the attention kernel
-            mf = self.mfold(i, *mshape) if n is None else None
+            tf = self.temporal_fold(i, *mshape) if n is None else None
             a = None
-            if mf is not None:
+            if tf is not None and tf[0] == "m":
+                mf = tf[1]
                 a = ops.motion_qkv_attention(h, mf.w, batch, frames, positions, self.heads, d,
                                              scale=attn.attn_scale, ln_fold=(mf.tab, mf.eps))
-            elif self.fuse_qkv_attention:
+            elif self.fuse_qkv_attention and tf is None:
                 if n is None:
                     n = ops.layer_norm(h, *self._nrm(i), pe=pe, pe_div=positions, pe_period=frames)
                 a = ops.motion_qkv_attention(n, attn._wqkv, batch, frames, positions, self.heads, d,
                                              scale=attn.attn_scale)
             if a is None:
-                if n is None:
-                    n = ops.layer_norm(h, *self._nrm(i), pe=pe, pe_div=positions, pe_period=frames)
-                qkv = ops.gemm(n, attn._wqkv)
+                if tf is not None and tf[0] == "p":  # norm i + PE folded into the QKV GEMM
+                    qkv = tf[1].gemm(h, pe_div=positions, pe_period=frames)
+                else:
+                    if n is None:
+                        n = ops.layer_norm(h, *self._nrm(i), pe=pe, pe_div=positions, pe_period=frames)
+                    qkv = ops.gemm(n, attn._wqkv)
                 a = ops.temporal_attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], batch, frames,
                                            positions, self.heads, d, scale=attn.attn_scale)
             # norm2 (+ PE) after attn1, norm3 after attn2
@@ -343,7 +369,7 @@ class AnimateDiffTransformer3D(nn.Module):
                                 two_pass=False, n_split=Fl * ops.gn_splits_per_frame(hw),
                                 rev3=dist.send_perm(B, Fl, hw))
             recv = dist.exchange(hn)                                   # rows (f, b, j)
-            if blk.mfold(1, 1, F, B * pl) is not None:  # norm1 + PE fold into the QKV attention
+            if blk.temporal_fold(1, 1, F, B * pl) is not None:  # norm1 + PE fold into the QKV attention / GEMM
                 h, n = ops.gemm(recv, self.proj_in._w, bias=self.proj_in._b), None
             else:
                 h, n = ops.gemm_ln(recv, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b, pe=blk.pos_embed._pe,
@@ -356,7 +382,7 @@ class AnimateDiffTransformer3D(nn.Module):
         hn = ops.group_norm(x.t, B, Fl * hw, self.groups, 1e-6, self.norm._g, self.norm._b, gather=gather,
                             two_pass=False, n_split=Fl * ops.gn_splits_per_frame(hw))
         if dist is None:  # norm1 (+ PE by frame) fused into proj_in's epilogue, or folded into the QKV attention
-            if blk.mfold(1, B, Fl, hw) is not None:
+            if blk.temporal_fold(1, B, Fl, hw) is not None:
                 h, n = ops.gemm(hn, self.proj_in._w, bias=self.proj_in._b), None
             else:
                 h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b, pe=blk.pos_embed._pe,

@@ -95,9 +95,13 @@ class LnFold:
     The kernel takes mean / rstd of each row from the A fragments it already holds, so the
     normalised rows are never written.  `pack` reorders output rows (GEGLU's interleave) after
     folding; `w` is the Linear's weight in fp32 as the unfolded path would round it (the q rows
-    already carry the softmax scale)."""
+    already carry the softmax scale).
+    pe ([frames][K], the motion block's sinusoidal table, added after the norm): folded as the row
+    bias W·pe[frame] (fp32 [frames][N], `pe_b`), frame = (row / pe_div) % frames as
+    vd_layernorm's; only the v2 / v6 plans take a row bias with the fold."""
 
-    def __init__(self, norm: nn.LayerNorm, w: torch.Tensor, b: Optional[torch.Tensor] = None, pack=None):
+    def __init__(self, norm: nn.LayerNorm, w: torch.Tensor, b: Optional[torch.Tensor] = None, pack=None,
+                 pe: Optional[torch.Tensor] = None):
         g = norm.weight.detach().double()
         be = norm.bias.detach().double()
         wd = w.detach().double()
@@ -111,12 +115,29 @@ class LnFold:
         self.s = self.w.double().sum(1).float().contiguous()
         self.b = bp.float().contiguous()
         self.eps = float(norm.eps)
+        self.pe_b = None
+        if pe is not None:
+            assert pack is None
+            self.pe_b = (pe.detach().double().to(wd.device) @ wd.T).float().contiguous()
+        self._rb = {}
 
     def runs(self, M: int, act: int = 0) -> bool:
-        return ops.ln_fold_runs(M, self.w, self.s, act=act)
+        return ops.ln_fold_runs(M, self.w, self.s, act=act, rowbias=self.pe_b is not None)
 
-    def gemm(self, x, act: int = 0):
-        return ops.gemm(x, self.w, bias=self.b, act=act, ln_fold=(self.s, self.eps))
+    def _rowbias(self, M, pe_div, pe_period):
+        """fp32 [ceil(M / pe_div)][N]: row r = W·pe[r % pe_period] (cached per shape)."""
+        key = ((M + pe_div - 1) // pe_div, pe_period)
+        t = self._rb.get(key)
+        if t is None:
+            idx = torch.arange(key[0], device=self.pe_b.device) % pe_period
+            t = self._rb[key] = self.pe_b[idx].contiguous()
+        return t
+
+    def gemm(self, x, act: int = 0, pe_div: int = 1, pe_period: int = 1):
+        if self.pe_b is None:
+            return ops.gemm(x, self.w, bias=self.b, act=act, ln_fold=(self.s, self.eps))
+        return ops.gemm(x, self.w, bias=self.b, act=act, rowbias=self._rowbias(x.shape[0], pe_div, pe_period),
+                        rb_div=pe_div, ln_fold=(self.s, self.eps))
 
 
 class MotionLnFold:

@@ -82,27 +82,40 @@ def gemm_plan_of(d):
     return k.value, sp.value
 
 
-def ln_fold_runs(M, w, s, *, act=ACT_NONE):
+def ln_fold_runs(M, w, s, *, act=ACT_NONE, rowbias=False):
     """True when vd_gemm runs Linear(LayerNorm(x)) over M rows of x with the norm folded into
-    the GEMM (vd_gemm_desc.ln_fold_s: w = W∘gamma, s = its row sums) — the v8 plan; the caller
-    otherwise writes the normalised rows and runs the plain GEMM.  Decided by the library's own
-    plan (with plan_div, so a frame shard and its unsharded replay decide alike)."""
+    the GEMM (vd_gemm_desc.ln_fold_s: w = W∘gamma, s = its row sums) — the v8 plan (K = 320) or
+    an unsplit v6 (the small M of a frame shard); the caller otherwise writes the normalised rows
+    and runs the plain GEMM.  Decided by the library's own plan (with plan_div, so a frame shard
+    and its unsharded replay decide alike)."""
     N, K = w.shape
     nout = N // 2 if act == ACT_GEGLU else N
     d = GemmDesc(a0=256, lda0=K, k0=K, a_mode=A_DENSE, w=_p(w), ldw=_rows(w), M=M, N=N, K=K, bias=256,
                  act=act, out=256, ldc=nout, ln_fold_s=_p(s), ln_fold_eps=1e-5)
-    return gemm_plan_of(d)[0] == 8
+    if rowbias:  # the motion block's PE by frame (LnFold(pe=...)): no v8 / v5 plan takes a row bias
+        d.rowbias, d.ld_rb, d.rb_div = 256, N, 1
+    return gemm_plan_of(d)[0] != 0
 
 
-def ln_fold_shape_ok(N, K, *, act=ACT_NONE):
-    """Whether a folded LayerNorm (ln_fold_s) can run for an N x K Linear at all (asked at a
-    row count the automatic plan folds): decides at prepare time which folded weights to build."""
+# row counts a folded LayerNorm is asked about at prepare time: the UNet's levels at 2-32 images
+LN_FOLD_PROBE_M = (256, 1024, 4096, 16384, 32768, 131072)
+
+
+def ln_fold_shape_ok(N, K, *, act=ACT_NONE, rowbias=False):
+    """Whether a folded LayerNorm (ln_fold_s) can run for an N x K Linear at any of the row counts
+    the UNet gives it (LN_FOLD_PROBE_M, automatic plan): decides at prepare time which folded
+    weights to build."""
     nout = N // 2 if act == ACT_GEGLU else N
-    d = GemmDesc(a0=256, lda0=K, k0=K, a_mode=A_DENSE, w=256, ldw=K, M=32768, N=N, K=K, bias=256, act=act,
-                 out=256, ldc=nout, ln_fold_s=256, ln_fold_eps=1e-5)
-    k, sp = C.c_int32(0), C.c_int32(0)
-    check(lib().vd_gemm_plan(C.byref(d), C.byref(k), C.byref(sp)), "vd_gemm_plan")
-    return k.value == 8
+    for M in LN_FOLD_PROBE_M:
+        d = GemmDesc(a0=256, lda0=K, k0=K, a_mode=A_DENSE, w=256, ldw=K, M=M, N=N, K=K, bias=256, act=act,
+                     out=256, ldc=nout, ln_fold_s=256, ln_fold_eps=1e-5)
+        if rowbias:
+            d.rowbias, d.ld_rb, d.rb_div = 256, N, 1
+        k, sp = C.c_int32(0), C.c_int32(0)
+        check(lib().vd_gemm_plan(C.byref(d), C.byref(k), C.byref(sp)), "vd_gemm_plan")
+        if k.value != 0:
+            return True
+    return False
 
 
 def _run_gemm(d, device, what):
