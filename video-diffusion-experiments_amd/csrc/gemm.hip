@@ -466,16 +466,22 @@ __device__ unsigned long long g2_diag[4096 * 8 * 6];
   } while (0)
 #endif
 
-// Σ over a bf16x8 fragment of x and of x² (fp32 dot-2 accumulation; every bf16 product is exact)
+// Σ over a bf16x8 fragment of x and of x² (fp32 dot-2 accumulation; every bf16 product is exact).
+// The pairs come from shufflevector: hipcc (ROCm 7.2) lowers bit_cast<bf16x2>(u32x4 element j) to
+// element 0 for every j (one dword loaded, the same register dotted four times) — found by this
+// kernel's parity test, reproduced stand-alone.
 __device__ __forceinline__ void frag_stats(const bf16x8& f, float& s, float& q) {
-  const u32x4 u = __builtin_bit_cast(u32x4, f);
-  const bf16x2_t one2 = __builtin_bit_cast(bf16x2_t, 0x3F803F80u);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const bf16x2_t p = __builtin_bit_cast(bf16x2_t, u[j]);
-    s = __builtin_amdgcn_fdot2_f32_bf16(p, one2, s, false);
-    q = __builtin_amdgcn_fdot2_f32_bf16(p, p, q, false);
-  }
+  const bf16x2_t one2 = {(__bf16)1.0f, (__bf16)1.0f};
+  const bf16x2_t p0 = __builtin_shufflevector(f, f, 0, 1), p1 = __builtin_shufflevector(f, f, 2, 3);
+  const bf16x2_t p2 = __builtin_shufflevector(f, f, 4, 5), p3 = __builtin_shufflevector(f, f, 6, 7);
+  s = __builtin_amdgcn_fdot2_f32_bf16(p0, one2, s, false);
+  q = __builtin_amdgcn_fdot2_f32_bf16(p0, p0, q, false);
+  s = __builtin_amdgcn_fdot2_f32_bf16(p1, one2, s, false);
+  q = __builtin_amdgcn_fdot2_f32_bf16(p1, p1, q, false);
+  s = __builtin_amdgcn_fdot2_f32_bf16(p2, one2, s, false);
+  q = __builtin_amdgcn_fdot2_f32_bf16(p2, p2, q, false);
+  s = __builtin_amdgcn_fdot2_f32_bf16(p3, one2, s, false);
+  q = __builtin_amdgcn_fdot2_f32_bf16(p3, p3, q, false);
 }
 
 // acc[a][b] -> rstd_b·(acc − mean_b·s[n]) for the lane's rows from its per-k-quarter sums (LNF)

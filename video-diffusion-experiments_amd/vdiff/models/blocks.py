@@ -270,17 +270,40 @@ class BasicTransformerBlock(nn.Module):
         global frame rank*f_loc + f."""
         C = h.shape[1]
         d = self.dim_head
-        pe = self.pos_embed._pe[dist.rank * frames_local:]
+        pe_off = dist.rank * frames_local
+        pe = self.pos_embed._pe[pe_off:]
         frames = frames_local * dist.world
-        n = ops.layer_norm(h, *self._nrm(1), pe=pe, pe_div=positions, pe_period=frames_local)
+        M = h.shape[0]
+
+        def pfold(i):  # norm i + PE folded into the Q and the K/V GEMM (the QKV GEMM's fold, sliced)
+            tf = self.temporal_fold(i, batch, frames_local, positions)
+            if tf is None or tf[0] != "p":
+                return None
+            cache = self.__dict__.setdefault("_pfold_split", {})
+            if i not in cache:
+                cache[i] = (tf[1].slice(0, C), tf[1].slice(C, 3 * C))
+            fq, fkv = cache[i]
+            return (fq, fkv) if fq.runs(M) and fkv.runs(M) else None
+
+        n = None
+        if pfold(1) is None:
+            n = ops.layer_norm(h, *self._nrm(1), pe=pe, pe_div=positions, pe_period=frames_local)
         for attn, i in ((self.attn1, 1), (self.attn2, 2)):
-            q = ops.gemm(n, attn._wqkv[:C])
-            kv = dist.gather_kv_frames(ops.gemm(n, attn._wqkv[C:]), batch, frames_local, positions,
-                                       ops.block_transpose)
+            pf = pfold(i) if n is None else None
+            if pf is not None:
+                q = pf[0].gemm(h, pe_div=positions, pe_period=frames_local, pe_off=pe_off)
+                kv = pf[1].gemm(h, pe_div=positions, pe_period=frames_local, pe_off=pe_off)
+            else:
+                q = ops.gemm(n, attn._wqkv[:C])
+                kv = ops.gemm(n, attn._wqkv[C:])
+            kv = dist.gather_kv_frames(kv, batch, frames_local, positions, ops.block_transpose)
             a = ops.temporal_attention_kv(q, kv[:, :C], kv[:, C:], batch, frames_local, frames, positions,
                                           self.heads, d, scale=attn.attn_scale)
-            h, n = self._out_norm(a, attn, i + 1, h, pe=pe if i == 1 else None, pe_div=positions,
-                                  pe_period=frames_local)
+            if i == 1 and pfold(2) is not None:  # norm2 folds into attn2's Q / K/V GEMMs
+                h, n = ops.gemm(a, attn._wo, bias=attn._bo, res=h), None
+            else:
+                h, n = self._out_norm(a, attn, i + 1, h, pe=pe if i == 1 else None, pe_div=positions,
+                                      pe_period=frames_local)
         return self._ff(h, n)
 
     def forward(self, hidden_states, attention_mask=None, encoder_hidden_states=None,

@@ -124,20 +124,30 @@ class LnFold:
     def runs(self, M: int, act: int = 0) -> bool:
         return ops.ln_fold_runs(M, self.w, self.s, act=act, rowbias=self.pe_b is not None)
 
-    def _rowbias(self, M, pe_div, pe_period):
-        """fp32 [ceil(M / pe_div)][N]: row r = W·pe[r % pe_period] (cached per shape)."""
-        key = ((M + pe_div - 1) // pe_div, pe_period)
+    def slice(self, lo: int, hi: int) -> "LnFold":
+        """The same fold for output rows lo .. hi of the Linear (e.g. the Q or the K/V part of a
+        fused QKV projection): per output column the arithmetic is unchanged."""
+        f = object.__new__(LnFold)
+        f.w, f.s, f.b, f.eps = self.w[lo:hi], self.s[lo:hi], self.b[lo:hi], self.eps
+        f.pe_b = None if self.pe_b is None else self.pe_b[:, lo:hi].contiguous()
+        f._rb = {}
+        return f
+
+    def _rowbias(self, M, pe_div, pe_period, pe_off=0):
+        """fp32 [ceil(M / pe_div)][N]: row r = W·pe[pe_off + r % pe_period] (cached per shape)."""
+        key = ((M + pe_div - 1) // pe_div, pe_period, pe_off)
         t = self._rb.get(key)
         if t is None:
-            idx = torch.arange(key[0], device=self.pe_b.device) % pe_period
+            idx = pe_off + torch.arange(key[0], device=self.pe_b.device) % pe_period
             t = self._rb[key] = self.pe_b[idx].contiguous()
         return t
 
-    def gemm(self, x, act: int = 0, pe_div: int = 1, pe_period: int = 1):
+    def gemm(self, x, act: int = 0, pe_div: int = 1, pe_period: int = 1, pe_off: int = 0):
         if self.pe_b is None:
             return ops.gemm(x, self.w, bias=self.b, act=act, ln_fold=(self.s, self.eps))
-        return ops.gemm(x, self.w, bias=self.b, act=act, rowbias=self._rowbias(x.shape[0], pe_div, pe_period),
-                        rb_div=pe_div, ln_fold=(self.s, self.eps))
+        return ops.gemm(x, self.w, bias=self.b, act=act,
+                        rowbias=self._rowbias(x.shape[0], pe_div, pe_period, pe_off), rb_div=pe_div,
+                        ln_fold=(self.s, self.eps))
 
 
 class MotionLnFold:
