@@ -102,23 +102,20 @@ def _plan(d):
     return k.value, sp.value
 
 
-def test_plan_folds_on_v8_and_unsplit_v2_v6():
+def test_plan_folds_on_v8_and_unsplit_v6():
     """vd_gemm_plan: a folded LayerNorm runs on v8 where the automatic plan would take v8
     (M >= 16384, K = 320, N a multiple of 160) or where v8 is forced (path 8, M >= 4096), and on
-    v2 / v6 wherever the plain GEMM's plan is an unsplit v2 / v6 (levels 2-4); every other
-    shape reports kernel 0 — vd_gemm refuses it and the model keeps the unfolded form."""
+    v6 wherever the plain GEMM's plan is an unsplit v6 (the small M of a frame shard); every other
+    shape — v2 / v3 plans, split K — reports kernel 0: vd_gemm refuses it and the model keeps the
+    unfolded form."""
     assert _plan(_desc(16384, 960)) == (8, 1)
     assert _plan(_desc(131072, 2560, act=ops.ACT_GEGLU)) == (8, 1)
     assert _plan(_desc(8192, 320)) == (6, 1)          # below the automatic v8 range: v6
     assert _plan(_desc(8192, 320, path=8))[0] == 8    # forced
     assert _plan(_desc(1024, 3840, K=1280)) == (6, 1)  # L3 QKV at 4 images
     assert _plan(_desc(256, 10240, K=1280, act=ops.ACT_GEGLU)) == (6, 1)
-    assert _plan(_desc(4096, 1920, K=640)) == (2, 1)   # L2 QKV at 4 images: the unsplit v2
-    assert _plan(_desc(1024, 10240, K=1280, act=ops.ACT_GEGLU)) == (2, 1)
-    assert _plan(_desc(32768, 640, K=640)) == (2, 1)   # L2 to_q at 32 images
+    assert _plan(_desc(4096, 1920, K=640))[0] == 0    # the plain plan is v2
     assert _plan(_desc(32768, 1920, K=640))[0] == 0   # the plain plan is v3
-    assert _plan(_desc(1024, 1280, K=5120))[0] == 0   # the plain plan splits K (v2, split 8)
-    assert _plan(_desc(65536, 5120, K=1280, act=ops.ACT_GEGLU))[0] == 0  # v3
     assert _plan(_desc(1024, 1280, K=1280, path=6))[0] == 0  # forced v6 splits K: no fold
     assert _plan(_desc(131072, 320, plan_m=8192)) == (6, 1)  # planned as a small shard: v6
     d = _desc(16384, 320)
@@ -128,7 +125,7 @@ def test_plan_folds_on_v8_and_unsplit_v2_v6():
 
 def test_fold_shape_gate_and_refusal():
     assert ops.ln_fold_shape_ok(960, 320) and ops.ln_fold_shape_ok(2560, 320, act=ops.ACT_GEGLU)
-    assert ops.ln_fold_shape_ok(1920, 640) and ops.ln_fold_shape_ok(10240, 1280, act=ops.ACT_GEGLU)
+    assert ops.ln_fold_shape_ok(3840, 1280) and ops.ln_fold_shape_ok(10240, 1280, act=ops.ACT_GEGLU)
     assert not ops.ln_fold_shape_ok(320, 328)         # K not a multiple of 32: v1 only
     # vd_gemm refuses a fold no kernel takes, before any launch (argument checks are host-side)
     d = _desc(32768, 1920, K=640)

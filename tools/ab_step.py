@@ -12,7 +12,8 @@ Switches:
              against the unfolded norm -> GEMM;
   cfg_dedup  conv_in + down_blocks[0].resnets[0] once for both CFG halves (DenoiseLoop.cfg_dedup);
   mfold      the motion block's norm1 / norm2 + PE folded into the fused QKV attention (_mfold);
-  pfold      the same norms + PE folded into the levels-2-4 QKV GEMM, PE as a row bias (_pfold)."""
+  pfold      the same norms + PE folded into the levels-2-4 QKV GEMM, PE as a row bias (_pfold);
+  fold_v6    the folds the plan runs on v6 (a rank's levels 2-4) against the unfolded form there."""
 from __future__ import annotations
 
 import argparse
@@ -63,7 +64,24 @@ def set_pfold(unet, on, saved):
             m._pfold = saved[key] if on else {}
 
 
-SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup, "mfold": set_mfold, "pfold": set_pfold}
+def set_fold_v6(unet, on, saved):  # folds the plan runs on v6 (levels 2-4 of a rank) vs none there
+    from vdiff import ops
+    orig = saved.setdefault("ln_fold_runs", ops.ln_fold_runs)
+
+    def runs(M, w, s, *, act=0, rowbias=False):
+        if not orig(M, w, s, act=act, rowbias=rowbias):
+            return False
+        N, K = w.shape
+        d = ops.GemmDesc(a0=256, lda0=K, k0=K, a_mode=0, w=w.data_ptr(), ldw=K, M=M, N=N, K=K, bias=256, act=act,
+                         out=256, ldc=N // 2 if act == ops.ACT_GEGLU else N, ln_fold_s=s.data_ptr(), ln_fold_eps=1e-5)
+        if rowbias:
+            d.rowbias, d.ld_rb, d.rb_div = 256, N, 1
+        return on or ops.gemm_plan_of(d)[0] != 6
+    ops.ln_fold_runs = runs
+
+
+SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup, "mfold": set_mfold, "pfold": set_pfold,
+            "fold_v6": set_fold_v6}
 
 
 def main():

@@ -65,7 +65,7 @@ def main():
         e1.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / args.reps
         kind = KIND[d.a_mode] + ("+res" if d.res else "") + ACT.get(d.act, "") + ("+ln" if d.ln_out else "") + \
-            ("+fold" if d.ln_fold_s else "")
+            ("+rb" if d.rowbias else "") + ("+fold" if d.ln_fold_s else "")
         kv, sp = C.c_int32(), C.c_int32()
         check(lib().vd_gemm_plan(C.byref(d), C.byref(kv), C.byref(sp)), "vd_gemm_plan")
         key = (kind, d.M, d.N, d.K, f"v{kv.value}" + (f"/s{sp.value}" if sp.value > 1 else ""))

@@ -466,57 +466,7 @@ __device__ unsigned long long g2_diag[4096 * 8 * 6];
   } while (0)
 #endif
 
-// Σ over a bf16x8 fragment of x and of x² (fp32 dot-2 accumulation; every bf16 product is exact).
-// The pairs come from shufflevector: hipcc (ROCm 7.2) lowers bit_cast<bf16x2>(u32x4 element j) to
-// element 0 for every j (one dword loaded, the same register dotted four times) — found by this
-// kernel's parity test, reproduced stand-alone.
-__device__ __forceinline__ void frag_stats(const bf16x8& f, float& s, float& q) {
-  const bf16x2_t one2 = {(__bf16)1.0f, (__bf16)1.0f};
-  const bf16x2_t p0 = __builtin_shufflevector(f, f, 0, 1), p1 = __builtin_shufflevector(f, f, 2, 3);
-  const bf16x2_t p2 = __builtin_shufflevector(f, f, 4, 5), p3 = __builtin_shufflevector(f, f, 6, 7);
-  s = __builtin_amdgcn_fdot2_f32_bf16(p0, one2, s, false);
-  q = __builtin_amdgcn_fdot2_f32_bf16(p0, p0, q, false);
-  s = __builtin_amdgcn_fdot2_f32_bf16(p1, one2, s, false);
-  q = __builtin_amdgcn_fdot2_f32_bf16(p1, p1, q, false);
-  s = __builtin_amdgcn_fdot2_f32_bf16(p2, one2, s, false);
-  q = __builtin_amdgcn_fdot2_f32_bf16(p2, p2, q, false);
-  s = __builtin_amdgcn_fdot2_f32_bf16(p3, one2, s, false);
-  q = __builtin_amdgcn_fdot2_f32_bf16(p3, p3, q, false);
-}
-
-// acc[a][b] -> rstd_b·(acc − mean_b·s[n]) for the lane's rows from its per-k-quarter sums (LNF)
-template <int MB, int NB>
-__device__ __forceinline__ void ln_fold_acc(const vd_gemm_desc& d, f32x4 (&acc)[NB][MB], float (&ls)[MB],
-                                            float (&lq)[MB], int nbase, int lane, int nodd = -1) {
-  const int fq = lane >> 4;
-  const float rk = 1.0f / (float)d.K;
-  float nmean[MB], rstd[MB];
-#pragma unroll
-  for (int b = 0; b < MB; ++b) {
-    float s = ls[b], q = lq[b];
-    s += __shfl_xor(s, 16, 64);
-    q += __shfl_xor(q, 16, 64);
-    s += __shfl_xor(s, 32, 64);
-    q += __shfl_xor(q, 32, 64);
-    const float mean = s * rk;
-    rstd[b] = rsqrtf(fmaxf(fmaf(q, rk, -mean * mean), 0.f) + d.ln_fold_eps);
-    nmean[b] = -mean;
-  }
-#pragma unroll
-  for (int a = 0; a < NB; ++a) {
-    const int n = (nodd >= 0 && a == NB - 1 ? nodd : nbase + a * 16) + 4 * fq;  // gemm_epilogue's columns
-    const float4 t = n < (int)d.N ? *(const float4*)(d.ln_fold_s + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float sv[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-    for (int b = 0; b < MB; ++b)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[a][b][j] = rstd[b] * fmaf(nmean[b], sv[j], acc[a][b][j]);
-  }
-}
-
-// LNF (round 5): the folded LayerNorm on v2 as on v6 (dense, unsplit units only — the plan): the
-// row statistics from dot-2 VALU on the X fragments of each k-step, reset with the accumulators
-template <int BN, int MODE, bool LNF = false>
+template <int BN, int MODE>
 __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                          uint32_t a1_bytes, uint32_t w_bytes,
                                                          int split) {
@@ -691,7 +641,6 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
   int cu = u_begin, ckt, ckt1;
   unit_kr(cu, ckt, ckt1);
   const int fr = lane & 15, fq = lane >> 4;
-  float ls[C::MB] = {}, lq[C::MB] = {};  // LNF: this lane's k-quarter sums of Σx, Σx² per row block
   int stage = 0;
 #ifdef VD_G2_STAMPS
   unsigned long long st0, st1, st2, st3, st4, sw = 0, sb = 0, sm = 0, stl = 0, tbeg;
@@ -745,12 +694,6 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
         }
         __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
       }
-      if constexpr (LNF) {
-#pragma unroll
-        for (int ks = 0; ks < BK / 32; ++ks)
-#pragma unroll
-          for (int b = 0; b < C::MB; ++b) frag_stats(xf[ks][b], ls[b], lq[b]);
-      }
     }
 #ifdef VD_G2_STAMPS
     G2_STAMP(st3);
@@ -759,11 +702,6 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
       const int tile = cu / split, sp = cu % split;
       const int64_t m0 = (int64_t)(tile / tiles_n) * G2_BM, n0 = (int64_t)(tile % tiles_n) * BN;
       if (split == 1) {
-        if constexpr (LNF) {
-          ln_fold_acc<C::MB, C::NB>(d, acc, ls, lq, (int)n0 + wcb, lane, ODDMAP ? (int)n0 + wodd : -1);
-#pragma unroll
-          for (int b = 0; b < C::MB; ++b) ls[b] = lq[b] = 0.f;
-        }
         gemm_epilogue<C::MB, C::NB>(d, acc, (int)m0 + wm * C::MB * 16, (int)n0 + wcb, lane,
                                     ODDMAP ? (int)n0 + wodd : -1);
       } else {  // split-K: raw fp32 slab ws[sp][m][n]; gemm_splitk_reduce applies the epilogue
@@ -1654,11 +1592,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
 // the grid oversubscribes the CUs, 4 / 6 stages (2 / 1 per CU) on small grids, where
 // each workgroup's k-loop is latency-bound and more tiles in flight pay directly.
 // LNF (round 5, vd_gemm_desc.ln_fold_s; dense, unsplit): the LayerNorm of A's rows folded in, as
-// v8's — but here the row statistics come from VALU dot products on the X fragments the wave already
-// holds (v_dot2_f32_bf16: 2 x 4 per fragment, Σx against ones and Σx² against itself), which fill the
-// gaps of a loop that runs far below the MFMA pipe's rate at these M; the lane's four k-quarters are
-// summed by two cross-lane adds after the loop, and the accumulators become rstd·(acc − mean·s[n])
-// before the common epilogue adds b' (the folded bias).
+// v8's: per k-step two more MFMAs per X fragment the wave already holds — ones·x (Σx in every entry)
+// and x·xᵀ (Σx² on the Gram block's diagonal) — in a loop that runs far below the MFMA pipe's rate at
+// these M (dot-2 VALU for the same sums cost ≈ 10 cycles each beside the MFMAs and 1.5-3x the time,
+// MI355X_MICROARCH.md "price of one filler"); the accumulators become rstd·(acc − mean·s[n]) before
+// the common epilogue adds b' (the folded bias) and any row bias (the motion block's W·pe[frame]).
 constexpr int G6_BM = 64, G6_BN = 64, G6_NT = 256;
 constexpr int G6_A = G6_BM * BK * 2, G6_W = G6_BN * BK * 2, G6_STAGE = G6_A + G6_W;  // 8 + 8 KiB
 
@@ -1764,7 +1702,10 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
   for (int j = 0; j < G6_S - 1; ++j)
     if (j < nk) issue(j);
   const int fr = lane & 15, fq = lane >> 4;
-  float ls[MB] = {}, lq[MB] = {};  // LNF: this lane's k-quarter sums of Σx, Σx² per row block
+  f32x4 sacc[LNF ? MB : 1], gacc[LNF ? MB : 1];  // LNF: ones·x and x·xᵀ per row block
+#pragma unroll
+  for (int b = 0; b < (LNF ? MB : 1); ++b) sacc[b] = gacc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
   int stage = 0;
   for (int it = 0; it < nk; ++it) {
     // k-steps it+1 .. it+S-2 (4 pieces each) may stay in flight
@@ -1801,14 +1742,36 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
 #pragma unroll
         for (int ks = 0; ks < BK / 32; ++ks)
 #pragma unroll
-          for (int b = 0; b < MB; ++b) frag_stats(xf[ks][b], ls[b], lq[b]);
+          for (int b = 0; b < MB; ++b) {
+            sacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, xf[ks][b], sacc[b], 0, 0, 0);
+            gacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[ks][b], xf[ks][b], gacc[b], 0, 0, 0);
+          }
       }
     }
     stage = stage == G6_S - 1 ? 0 : stage + 1;
   }
   const int mbase = (int)m0 + wm * 32, nbase = (int)n0 + wn * 32;
   if constexpr (LNF) {  // dense, unsplit (plan): the whole row went through this wave
-    ln_fold_acc<MB, NB>(d, acc, ls, lq, nbase, lane);
+    // the lane's outputs of row block b belong to A row fr: Σx in every entry of sacc[b], Σx² the
+    // Gram block's diagonal entry (fr, fr), held by lane fr + 16 (fr >> 2) at index fr & 3
+    const float rk = 1.0f / (float)d.K;
+    const int j3 = fr & 3;
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      const float gd = j3 == 0 ? gacc[b][0] : j3 == 1 ? gacc[b][1] : j3 == 2 ? gacc[b][2] : gacc[b][3];
+      const float sxx = __shfl(gd, fr + 16 * (fr >> 2), 64);
+      const float mean = sacc[b][0] * rk;
+      const float rstd = rsqrtf(fmaxf(fmaf(sxx, rk, -mean * mean), 0.f) + d.ln_fold_eps);
+#pragma unroll
+      for (int a = 0; a < NB; ++a) {
+        const int n = nbase + a * 16 + 4 * fq;
+        const float4 t = n < (int)N ? *(const float4*)(d.ln_fold_s + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        acc[a][b][0] = rstd * fmaf(-mean, t.x, acc[a][b][0]);
+        acc[a][b][1] = rstd * fmaf(-mean, t.y, acc[a][b][1]);
+        acc[a][b][2] = rstd * fmaf(-mean, t.z, acc[a][b][2]);
+        acc[a][b][3] = rstd * fmaf(-mean, t.w, acc[a][b][3]);
+      }
+    }
     gemm_epilogue<MB, NB>(d, acc, mbase, nbase, lane);
     return;
   }
@@ -2237,13 +2200,7 @@ int launch2(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, ui
   const int64_t grid = (units + rounds - 1) / rounds;
   if (d.a_mode == VD_A_CONV3X3)
     hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_CONV3X3>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
-  else if constexpr (BN != 32) {
-    if (d.ln_fold_s)
-      hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE, true>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb,
-                         split);
-    else
-      hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
-  } else
+  else
     hipLaunchKernelGGL((gemm2_kernel<BN, VD_A_DENSE>), dim3((unsigned)grid), dim3(G2_NT), 0, s, d, a0b, a1b, wb, split);
   int rc = vd_launch_status();
   if (rc != VD_OK || split == 1) return rc;
@@ -2433,8 +2390,11 @@ Plan plan_core(const vd_gemm_desc& d) {
   const bool v8auto = v8ok && M >= 16384;
   if (path == 8 && !v8ok) path = 0;  // forced v8 on a shape it does not take: the product plan
   // a folded LayerNorm (ln_fold_s) runs on v8 wherever v8 would run the plain GEMM (or is forced),
-  // and on v2 / v6 wherever the plain GEMM's plan is an unsplit v2 / v6 (levels 2-4, the small M
-  // of a frame-sharded rank); no other kernel carries it: ver 0 = not runnable, the caller takes the unfolded form
+  // and on v6 wherever the plain GEMM's plan is an unsplit v6 (levels 2-4 of a frame-sharded rank,
+  // the mid block); no other kernel carries it: ver 0 = not runnable, the caller takes the unfolded
+  // form.  (Round 5 measured the fold on v2 / v3 too — row statistics by dot-2 VALU: 1.4-1.5x the v2
+  // GEMM's time, 20x v3's — and withdrew it: those kernels run at the MFMA / issue limit, and
+  // each of their N tiles would recompute the statistics of the same rows.)
   if (d.ln_fold_s) {
     if ((v8auto && path == 0) || (v8ok && path == 8)) {
       p.ver = 8;
@@ -2444,7 +2404,7 @@ Plan plan_core(const vd_gemm_desc& d) {
     vd_gemm_desc g = d;
     g.ln_fold_s = nullptr;
     const Plan q = plan_core(g);
-    if ((q.ver == 6 || (q.ver == 2 && q.bn != 32)) && q.split == 1 && d.a_mode == VD_A_DENSE) return q;
+    if (q.ver == 6 && q.split == 1 && d.a_mode == VD_A_DENSE) return q;
     p.ver = 0;
     return p;
   }
@@ -2590,11 +2550,11 @@ Plan plan_core(const vd_gemm_desc& d) {
   return p;
 }
 
-// a folded LayerNorm only ever runs on v8 or an unsplit v2 / v6: every other outcome of the plan (its
+// a folded LayerNorm only ever runs on v8 or an unsplit v6: every other outcome of the plan (its
 // early exits included) is "no kernel"
 Plan plan(const vd_gemm_desc& d) {
   Plan p = plan_core(d);
-  if (d.ln_fold_s && p.ver != 8 && !((p.ver == 6 || (p.ver == 2 && p.bn != 32)) && p.split == 1)) {
+  if (d.ln_fold_s && p.ver != 8 && !(p.ver == 6 && p.split == 1)) {
     p.ver = 0;
     p.split = 1;
     p.ws_bytes = 0;

@@ -155,6 +155,7 @@ class FrameShard:
         tools/capture_probe.py; a forked COMPUTE stream captures and replays correctly.)
         The block is per position, so which positions a rank takes per chunk is free: chunk c
         sends positions (c*W + r)*pc + j to rank r, making every chunk's buffers contiguous."""
+        from .. import ops  # the plan controls only (no launch)
         W, C = self.world, self.chunks
         if hw % W:
             raise ValueError(f"{hw} positions do not shard over {W} ranks")
@@ -181,7 +182,8 @@ class FrameShard:
                 ctx = contextlib.nullcontext()
             with ctx:
                 hp = transpose(recv[c], W, batch, frames_local * pc)      # (b, s, f_loc, j) = (b, f, j)
-                hp = block(hp, batch, frames_local * W, pc)
+                with ops.plan_scaled(C):  # the chunk planned as the whole block: same kernels / folds
+                    hp = block(hp, batch, frames_local * W, pc)
                 back = transpose(hp, batch, W, frames_local * pc)        # (s, b, f_loc, j)
                 if cuda:
                     done = torch.cuda.Event()

@@ -46,9 +46,24 @@ def _rows(t, dtype=BF16):
 class _GemmPlan:
     path = 0       # vd_gemm_desc.path for the GEMMs issued (0 = the automatic plan)
     plan_div = 0   # > 0: plan every GEMM whose M it divides as if M were M / plan_div
+    plan_mul = 1   # > 1: plan every GEMM as if M were M * plan_mul (before plan_div)
 
 
 _PLAN = _GemmPlan()
+
+
+@contextlib.contextmanager
+def plan_scaled(mul: int):
+    """Plan every GEMM (and the fused-kernel shape questions) inside the block as if its M were
+    `mul` times larger: the motion block run on one of `mul` position chunks
+    (FrameShard(overlap_chunks=mul)) then makes every kernel, split-K and LayerNorm-fold decision
+    the whole block would, so chunking changes the launch count, never the arithmetic."""
+    old = _PLAN.plan_mul
+    _PLAN.plan_mul = old * int(mul)
+    try:
+        yield
+    finally:
+        _PLAN.plan_mul = old
 
 
 @contextlib.contextmanager
@@ -69,8 +84,11 @@ def gemm_plan(path: int = 0, plan_div: int = 0):
 
 def _plan_controls(d):
     d.path = _PLAN.path
-    if _PLAN.plan_div > 1 and d.M % _PLAN.plan_div == 0:
-        d.plan_m = d.M // _PLAN.plan_div
+    m = d.M * _PLAN.plan_mul
+    if _PLAN.plan_div > 1 and m % _PLAN.plan_div == 0:
+        m //= _PLAN.plan_div
+    if m != d.M:
+        d.plan_m = m
 
 
 def gemm_plan_of(d):
@@ -416,6 +434,7 @@ def motion_qkv_takes(batch, frames, positions, heads, d):
     """Whether vd_motion_qkv_attention takes this shape (vd_motion_qkv_attention_takes; no launch).
     Under gemm_plan(plan_div=N) the question is asked for one of N frame shards (batch 1, the
     positions divided by N), so an unsharded replay folds the motion norms exactly where a shard would."""
+    positions *= _PLAN.plan_mul
     if _PLAN.plan_div > 1 and (batch * positions) % _PLAN.plan_div == 0:
         batch, positions = 1, batch * positions // _PLAN.plan_div
     return bool(lib().vd_motion_qkv_attention_takes(batch, frames, positions, heads, d))
