@@ -132,12 +132,12 @@ typedef struct vd_gemm_desc {
    * column k of the Linear's W scaled by gamma[k], rounded to bf16 once), bias = b + W·beta
    * (fp32), and ln_fold_s[n] = Σ_k w[n][k] in fp32 (of the bf16 w).  The kernel takes each row's
    * mean and rstd = 1/sqrt(var + ln_fold_eps) from A itself (Σx and Σx² over the A fragments it
-   * holds: two extra MFMAs per k-step on v8, dot-2 VALU on v6) and its epilogue forms
+   * holds: two extra MFMAs per X fragment, on v8 and v6) and its epilogue forms
    *   rstd·(Σ_k w[n][k] x[m][k] − mean·ln_fold_s[n]) + bias[n]   (then act / GEGLU as usual)
    * = Linear(LayerNorm(x)) without the normalised rows being written or read.  Only the
-   * weight-stationary v8 path (K = 320) and an unsplit v2 / v6 (levels 2-4) carry it (dense, no
+   * weight-stationary v8 path (K = 320) and an unsplit v6 (levels 2-4 of a rank) carry it (dense, no
    * residual / rmap; a row bias — the motion block's positional encoding W·pe[frame] — is added
-   * after the fold on v2 / v6): vd_gemm_plan reports kernel 0 and vd_gemm returns
+   * after the fold on v6): vd_gemm_plan reports kernel 0 and vd_gemm returns
    * VD_EUNSUPPORTED for any other plan. */
   const float* ln_fold_s; float ln_fold_eps;
 } vd_gemm_desc;

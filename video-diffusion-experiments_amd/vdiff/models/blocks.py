@@ -153,7 +153,7 @@ class BasicTransformerBlock(nn.Module):
                 w = torch.cat([attn.to_q.weight.float() * c, attn.to_k.weight.float(), attn.to_v.weight.float()], 0)
                 self._mfold[i] = MotionLnFold(nrm, w, self.pos_embed.pe[0], self.heads, self.dim_head)
         # elsewhere (levels 2-4: d = 80 / 160, no fused QKV attention) norm1 / norm2 + PE fold into
-        # the QKV GEMM, the PE as the row bias W·pe[frame] (LnFold(pe=...), v2 / v6 plans)
+        # the QKV GEMM, the PE as the row bias W·pe[frame] (LnFold(pe=...), the v6 plan)
         self._pfold = {}
         if self.pos_embed is not None:
             c = self.attn1.dim_head ** -0.5 * math.log2(math.e)

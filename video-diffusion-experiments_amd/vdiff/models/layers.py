@@ -98,7 +98,7 @@ class LnFold:
     already carry the softmax scale).
     pe ([frames][K], the motion block's sinusoidal table, added after the norm): folded as the row
     bias W·pe[frame] (fp32 [frames][N], `pe_b`), frame = (row / pe_div) % frames as
-    vd_layernorm's; only the v2 / v6 plans take a row bias with the fold."""
+    vd_layernorm's; only the v6 plan takes a row bias with the fold."""
 
     def __init__(self, norm: nn.LayerNorm, w: torch.Tensor, b: Optional[torch.Tensor] = None, pack=None,
                  pe: Optional[torch.Tensor] = None):
