@@ -96,22 +96,9 @@ __device__ __forceinline__ void mq_wait_vm() {
   else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-}
-
-__device__ __forceinline__ void mq_wait_vm_rt(int n) {  // s_waitcnt vmcnt(n), n in 0..9
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-  }
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
 }
 
 template <int D>
@@ -242,10 +229,14 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
     const int t = h * Cf::NCH + kc;
     // this wave's pieces of chunk t landed: the younger ones are chunks t+1 .. min(t+S-2, T-1)
     const int ahead = (T - 1 - t) < (MQ2_S - 2) ? (T - 1 - t) : (MQ2_S - 2);
-    if constexpr (LNF) {  // + one table piece for every head-first chunk among them
-      int younger = 2 * ahead;
-      for (int u = t + 1; u <= t + ahead; ++u) younger += (u % Cf::NCH) == 0;
-      mq_wait_vm_rt(younger);
+    // LNF: + one table piece for every head-first chunk among them.  With the full window (4 chunks
+    // ahead, every chunk but the last head's tail) that is one piece exactly when kc >= 1 — a
+    // compile-time count in this unrolled loop; the tail (head 7, kc >= 1) has no younger table piece.
+    // (A run-time count through a 10-way switch cost the kernel 18 %: 156.5 vs 132.7 us per launch.)
+    static_assert(MQ2_S - 2 == 4 && Cf::NCH == 5, "the static table-piece count below");
+    if (LNF && ahead >= 4) {
+      if (kc == 0) mq_wait_vm<8>();
+      else mq_wait_vm<9>();
     } else if (ahead >= 4) mq_wait_vm<8>();
     else if (ahead == 3) mq_wait_vm<6>();
     else if (ahead == 2) mq_wait_vm<4>();
