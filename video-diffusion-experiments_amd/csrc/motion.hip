@@ -107,7 +107,8 @@ struct Mq2Cfg {
   static constexpr int W_BYTES = B::NWP * B::KC * 2;               // 16 KiB ring slot
   static constexpr int S_BYTES = B::S_ELEMS * 2;                   // per-wave scratch
   static constexpr int TAB_BYTES = 8192;                           // LNF: one head's s | P' table
-  static constexpr int LDS_BYTES = MQ2_S * W_BYTES + B::P * S_BYTES + 2 * TAB_BYTES;
+  static constexpr int STAT_BYTES = 2 * MF * 8;                     // LNF: per wave (-mean, rstd) of 2 x 16 rows
+  static constexpr int LDS_BYTES = MQ2_S * W_BYTES + B::P * S_BYTES + 2 * TAB_BYTES + B::P * STAT_BYTES;
   static_assert(B::NWP == 128 && B::KC == 64, "16 pieces of 8 ring rows x 128 B per chunk");
   static_assert(8 * 1024 == TAB_BYTES && 3 * B::C / 8 * (1 + MF) <= TAB_BYTES / 4, "table: one KiB piece per wave");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
@@ -143,6 +144,9 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
   bf16_t* k_s = s_l + MF * Cf::DPAD;                     // [16][DPAD]
   bf16_t* v_s = s_l + 2 * MF * Cf::DPAD;                 // V image [16][VS]
   const uint32_t tab0 = (uint32_t)(MQ2_S * C2::W_BYTES + Cf::P * C2::S_BYTES);  // LNF tables (byte offset)
+  // LNF: this wave's row statistics, parked in LDS between the prologue and the head epilogues (in
+  // VGPRs the kernel spilled: it sits at the 256-register limit)
+  float2* const st_l = (float2*)(lds2 + tab0 + 2 * C2::TAB_BYTES + wave * C2::STAT_BYTES);
 
   const int64_t nblk_p = (positions + PWG - 1) / PWG;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
@@ -193,11 +197,8 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
   // LNF: each token row's mean and rstd (lane (fr, fq) holds row fr's channels 32 kk + 8 fq ..):
   // ones·x gives the row sum in every entry, x·x^T the Gram block whose diagonal (fr, fr) sits in
   // lane fr + 16 (fr >> 2), register fr & 3
-  float nmean[PW], rstd[PW];
 #pragma unroll
   for (int pw = 0; pw < PW; ++pw) {
-    nmean[pw] = 0.f;
-    rstd[pw] = 1.f;
     if constexpr (LNF) {
       const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
       f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, gacc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -211,8 +212,7 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
       const float sxx = __shfl(gd, fr + 16 * (fr >> 2), 64);
       constexpr float RK = 1.0f / (float)Cf::C;
       const float mean = sacc[0] * RK;
-      rstd[pw] = rsqrtf(fmaxf(fmaf(sxx, RK, -mean * mean), 0.f) + eps);
-      nmean[pw] = -mean;
+      if (fq == 0) st_l[pw * MF + fr] = make_float2(-mean, rsqrtf(fmaxf(fmaf(sxx, RK, -mean * mean), 0.f) + eps));
     }
   }
 
@@ -291,10 +291,11 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
           if constexpr (LNF) {
             const float* tb = (const float*)(lds2 + tab0 + (h & 1) * C2::TAB_BYTES);
             const float4 sv = *(const float4*)(tb + ch), pv = *(const float4*)(tb + 3 * D + fr * 3 * D + ch);
-            v[0] = fmaf(rstd[pw], fmaf(nmean[pw], sv.x, v[0]), pv.x);
-            v[1] = fmaf(rstd[pw], fmaf(nmean[pw], sv.y, v[1]), pv.y);
-            v[2] = fmaf(rstd[pw], fmaf(nmean[pw], sv.z, v[2]), pv.z);
-            v[3] = fmaf(rstd[pw], fmaf(nmean[pw], sv.w, v[3]), pv.w);
+            const float2 st = st_l[pw * MF + fr];  // (-mean, rstd) of row fr
+            v[0] = fmaf(st.y, fmaf(st.x, sv.x, v[0]), pv.x);
+            v[1] = fmaf(st.y, fmaf(st.x, sv.y, v[1]), pv.y);
+            v[2] = fmaf(st.y, fmaf(st.x, sv.z, v[2]), pv.z);
+            v[3] = fmaf(st.y, fmaf(st.x, sv.w, v[3]), pv.w);
           }
           *(uint2*)dst = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         }
