@@ -17,6 +17,7 @@ Every block has two entry points over the same kernels (see layers.py):
 """
 from __future__ import annotations
 
+import contextlib
 import math
 from collections import namedtuple
 from typing import Optional
@@ -204,20 +205,27 @@ class BasicTransformerBlock(nn.Module):
     # spatial: tokens are (image, pixel) rows
     # run_*: `n` = norm1(h) when the caller's GEMM already produced it (ops.gemm_ln: the
     # LayerNorm fused into the epilogue of the GEMM writing h, or run right after it)
-    def run_spatial(self, h, n_img, hw, ctx: Ctx, n=None):
+    def run_spatial(self, h, n_img, hw, ctx: Ctx, n=None, dup=False):
+        """dup (the CFG dedup, UNetMotionModel.forward_rows): h holds ONE guidance half; everything
+        before the cross-attention reads no text, so norm1 -> self-attention -> norm2 -> to_q run on
+        it and h, q are duplicated for the cross-attention on both halves — planned as the whole
+        batch (ops.plan_scaled), so the dedup changes no kernel choice and no bit of the result."""
         C = h.shape[1]
         d = self.dim_head
-        f1 = self.fold(1, h.shape[0]) if n is None else None
-        if f1 is not None:
-            qkv = f1.gemm(h)
-        else:
-            if n is None:
-                n = ops.layer_norm(h, *self._nrm(1))
-            qkv = ops.gemm(n, self.attn1._wqkv)
-        a = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], n_img, self.heads, hw, hw, d,
-                          scale=self.attn1.attn_scale)
-        h, n = self._out_norm(a, self.attn1, 2, h)
-        q = self.fold(2, h.shape[0]).gemm(h) if n is None else ops.gemm(n, self.attn2._wq)
+        with ops.plan_scaled(2) if dup else contextlib.nullcontext():
+            f1 = self.fold(1, h.shape[0]) if n is None else None
+            if f1 is not None:
+                qkv = f1.gemm(h)
+            else:
+                if n is None:
+                    n = ops.layer_norm(h, *self._nrm(1))
+                qkv = ops.gemm(n, self.attn1._wqkv)
+            a = ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], n_img, self.heads, hw, hw, d,
+                              scale=self.attn1.attn_scale)
+            h, n = self._out_norm(a, self.attn1, 2, h)
+            q = self.fold(2, h.shape[0]).gemm(h) if n is None else ops.gemm(n, self.attn2._wq)
+        if dup:
+            h, q, n_img = torch.cat([h, h]), torch.cat([q, q]), 2 * n_img
         kv = None if ctx.kv_cache is None else ctx.kv_cache.get(id(self.attn2))
         if kv is None:
             kv = self.attn2.project_kv(ctx.ehs_rows)
@@ -335,15 +343,20 @@ class Transformer2DModel(nn.Module):
             [BasicTransformerBlock(inner, heads, dim_head, cross_attention_dim=cross_attention_dim)])
         self.proj_out = Conv2d(inner, in_channels, 1)
 
-    def run(self, x: Act, ctx: Ctx) -> Act:
+    def run(self, x: Act, ctx: Ctx, half: Act = None) -> Act:
+        """half (the CFG dedup): x's first guidance half (x = [half; half]): the block runs on it up
+        to the cross-attention (BasicTransformerBlock.run_spatial dup)."""
         hw = x.h * x.w
-        hn = ops.group_norm(x.t, x.n, hw, self.groups, 1e-6, self.norm._g, self.norm._b)
+        src = x if half is None else half
         blk = self.transformer_blocks[0]
-        if blk.fold(1, hn.shape[0]) is not None:  # norm1 folds into the QKV GEMM
-            h = blk.run_spatial(ops.gemm(hn, self.proj_in._w, bias=self.proj_in._b), x.n, hw, ctx)
-        else:
-            h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b)
-            h = blk.run_spatial(h, x.n, hw, ctx, n=n)
+        with ops.plan_scaled(2) if half is not None else contextlib.nullcontext():
+            hn = ops.group_norm(src.t, src.n, hw, self.groups, 1e-6, self.norm._g, self.norm._b)
+            fold1 = blk.fold(1, hn.shape[0]) is not None  # norm1 folds into the QKV GEMM
+            if fold1:
+                h, n = ops.gemm(hn, self.proj_in._w, bias=self.proj_in._b), None
+            else:
+                h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b)
+        h = blk.run_spatial(h, src.n, hw, ctx, n=n, dup=half is not None)
         out = ops.gemm(h, self.proj_out._w, bias=self.proj_out._b, res=x.t)
         return Act(out, x.n, x.h, x.w)
 
@@ -451,14 +464,17 @@ class AnimateDiffTransformer3D(nn.Module):
 
 class _MotionBlockBase(nn.Module):
     def _run_layers(self, x, ctx, skips_in=None, res0=None):
-        """res0: resnets[0]'s output computed by the caller (UNetMotionModel's CFG dedup)."""
+        """res0 = (full, half): resnets[0]'s output computed by the caller on one guidance half
+        (UNetMotionModel's CFG dedup) and duplicated; attentions[0] runs on the half up to its
+        cross-attention."""
         outs = []
         attns = getattr(self, "attentions", None)
         for i, res in enumerate(self.resnets):
             skip = skips_in.pop() if skips_in is not None else None
-            x = res0 if (i == 0 and res0 is not None) else res.run(x, ctx, skip=skip)
+            dup = i == 0 and res0 is not None
+            x = res0[0] if dup else res.run(x, ctx, skip=skip)
             if attns is not None:
-                x = attns[i].run(x, ctx)
+                x = attns[i].run(x, ctx, half=res0[1] if dup else None)
             x = self.motion_modules[i].run(x, ctx)
             outs.append(x)
         return x, outs

@@ -128,14 +128,17 @@ class UNetMotionModel(nn.Module):
         res0 = None
         if ctx.cfg_dup and ctx.batch % 2 == 0:
             # CFG dedup: both halves of x_rows are the same latents and the same timestep, so
-            # conv_in and down_blocks[0].resnets[0] (nothing reads the text embeddings before
-            # the first cross-attention) run on one half; their outputs are copied to the other
+            # conv_in, down_blocks[0].resnets[0] and attentions[0] up to its cross-attention
+            # (nothing reads the text embeddings before it) run on one half; their outputs are
+            # copied to the other
+            # (planned as the whole batch, ops.plan_scaled: the same kernels, the same bits)
             half = x_rows.shape[0] // 2
             t = torch.empty(x_rows.shape[0], self.conv_in.out_channels, device=x_rows.device, dtype=torch.bfloat16)
-            ops.conv3x3(x_rows[:half], n_img // 2, h, w, self.conv_in._w, bias=self.conv_in._b, out=t[:half])
-            r1 = blocks[0].resnets[0].run(Act(t[:half], n_img // 2, h, w), ctx)
+            with ops.plan_scaled(2):
+                ops.conv3x3(x_rows[:half], n_img // 2, h, w, self.conv_in._w, bias=self.conv_in._b, out=t[:half])
+                r1 = blocks[0].resnets[0].run(Act(t[:half], n_img // 2, h, w), ctx)
             t[half:].copy_(t[:half])
-            res0 = Act(torch.cat([r1.t, r1.t]), n_img, h, w)
+            res0 = (Act(torch.cat([r1.t, r1.t]), n_img, h, w), r1)
         else:
             t, _, _ = ops.conv3x3(x_rows, n_img, h, w, self.conv_in._w, bias=self.conv_in._b)
         x = Act(t, n_img, h, w)
