@@ -224,17 +224,39 @@ class BasicTransformerBlock(nn.Module):
                               scale=self.attn1.attn_scale)
             h, n = self._out_norm(a, self.attn1, 2, h)
             q = self.fold(2, h.shape[0]).gemm(h) if n is None else ops.gemm(n, self.attn2._wq)
-        if dup:
-            h, q, n_img = torch.cat([h, h]), torch.cat([q, q]), 2 * n_img
         kv = None if ctx.kv_cache is None else ctx.kv_cache.get(id(self.attn2))
         if kv is None:
             kv = self.attn2.project_kv(ctx.ehs_rows)
             if ctx.kv_cache is not None:
                 ctx.kv_cache[id(self.attn2)] = kv
-        a = ops.attention(q, kv[:, :C], kv[:, C:], n_img, self.heads, hw, ctx.ctx_len, d,
-                          kv_div=ctx.frames, scale=self.attn2.attn_scale)
-        h, n = self._out_norm(a, self.attn2, 3, h)
+        if dup:  # the cross-attention of each guidance half on the shared q: no copy of q or h
+            L, Mh = kv.shape[0] // 2, h.shape[0]
+            a = torch.empty(2 * Mh, C, device=h.device, dtype=h.dtype)
+            for g in range(2):
+                ops.attention(q, kv[g * L:(g + 1) * L, :C], kv[g * L:(g + 1) * L, C:], n_img, self.heads, hw,
+                              ctx.ctx_len, d, kv_div=ctx.frames, scale=self.attn2.attn_scale, out=a[g * Mh:(g + 1) * Mh])
+            h, n = self._out_norm_dup(a, self.attn2, 3, h)
+        else:
+            a = ops.attention(q, kv[:, :C], kv[:, C:], n_img, self.heads, hw, ctx.ctx_len, d,
+                              kv_div=ctx.frames, scale=self.attn2.attn_scale)
+            h, n = self._out_norm(a, self.attn2, 3, h)
         return self._ff(h, n)
+
+    def _out_norm_dup(self, a, attn, i, h):
+        """_out_norm for both guidance halves of `a` on the one residual half h (the CFG dedup):
+        one GEMM per half into the halves of the output, planned as the whole batch."""
+        M, Mh = a.shape[0], h.shape[0]
+        out = torch.empty(M, h.shape[1], device=h.device, dtype=h.dtype)
+        folded = self.fold(i, M) is not None
+        n = None if folded else torch.empty_like(out)
+        with ops.plan_scaled(2):
+            for g in range(2):
+                sl = slice(g * Mh, (g + 1) * Mh)
+                if folded:
+                    ops.gemm(a[sl], attn._wo, bias=attn._bo, res=h, out=out[sl])
+                else:
+                    ops.gemm_ln(a[sl], attn._wo, *self._nrm(i), bias=attn._bo, res=h, out=out[sl], ln_out=n[sl])
+        return out, n
 
     # temporal: tokens are (video, frame, position) rows; attention over frames
     def run_temporal(self, h, batch, frames, positions, n=None):
@@ -357,7 +379,15 @@ class Transformer2DModel(nn.Module):
             else:
                 h, n = ops.gemm_ln(hn, self.proj_in._w, *blk._nrm(1), bias=self.proj_in._b)
         h = blk.run_spatial(h, src.n, hw, ctx, n=n, dup=half is not None)
-        out = ops.gemm(h, self.proj_out._w, bias=self.proj_out._b, res=x.t)
+        if half is None:
+            out = ops.gemm(h, self.proj_out._w, bias=self.proj_out._b, res=x.t)
+        else:  # the residual is the one half for both guidance halves (x = [half; half] is never built)
+            Mh = half.t.shape[0]
+            out = torch.empty(2 * Mh, half.t.shape[1], device=h.device, dtype=h.dtype)
+            with ops.plan_scaled(2):
+                for g in range(2):
+                    ops.gemm(h[g * Mh:(g + 1) * Mh], self.proj_out._w, bias=self.proj_out._b, res=half.t,
+                             out=out[g * Mh:(g + 1) * Mh])
         return Act(out, x.n, x.h, x.w)
 
     def forward(self, hidden_states, encoder_hidden_states=None, timestep=None, added_cond_kwargs=None,
@@ -472,7 +502,11 @@ class _MotionBlockBase(nn.Module):
         for i, res in enumerate(self.resnets):
             skip = skips_in.pop() if skips_in is not None else None
             dup = i == 0 and res0 is not None
-            x = res0[0] if dup else res.run(x, ctx, skip=skip)
+            if dup:  # res0 = (the full batch's shape, its first guidance half)
+                x = res0[0] if attns is not None else Act(torch.cat([res0[1].t, res0[1].t]), res0[0].n, res0[0].h,
+                                                           res0[0].w)
+            else:
+                x = res.run(x, ctx, skip=skip)
             if attns is not None:
                 x = attns[i].run(x, ctx, half=res0[1] if dup else None)
             x = self.motion_modules[i].run(x, ctx)

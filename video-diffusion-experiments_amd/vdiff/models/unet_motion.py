@@ -138,7 +138,7 @@ class UNetMotionModel(nn.Module):
                 ops.conv3x3(x_rows[:half], n_img // 2, h, w, self.conv_in._w, bias=self.conv_in._b, out=t[:half])
                 r1 = blocks[0].resnets[0].run(Act(t[:half], n_img // 2, h, w), ctx)
             t[half:].copy_(t[:half])
-            res0 = (Act(torch.cat([r1.t, r1.t]), n_img, h, w), r1)
+            res0 = (Act(None, n_img, h, w), r1)  # the full batch is never materialised
         else:
             t, _, _ = ops.conv3x3(x_rows, n_img, h, w, self.conv_in._w, bias=self.conv_in._b)
         x = Act(t, n_img, h, w)
