@@ -196,6 +196,33 @@ def test_denoise_loop_graph_matches_oracle(tiny_unet, gold, use_graph):
     assert int(loop.step_idx.item()) == 3
 
 
+@pytest.mark.parametrize("model", ["tiny", "full2"])
+def test_cfg_dedup_is_bit_exact(tiny_unet, model):
+    """The CFG dedup (DenoiseLoop.cfg_dedup: conv_in, resnets[0] and attentions[0] up to its
+    cross-attention on one guidance half, planned as the whole batch by ops.plan_scaled) changes
+    no kernel choice and no bit: the hipGraph loop with and without it is identical (tiny model at
+    4 frames; the full model at 2 frames, whose level-1 path runs v8 / flash40)."""
+    if model == "tiny":
+        unet, shape, cdim = tiny_unet, (1, 4, 4, 64, 64), tiny_unet.config["cross_attention_dim"]
+    else:
+        from vdiff.weights import materialize_synthetic
+        unet = materialize_synthetic("full", device="cuda", seed=0).prepare()
+        shape, cdim = (1, 4, 2, 64, 64), unet.config["cross_attention_dim"]
+    g = torch.Generator(device="cuda").manual_seed(5)
+    lat = torch.randn(*shape, device="cuda", generator=g)
+    ehs = torch.randn(2, 77, cdim, device="cuda", generator=g)
+    outs = []
+    for dedup in (True, False):
+        s = DDIMScheduler(beta_schedule="linear", steps_offset=1, clip_sample=False)
+        s.set_timesteps(50)
+        loop = DenoiseLoop(unet, s, lat.clone(), ehs, 7.5, use_graph=True)
+        loop.cfg_dedup = dedup
+        loop = loop.prime()
+        assert loop.graph is not None, loop.graph_error
+        outs.append(loop.run(2).clone())
+    assert torch.equal(outs[0], outs[1]), f"rel {rel_l2(outs[0], outs[1]):.2e}"
+
+
 def test_euler_scheduler_api_and_graph_loop_match_oracle(tiny_unet, gold):
     """EulerDiscreteScheduler (the reference's
     01_baseline_generation.py:76-80 configuration) behind the same surface: the
