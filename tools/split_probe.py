@@ -26,12 +26,19 @@ SHAPES = [("conv+res", 4, 32, 32, 640, 640), ("conv+res", 4, 16, 16, 1280, 1280)
           ("dense", 256, 1280, 2560), ("dense", 1024, 1280, 2560)]
 
 
+# the rank's unsplit v6 shapes (K <= 1280), where forced v6 splits K toward 2 workgroups per CU
+V6_SHAPES = [("dense+res", 1024, 1280, 1280), ("dense", 1024, 1280, 1280), ("dense+res", 256, 1280, 1280),
+             ("dense", 256, 3840, 1280), ("dense", 1024, 1280, 640), ("dense+res", 4096, 640, 640),
+             ("dense", 256, 1280, 1280)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--set", default="split", choices=["split", "v6"])
     args = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(0)
-    for sh in SHAPES:
+    for sh in (SHAPES if args.set == "split" else V6_SHAPES):
         kind = sh[0]
         if kind.startswith("conv"):
             _, n, hh, ww, N, cin = sh
