@@ -156,6 +156,7 @@ class BasicTransformerBlock(nn.Module):
         # elsewhere (levels 2-4: d = 80 / 160, no fused QKV attention) norm1 / norm2 + PE fold into
         # the QKV GEMM, the PE as the row bias W·pe[frame] (LnFold(pe=...), the v6 plan)
         self._pfold = {}
+        self._pfold_split = {}  # the kv-gather window's Q and K/V slices of a _pfold (run_temporal_gathered)
         if self.pos_embed is not None:
             c = self.attn1.dim_head ** -0.5 * math.log2(math.e)
             for i, (nrm, attn) in ((1, (self.norm1, self.attn1)), (2, (self.norm2, self.attn2))):
@@ -309,10 +310,9 @@ class BasicTransformerBlock(nn.Module):
             tf = self.temporal_fold(i, batch, frames_local, positions)
             if tf is None or tf[0] != "p":
                 return None
-            cache = self.__dict__.setdefault("_pfold_split", {})
-            if i not in cache:
-                cache[i] = (tf[1].slice(0, C), tf[1].slice(C, 3 * C))
-            fq, fkv = cache[i]
+            if i not in self._pfold_split:
+                self._pfold_split[i] = (tf[1].slice(0, C), tf[1].slice(C, 3 * C))
+            fq, fkv = self._pfold_split[i]
             return (fq, fkv) if fq.runs(M) and fkv.runs(M) else None
 
         n = None
