@@ -13,11 +13,16 @@ Switches:
   cfg_dedup  conv_in + down_blocks[0].resnets[0] once for both CFG halves (DenoiseLoop.cfg_dedup);
   mfold      the motion block's norm1 / norm2 + PE folded into the fused QKV attention (_mfold);
   pfold      the same norms + PE folded into the levels-2-4 QKV GEMM, PE as a row bias (_pfold);
-  fold_v6    the folds the plan runs on v6 (a rank's levels 2-4) against the unfolded form there."""
+  fold_v6    the folds the plan runs on v6 (a rank's levels 2-4) against the unfolded form there;
+  gn_apply   vd_gn_apply_g's blocks per instance (ops.gn_apply_blocks) as GN_APPLY_SPEC="T,R" (about
+             T blocks in all, at least R rows each) against the product choice;
+  gn_split   vd_gn_partial_g's records per image (ops.gn_image_splits) capped at GN_SPLIT_CAP
+             (default 64) and at least GN_SPLIT_ROWS (default 16) rows each."""
 from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -80,8 +85,30 @@ def set_fold_v6(unet, on, saved):  # folds the plan runs on v6 (levels 2-4 of a 
     ops.ln_fold_runs = runs
 
 
+def set_gn_apply(unet, on, saved):
+    import math
+
+    from vdiff import ops
+    orig = saved.setdefault("gn_apply_blocks", ops.gn_apply_blocks)
+    t, r = (int(v) for v in os.environ.get("GN_APPLY_SPEC", "512,1").split(","))
+
+    def blocks(n_inst, pix, C):
+        return max(1, min(max(1, pix // r), math.ceil(t / n_inst)))
+    ops.gn_apply_blocks = blocks if on else orig
+
+
+def set_gn_split(unet, on, saved):
+    from vdiff import ops
+    orig = saved.setdefault("gn_image_splits", ops.gn_image_splits)
+    cap, rows = int(os.environ.get("GN_SPLIT_CAP", "64")), int(os.environ.get("GN_SPLIT_ROWS", "16"))
+
+    def splits(pix):
+        return max(1, min(pix // rows, cap))
+    ops.gn_image_splits = splits if on else orig
+
+
 SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup, "mfold": set_mfold, "pfold": set_pfold,
-            "fold_v6": set_fold_v6}
+            "fold_v6": set_fold_v6, "gn_apply": set_gn_apply, "gn_split": set_gn_split}
 
 
 def main():

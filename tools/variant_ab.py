@@ -2,10 +2,12 @@
 that selects an experimental code path under #ifdef) against the product build.  Round 5 used it
 for VD_G2_PRIO — the v2 GEMM's MFMA stretch at raised wave priority (s_setprio 1 around the
 k-tile's MFMAs): 47.32 vs 46.79 ms at 16 frames, 12.19 vs 12.14 at 8-way, not kept
-(profiles/r05_g2_prio_refuted.txt); the #ifdef was removed with it.
+(profiles/r05_g2_prio_refuted.txt); and for VD_GN_BT=512 / 1024 (GroupNorm partial blocks of
+512 / 1024 threads: slower at every shape, profiles/r05_gn_launch_shape_refuted.txt).  The
+#ifdefs were removed with the results.
 
-    python tools/variant_ab.py --build --define VD_SOMETHING   # here (CPU): tools/diag_build/libvdiff_variant.so
-    python tools/variant_ab.py [--world 8]                     # GPU box
+    python tools/variant_ab.py --build --define VD_SOMETHING [--name v]   # here (CPU): tools/diag_build/libvdiff_v.so
+    python tools/variant_ab.py [--world 8] [--name v1,v2]                 # GPU box
 
 Both libraries are loaded in one process (the variant with RTLD_LOCAL); vdiff's calls go through
 vdiff._lib.lib(), whose handle is swapped while each arm's hipGraph is captured, then the two
@@ -23,22 +25,37 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 PKG = ROOT / "video-diffusion-experiments_amd"
 OUT = ROOT / "tools" / "diag_build"
-LIB = OUT / "libvdiff_variant.so"
 
 
-def build(define):
+def lib_path(name):
+    return OUT / f"libvdiff_{name}.so"
+
+
+def load_variant(name):
+    """The variant library loaded beside the product one, its ctypes signatures set."""
+    from vdiff import _lib as L
+    var = C.CDLL(str(lib_path(name)), mode=os.RTLD_NOW | os.RTLD_LOCAL)
+    for fn_name, (argt, rest) in L.SIGNATURES.items():
+        fn = getattr(var, fn_name)
+        fn.argtypes, fn.restype = argt, rest
+    return var
+
+
+def build(define, name):
     sys.path.insert(0, str(PKG))
     import build_ext as B
     OUT.mkdir(exist_ok=True)
-    defs = ['-DVD_BUILD_HASH="diag"', f'-DVD_BUILD_ARCH="{B.ARCH}"', f"-D{define}"]
+    defs = ['-DVD_BUILD_HASH="diag"', f'-DVD_BUILD_ARCH="{B.ARCH}"'] + [f"-D{d}" for d in define.split(",")]
     objs = []
     for src in sorted(B.CSRC.glob("*.hip")):
-        obj = OUT / (src.stem + "_variant.o")
+        obj = OUT / (src.stem + f"_{name}.o")
         subprocess.run([B.HIPCC, *B.CFLAGS, *defs, "-c", str(src), "-o", str(obj)], check=True)
         objs.append(str(obj))
-    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(LIB), *objs,
+    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(lib_path(name)), *objs,
                     "-L/opt/rocm/lib", "-lrccl"], check=True)
-    print("built", LIB)
+    for o in objs:
+        os.remove(o)
+    print("built", lib_path(name))
 
 
 def run(args):
@@ -48,10 +65,7 @@ def run(args):
     from vdiff import _lib as L
     from vdiff.weights import materialize_synthetic
     base = L.lib()
-    var = C.CDLL(str(LIB), mode=os.RTLD_NOW | os.RTLD_LOCAL)
-    for name, (argt, rest) in L.SIGNATURES.items():
-        fn = getattr(var, name)
-        fn.argtypes, fn.restype = argt, rest
+    arms = [("base", base)] + [(n, load_variant(n)) for n in args.name.split(",")]
     unet = materialize_synthetic("full", device="cuda", seed=0)
     if args.world > 1:
         from rank_emulate import EmulatedShard
@@ -64,7 +78,7 @@ def run(args):
     s.set_timesteps(50)
     ts = s.timesteps.repeat(1 + (args.rounds * args.steps + 10) // 50)
     loops = {}
-    for arm, h in (("base", base), ("variant", var)):
+    for arm, h in arms:
         L._lib = h
         lp = DenoiseLoop(unet, s, lat.clone(), ehs, 7.5, timesteps=ts, use_graph=True).prime()
         assert lp.graph is not None, lp.graph_error
@@ -88,10 +102,11 @@ def run(args):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
-    ap.add_argument("--define", default="VD_DIAG_VARIANT", help="the -D define of the variant build")
+    ap.add_argument("--define", default="VD_DIAG_VARIANT", help="the -D define(s) of the variant build, comma-separated")
+    ap.add_argument("--name", default="variant", help="variant library name(s); several, comma-separated, at run time")
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--steps", type=int, default=10)
     a = ap.parse_args()
-    build(a.define) if a.build else run(a)
+    build(a.define, a.name) if a.build else run(a)

@@ -344,6 +344,20 @@ def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, ga
     return gn_apply(x, ss, pix, silu, x1=x1, rev3=rev3)
 
 
+def gn_image_splits(pix: int) -> int:
+    """Partial records per image instance of vd_gn_partial_g: a function of the image size alone
+    (frame-sharded ranks then match the unsharded run bit for bit), at most 32 (the apply prologue
+    merges splits x groups records)."""
+    return max(1, min(pix // 16, 32))
+
+
+def gn_apply_blocks(n_inst: int, pix: int, C: int) -> int:
+    """Apply blocks per instance of vd_gn_apply_g: ~1024 in all.  Each block re-merges the
+    instance's records in its prologue, so a block's rows set how far that prologue is amortised;
+    the choice changes no bit (the apply is elementwise on the same {a, b})."""
+    return max(1, min(pix, math.ceil(1024 / n_inst)))
+
+
 def group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, out=None, n_split=None):
     """vd_gn_partial_g + vd_gn_apply_g.  Splits: <= 32 per instance (the apply prologue reads
     splits x groups records); the split count is a function of the image size alone (the same
@@ -352,15 +366,14 @@ def group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=No
     per frame x frames)."""
     _dev(x, x1, gamma, beta, out)
     C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
-    n_split = n_split or max(1, min(pix // 16, 32))
+    n_split = n_split or gn_image_splits(pix)
     ws = torch.empty(n_inst, n_split, groups, 4, device=x.device, dtype=torch.float32)
     x1p, ld1 = (_p(x1), _rows(x1)) if x1 is not None else (None, 0)
     check(lib().vd_gn_partial_g(_p(x), _rows(x), x.shape[1], x1p, ld1, C, n_inst, pix, n_split, groups, _p(ws),
                                 _stream()), "vd_gn_partial_g")
     if out is None:
         out = torch.empty(x.shape[0], C, device=x.device, dtype=BF16)
-    bpi = max(1, min(pix, math.ceil(1024 / n_inst)))
-    rows_per_blk = math.ceil(pix / bpi)
+    rows_per_blk = math.ceil(pix / gn_apply_blocks(n_inst, pix, C))
     check(lib().vd_gn_apply_g(_p(x), _rows(x), x.shape[1], x1p, ld1, C, n_inst, pix, _p(ws), n_split, groups, eps,
                               _p(gamma), _p(beta), int(silu), _p(out), _rows(out), rows_per_blk, _stream()),
           "vd_gn_apply_g")
