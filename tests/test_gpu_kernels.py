@@ -222,6 +222,48 @@ def test_gemm_v8_weight_stationary(cuda, M, N, kind):
     close_bf16(got, x)
 
 
+@pytest.mark.parametrize("M,N,K,kind", [(2, 1280, 320, "silu"), (2, 1280, 1280, "bias"), (2, 20160, 1280, "f32"),
+                                        (1, 52, 264, "res"), (5, 1292, 776, "rowbias"), (16, 4096, 2560, "gelu"),
+                                        (3, 640, 96, "nobias")])
+def test_gemm_v9_skinny(cuda, M, N, K, kind):
+    """v9 (M <= 16: the time-embedding MLP and the resnets' concatenated time_emb_proj): the plan
+    takes it; every epilogue it carries, a partial last 16-column block (N = 52, 1292) and a
+    partial last 32-k step (K = 264, 776, 96); bit-equal to v1, whose MFMA chain it keeps, and
+    within bf16 output rounding of fp32."""
+    assert ops.gemm_plan_of(GemmDesc(a0=256, lda0=K, k0=K, a_mode=0, w=256, ldw=K, M=M, N=N, K=K, out=256,
+                                     ldc=N))[0] == 9
+    a = rnd(M, K)
+    w = rnd(N, K, std=K ** -0.5)
+    bias = None if kind == "nobias" else torch.randn(N, device=cuda)
+    kw = {}
+    if kind in ("silu", "gelu"):
+        kw["act"] = ops.ACT_SILU if kind == "silu" else ops.ACT_GELU
+    elif kind == "f32":
+        kw["out_f32"] = True
+    elif kind == "res":
+        kw["res"] = rnd(M, N)
+    elif kind == "rowbias":
+        kw["rowbias"], kw["rb_div"] = torch.randn(M, N, device=cuda), 1
+    got = ops.gemm(a, w, bias=bias, **kw)
+    with ops.gemm_plan(path=1):
+        ref = ops.gemm(a, w, bias=bias, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), f"v9 != v1 bits: max |diff| {(got.float() - ref.float()).abs().max().item()}"
+    x = a.float() @ w.float().T + (bias if bias is not None else 0)
+    if kind == "res":
+        x = x + kw["res"].float()
+    elif kind == "rowbias":
+        x = x + kw["rowbias"]
+    elif kind == "silu":
+        x = F.silu(x)
+    elif kind == "gelu":
+        x = F.gelu(x)
+    if kind == "f32":
+        close_f32(got, x, rtol=1e-4, atol=1e-4)
+    else:
+        close_bf16(got, x)
+
+
 def test_gemm_v8_strided_operands(cuda):
     """v8 on column-slice views: A with lda0 = 384, out and residual slices of wider
     buffers (ldc = ld_res = N + 160) — v8's own A / store / residual address arithmetic — bit-equal

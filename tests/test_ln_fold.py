@@ -102,6 +102,24 @@ def _plan(d):
     return k.value, sp.value
 
 
+def test_plan_skinny_m_takes_v9():
+    """vd_gemm_plan: M <= 16 dense rows (the time-embedding MLP, M = the UNet batch) run on v9
+    (bit-identical to v1); a forced v1, a GEGLU, a folded LayerNorm or M = 17 keep the other plans."""
+    d = _desc(2, 1280, K=1280)
+    d.ln_fold_s = None
+    assert _plan(d) == (9, 1)
+    d.M = 16
+    assert _plan(d) == (9, 1)
+    d.M = 17
+    assert _plan(d)[0] == 1
+    d.M, d.path = 2, 1
+    assert _plan(d)[0] == 1
+    g = _desc(2, 2560, K=1280, act=ops.ACT_GEGLU)
+    g.ln_fold_s = None
+    assert _plan(g)[0] == 1
+    assert _plan(_desc(2, 1280, K=1280))[0] == 0  # a fold at M = 2: no kernel, the unfolded form
+
+
 def test_plan_folds_on_v8_and_unsplit_v6():
     """vd_gemm_plan: a folded LayerNorm runs on v8 where the automatic plan would take v8
     (M >= 16384, K = 320, N a multiple of 160) or where v8 is forced (path 8, M >= 4096), and on

@@ -16,6 +16,7 @@ Switches:
   fold_v6    the folds the plan runs on v6 (a rank's levels 2-4) against the unfolded form there;
   gn_apply   vd_gn_apply_g's blocks per instance (ops.gn_apply_blocks) as GN_APPLY_SPEC="T,R" (about
              T blocks in all, at least R rows each) against the product choice;
+  skinny     the time-embedding GEMMs (M = 2) on v9 against v1 (forced path 1);
   gn_split   vd_gn_partial_g's records per image (ops.gn_image_splits) capped at GN_SPLIT_CAP
              (default 64) and at least GN_SPLIT_ROWS (default 16) rows each."""
 from __future__ import annotations
@@ -107,8 +108,18 @@ def set_gn_split(unet, on, saved):
     ops.gn_image_splits = splits if on else orig
 
 
+def set_skinny(unet, on, saved):
+    from vdiff import ops
+    orig = saved.setdefault("make_ctx", unet.make_ctx)
+
+    def make_ctx_v1(*a, **k):
+        with ops.gemm_plan(path=1):
+            return orig(*a, **k)
+    unet.make_ctx = orig if on else make_ctx_v1
+
+
 SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup, "mfold": set_mfold, "pfold": set_pfold,
-            "fold_v6": set_fold_v6, "gn_apply": set_gn_apply, "gn_split": set_gn_split}
+            "fold_v6": set_fold_v6, "gn_apply": set_gn_apply, "gn_split": set_gn_split, "skinny": set_skinny}
 
 
 def main():

@@ -404,6 +404,54 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const vd_gemm_desc d) {
     gemm_epilogue<MB, NB>(d, acc, (int)m0 + wm * MB * 16, (int)n0 + wn * (BN / 2), lane);
 }
 
+// ============================================================================ v9
+// Skinny GEMM, M <= 16: the time-embedding MLP and the resnets' concatenated time_emb_proj (M = the
+// UNet batch, 2 with CFG) — weight streaming, HBM-bound.  v1's 128 x 160 tiles put these on 8 / 126
+// workgroups (22 / 31 us per launch at N = 1280 / 20160).  One wave owns 16 output columns and all
+// of K; its MFMA chain is v1's (C^T = W . A^T by v_mfma_f32_16x16x32_bf16, k ascending, one
+// accumulator, zero-filled past K), so the result is bit-identical to v1's.  The fragments come
+// straight from global memory (no LDS): lane (fr, fq) holds W row n0 + fr and A row fr (zero for
+// fr >= M), k slice 8*fq .. +7 of each 32-k step; G9_U steps of loads are in flight ahead of the
+// MFMAs that consume the previous G9_U.  The epilogue is gemm_epilogue's narrow path (MB = NB = 1).
+constexpr int G9_NW = 4, G9_U = 8, G9_MMAX = 16;
+__global__ __launch_bounds__(G9_NW * 64) void gemm9_kernel(const vd_gemm_desc d) {
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int n0 = (blockIdx.x * G9_NW + (threadIdx.x >> 6)) * 16;
+  const int N = (int)d.N, M = (int)d.M, K = (int)d.K;
+  if (n0 >= N) return;  // wave-uniform; no barriers below
+  const bool nok = n0 + fr < N, mok = fr < M;
+  const bf16_t* wp = (const bf16_t*)d.w + (int64_t)(nok ? n0 + fr : 0) * d.ldw + 8 * fq;
+  const bf16_t* ap = (const bf16_t*)d.a0 + (int64_t)(mok ? fr : 0) * d.lda0 + 8 * fq;
+  const int nsteps = (K + 31) / 32;
+  uint4 wc[G9_U], ac[G9_U], wn[G9_U], an[G9_U];
+  auto load = [&](int s0, uint4 (&wv)[G9_U], uint4 (&av)[G9_U]) {
+#pragma unroll
+    for (int u = 0; u < G9_U; ++u) {
+      const int k = (s0 + u) * 32;
+      const bool kok = k + 8 * fq < K;
+      wv[u] = nok && kok ? *(const uint4*)(wp + k) : make_uint4(0, 0, 0, 0);
+      av[u] = mok && kok ? *(const uint4*)(ap + k) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  f32x4 acc[1][1] = {{f32x4{0.f, 0.f, 0.f, 0.f}}};
+  load(0, wc, ac);
+  for (int s0 = 0; s0 < nsteps; s0 += G9_U) {
+    if (s0 + G9_U < nsteps) load(s0 + G9_U, wn, an);
+#pragma unroll
+    for (int u = 0; u < G9_U; ++u)
+      if (s0 + u < nsteps)
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wc[u]),
+                                                             __builtin_bit_cast(bf16x8, ac[u]), acc[0][0], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < G9_U; ++u) {
+      wc[u] = wn[u];
+      ac[u] = an[u];
+    }
+  }
+  gemm_epilogue<1, 1>(d, acc, 0, n0, lane);
+}
+
 // ============================================================================ v2
 // LDS-DMA GEMM: BM = 256, BN in {128, 160}, BK = 64, 512 threads = 8 waves as
 // 4(M) x 2(N), each wave 64 x BN/2.  Operands reach LDS by `buffer_load_dwordx4
@@ -2221,6 +2269,12 @@ int launch(const vd_gemm_desc& d, hipStream_t s) {
   return vd_launch_status();
 }
 
+int launch9(const vd_gemm_desc& d, hipStream_t s) {
+  const int64_t waves = (d.N + 15) / 16;
+  hipLaunchKernelGGL(gemm9_kernel, dim3((unsigned)((waves + G9_NW - 1) / G9_NW)), dim3(G9_NW * 64), 0, s, d);
+  return vd_launch_status();
+}
+
 template <int BN, int WM, int WN, int STAGES>
 int launch4(const vd_gemm_desc& d, hipStream_t s, uint32_t a0b, uint32_t a1b, uint32_t wb, int split) {
   using C = G4<BN, WM, WN, STAGES>;
@@ -2364,6 +2418,12 @@ Plan plan_core(const vd_gemm_desc& d) {
   Plan p;
   int path = d.path;
   const int64_t M = d.plan_m > 0 ? d.plan_m : d.M;  // the row count the plan is made for
+  // v9 (M <= 16 rows, dense, one operand, no GEGLU / LayerNorm / row map): bit-identical to v1
+  if (path == 0 && M <= G9_MMAX && d.M <= G9_MMAX && d.a_mode == VD_A_DENSE && d.k0 == d.K &&
+      d.act != VD_ACT_GEGLU && !d.ln_out && !d.ln_fold_s && !d.rmap_inner) {
+    p.ver = 9;
+    return p;
+  }
   if (path == 1 || d.K % G4_BK || d.k0 % G4_BK || M < G6_BM || (d.N < 64 && d.N > 32)) return p;
   const int64_t a_rows = d.a_mode == VD_A_CONV3X3
                              ? (int64_t)d.n_img / d.frames_out * d.frames_in * d.h_in * d.w_in : d.M;
@@ -2653,6 +2713,7 @@ extern "C" int vd_gemm(const vd_gemm_desc* dp, vd_stream_t stream) {
     return vd_layernorm(d.out, d.ldc, d.M, d.N, d.ln_gamma, d.ln_beta, d.ln_eps, d.ln_pe, d.ln_pe_div,
                         d.ln_pe_period, d.ln_out, d.ld_ln, stream);
   }
+  if (p.ver == 9) return launch9(d, s);
   if (p.ver == 8) return launch8(d, s, p.a0b, p.wb);
   if (p.ver == 3) return launch3(d, s, p.a0b, p.a1b, p.wb, p.split);
   if (p.ver == 6) return launch6(d, s, p.a0b, p.a1b, p.wb, p.split);
