@@ -197,6 +197,13 @@ int vd_gn_apply_g(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int6
                   int32_t n_split_total, int32_t groups, float eps, const float* gamma,
                   const float* beta, int32_t silu, void* y, int64_t ldy, int64_t rows_per_blk,
                   vd_stream_t stream);
+/* vd_gn_finalize over vd_gn_partial_g's per-group records (ws: n_inst*n_split_total*groups
+ * float4, e.g. all-gathered from frame-sharded ranks) -> scale_shift[inst][C] {a, b}: the
+ * motion-module norm, whose video instances need more records than vd_gn_apply_g's prologue
+ * merges (round 5: C/groups times fewer records than vd_gn_partial's per-channel ones). */
+int vd_gn_finalize_g(const float* ws, int64_t n_inst, int32_t n_split_total, int64_t C,
+                     int32_t groups, float eps, const float* gamma, const float* beta,
+                     float* scale_shift, vd_stream_t stream);
 
 /* ---------------------------------------------------------------- LayerNorm
  * BasicTransformerBlock.norm1/2/3 (eps 1e-5) over the last dim of bf16 rows,

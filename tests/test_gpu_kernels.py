@@ -417,6 +417,32 @@ def test_gemm_row_map(cuda, path, M, N, K):
     close_bf16(got, rev3_reference(a.float() @ w.float().T + bias, n1, n2, inner) + res.float())
 
 
+def test_gn_finalize_group_records(cuda):
+    """vd_gn_finalize_g (the motion norm on vd_gn_partial_g's per-group records): fp64 GroupNorm
+    statistics over (C/G, F, H, W) within fp32 rounding, and the records of a video's frames made
+    in two frame halves and concatenated along the split axis — what a 2-way frame-sharded
+    all-gather hands over — give the whole video's scale / shift bit for bit."""
+    B, F, HW, C, G, eps = 2, 4, 1024, 640, 32, 1e-6
+    x = bf(torch.randn(B * F * HW, C, device=cuda) * 2 + 0.5)
+    g = 1 + 0.1 * torch.randn(C, device=cuda)
+    b = 0.1 * torch.randn(C, device=cuda)
+    sp = ops.gn_splits_per_frame(HW)
+    ss = ops.gn_finalize_g(ops.gn_partial_g(x, C, B, F * HW, F * sp, G), C, eps, g, b)
+    xv = x.view(B, F, HW, C)
+    halves = [xv[:, i * F // 2:(i + 1) * F // 2].reshape(-1, C).contiguous() for i in range(2)]
+    ws2 = torch.cat([ops.gn_partial_g(h, C, B, F // 2 * HW, F // 2 * sp, G) for h in halves], 1)
+    ss2 = ops.gn_finalize_g(ws2, C, eps, g, b)
+    torch.cuda.synchronize()
+    assert torch.equal(ss, ss2)
+    xd = x.double().view(B, F * HW, G, C // G)
+    mean = xd.mean((1, 3))
+    rstd = (xd.var((1, 3), unbiased=False) + eps).rsqrt()
+    a = (rstd[:, :, None] * g.double().view(G, C // G)).reshape(B, C)
+    sh = b.double() - mean.repeat_interleave(C // G, 1) * a
+    torch.testing.assert_close(ss[..., 0].double(), a, rtol=2e-5, atol=0)
+    torch.testing.assert_close(ss[..., 1].double(), sh, rtol=0, atol=2e-5 * a.abs().max().item())
+
+
 def test_gn_apply_rev3(cuda):
     """vd_gn_apply_rev3: the motion norm writing the all-to-all's send order directly equals the
     plain apply followed by the row permutation, bit for bit."""

@@ -16,6 +16,8 @@ Switches:
   fold_v6    the folds the plan runs on v6 (a rank's levels 2-4) against the unfolded form there;
   gn_apply   vd_gn_apply_g's blocks per instance (ops.gn_apply_blocks) as GN_APPLY_SPEC="T,R" (about
              T blocks in all, at least R rows each) against the product choice;
+  gn_grec    the motion norm on per-group records (vd_gn_partial_g + vd_gn_finalize_g) against
+             per-channel ones (vd_gn_partial + vd_gn_finalize);
   skinny     the time-embedding GEMMs (M = 2) on v9 against v1 (forced path 1);
   gn_split   vd_gn_partial_g's records per image (ops.gn_image_splits) capped at GN_SPLIT_CAP
              (default 64) and at least GN_SPLIT_ROWS (default 16) rows each."""
@@ -118,8 +120,25 @@ def set_skinny(unet, on, saved):
     unet.make_ctx = orig if on else make_ctx_v1
 
 
+def set_gn_grec(unet, on, saved):
+    from vdiff import ops
+    orig = saved.setdefault("group_norm", ops.group_norm)
+
+    def per_channel(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, gather=None, two_pass=True,
+                    n_split=None, rev3=None):
+        if two_pass and gather is None and rev3 is None:
+            return orig(x, n_inst, pix, groups, eps, gamma, beta, silu=silu, x1=x1, n_split=n_split)
+        C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
+        ws = ops.gn_partial(x, C, n_inst, pix, n_split or ops.gn_splits(n_inst, pix), x1=x1)
+        if gather is not None:
+            ws = gather(ws)
+        ss = ops.gn_finalize(ws, groups, eps, gamma, beta)
+        return ops.gn_apply(x, ss, pix, silu, x1=x1, rev3=rev3)
+    ops.group_norm = orig if on else per_channel
+
+
 SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup, "mfold": set_mfold, "pfold": set_pfold,
-            "fold_v6": set_fold_v6, "gn_apply": set_gn_apply, "gn_split": set_gn_split, "skinny": set_skinny}
+            "fold_v6": set_fold_v6, "gn_apply": set_gn_apply, "gn_split": set_gn_split, "skinny": set_skinny, "gn_grec": set_gn_grec}
 
 
 def main():
@@ -129,6 +148,7 @@ def main():
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--swap", action="store_true", help="capture and replay the off arm first (order-bias check)")
     args = ap.parse_args()
     unet = materialize_synthetic("full", device="cuda", seed=0)
     if args.world > 1:
@@ -142,7 +162,7 @@ def main():
     s.set_timesteps(50)
     ts = s.timesteps.repeat(1 + (args.rounds * args.steps + 10) // 50)
     saved, loops = {}, {}
-    for arm in ("on", "off"):
+    for arm in (("off", "on") if args.swap else ("on", "off")):
         hook = SWITCHES[args.switch](unet, arm == "on", saved)
         lp = DenoiseLoop(unet, s, lat.clone(), ehs, 7.5, timesteps=ts, use_graph=True)
         if callable(hook):

@@ -177,7 +177,9 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
 }
 
 // One block per (instance, group): Chan-combine the n_split x (C/groups) records
-// of the group in parallel (per-thread, then an LDS tree), then write {a, b}.
+// of the group in parallel (per-thread, then an LDS tree), then write {a, b}.  GREC: the
+// records are vd_gn_partial_g's, one per (instance, split, group) — C/groups times fewer.
+template <bool GREC>
 __global__ __launch_bounds__(NT) void gn_finalize_kernel(const float4* ws, int n_split, int64_t C,
                                                          int groups, float eps, const float* gamma,
                                                          const float* beta, float2* ss) {
@@ -185,8 +187,10 @@ __global__ __launch_bounds__(NT) void gn_finalize_kernel(const float4* ws, int n
   const int inst = blockIdx.x / groups;
   const int g = blockIdx.x % groups;
   const int cpg = (int)(C / groups);
-  const int nrec = n_split * cpg;
-  const float4* src = ws + (int64_t)inst * n_split * C + (int64_t)g * cpg;
+  const int rpg = GREC ? 1 : cpg;  // records per (split, group)
+  const int64_t rstride = GREC ? groups : C;
+  const int nrec = n_split * rpg;
+  const float4* src = ws + (int64_t)inst * n_split * rstride + (int64_t)g * rpg;
   // 4 independent accumulators: 4 record loads in flight and 4 merge chains
   float n[4] = {0.f, 0.f, 0.f, 0.f}, mean[4] = {0.f, 0.f, 0.f, 0.f}, m2[4] = {0.f, 0.f, 0.f, 0.f};
   for (int r0 = threadIdx.x; r0 < nrec; r0 += 4 * NT) {
@@ -194,8 +198,8 @@ __global__ __launch_bounds__(NT) void gn_finalize_kernel(const float4* ws, int n
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int r = r0 + u * NT;
-      const int s = r / cpg, q = r - s * cpg;
-      v[u] = r < nrec ? src[(int64_t)s * C + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int s = r / rpg, q = r - s * rpg;
+      v[u] = r < nrec ? src[(int64_t)s * rstride + q] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) chan_merge(n[u], mean[u], m2[u], v[u].x, v[u].y, v[u].z);
@@ -532,7 +536,18 @@ extern "C" int vd_gn_finalize(const float* ws, int64_t n_inst, int32_t n_split_t
                               float* scale_shift, vd_stream_t stream) {
   VD_CHECK_ARG(ws && gamma && beta && scale_shift && n_inst > 0 && n_split_total > 0);
   VD_CHECK_ARG(groups > 0 && C % groups == 0 && n_inst * groups < 0x7fffffff);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3((unsigned)(n_inst * groups)), dim3(NT), 0,
+  hipLaunchKernelGGL(gn_finalize_kernel<false>, dim3((unsigned)(n_inst * groups)), dim3(NT), 0,
+                     (hipStream_t)stream, (const float4*)ws, n_split_total, C, groups, eps, gamma,
+                     beta, (float2*)scale_shift);
+  return vd_launch_status();
+}
+
+extern "C" int vd_gn_finalize_g(const float* ws, int64_t n_inst, int32_t n_split_total, int64_t C,
+                                int32_t groups, float eps, const float* gamma, const float* beta,
+                                float* scale_shift, vd_stream_t stream) {
+  VD_CHECK_ARG(ws && gamma && beta && scale_shift && n_inst > 0 && n_split_total > 0);
+  VD_CHECK_ARG(groups > 0 && C % groups == 0 && n_inst * groups < 0x7fffffff);
+  hipLaunchKernelGGL(gn_finalize_kernel<true>, dim3((unsigned)(n_inst * groups)), dim3(NT), 0,
                      (hipStream_t)stream, (const float4*)ws, n_split_total, C, groups, eps, gamma,
                      beta, (float2*)scale_shift);
   return vd_launch_status();

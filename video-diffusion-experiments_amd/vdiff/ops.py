@@ -308,6 +308,24 @@ def gn_finalize(ws, groups, eps, gamma, beta):
     return ss
 
 
+def gn_partial_g(x, C, n_inst, pix, n_split, groups, x1=None):
+    """vd_gn_partial_g: one {n, mean, M2} record per (instance, split, group)."""
+    _dev(x, x1)
+    ws = torch.empty(n_inst, n_split, groups, 4, device=x.device, dtype=torch.float32)
+    x1p, ld1 = (_p(x1), _rows(x1)) if x1 is not None else (None, 0)
+    check(lib().vd_gn_partial_g(_p(x), _rows(x), x.shape[1], x1p, ld1, C, n_inst, pix, n_split, groups, _p(ws),
+                                _stream()), "vd_gn_partial_g")
+    return ws
+
+
+def gn_finalize_g(ws, C, eps, gamma, beta):
+    n_inst, n_split, groups, _ = ws.shape
+    ss = torch.empty(n_inst, C, 2, device=ws.device, dtype=torch.float32)
+    check(lib().vd_gn_finalize_g(_p(ws), n_inst, n_split, C, groups, eps, _p(gamma), _p(beta), _p(ss),
+                                 _stream()), "vd_gn_finalize_g")
+    return ss
+
+
 def gn_apply(x, ss, pix, silu, x1=None, out=None, rev3=None):
     """rev3 = (n1, n2, inner): input row m lands at output row rev3(m) (vd_gn_apply_rev3)."""
     _dev(x, x1, ss)
@@ -335,12 +353,20 @@ def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, ga
     blocks on an arrival counter) was slower at every image norm of the step and is gone
     (round 4, profiles/r04_gn_one_launch_refuted.txt)."""
     C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
-    if two_pass and gather is None and rev3 is None and C <= 2560 and 256 % groups == 0:
+    grec = C <= 2560 and 256 % groups == 0
+    if two_pass and gather is None and rev3 is None and grec:
         return group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=silu, x1=x1)
-    ws = gn_partial(x, C, n_inst, pix, n_split or gn_splits(n_inst, pix), x1=x1)
-    if gather is not None:
-        ws = gather(ws)
-    ss = gn_finalize(ws, groups, eps, gamma, beta)
+    n_split = n_split or gn_splits(n_inst, pix)
+    if grec:  # per-group records (round 5: C/groups times fewer for the gather and the finalize)
+        ws = gn_partial_g(x, C, n_inst, pix, n_split, groups, x1=x1)
+        if gather is not None:
+            ws = gather(ws)
+        ss = gn_finalize_g(ws, C, eps, gamma, beta)
+    else:
+        ws = gn_partial(x, C, n_inst, pix, n_split, x1=x1)
+        if gather is not None:
+            ws = gather(ws)
+        ss = gn_finalize(ws, groups, eps, gamma, beta)
     return gn_apply(x, ss, pix, silu, x1=x1, rev3=rev3)
 
 
@@ -367,10 +393,8 @@ def group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=No
     _dev(x, x1, gamma, beta, out)
     C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
     n_split = n_split or gn_image_splits(pix)
-    ws = torch.empty(n_inst, n_split, groups, 4, device=x.device, dtype=torch.float32)
+    ws = gn_partial_g(x, C, n_inst, pix, n_split, groups, x1=x1)
     x1p, ld1 = (_p(x1), _rows(x1)) if x1 is not None else (None, 0)
-    check(lib().vd_gn_partial_g(_p(x), _rows(x), x.shape[1], x1p, ld1, C, n_inst, pix, n_split, groups, _p(ws),
-                                _stream()), "vd_gn_partial_g")
     if out is None:
         out = torch.empty(x.shape[0], C, device=x.device, dtype=BF16)
     rows_per_blk = math.ceil(pix / gn_apply_blocks(n_inst, pix, C))
