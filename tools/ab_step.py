@@ -18,6 +18,8 @@ Switches:
              T blocks in all, at least R rows each) against the product choice;
   gn_grec    the motion norm on per-group records (vd_gn_partial_g + vd_gn_finalize_g) against
              per-channel ones (vd_gn_partial + vd_gn_finalize);
+  gn_mframe  the motion norm's records per frame (ops.gn_splits_per_frame) capped at GN_MFRAME_CAP
+             (default 64) against the product choice;
   skinny     the time-embedding GEMMs (M = 2) on v9 against v1 (forced path 1);
   gn_split   vd_gn_partial_g's records per image (ops.gn_image_splits) capped at GN_SPLIT_CAP
              (default 64) and at least GN_SPLIT_ROWS (default 16) rows each."""
@@ -137,8 +139,18 @@ def set_gn_grec(unet, on, saved):
     ops.group_norm = orig if on else per_channel
 
 
+def set_gn_mframe(unet, on, saved):
+    from vdiff import ops
+    orig = saved.setdefault("gn_splits_per_frame", ops.gn_splits_per_frame)
+    cap = int(os.environ.get("GN_MFRAME_CAP", "64"))
+
+    def per_frame(hw):
+        return max(1, min(hw // 16, cap))
+    ops.gn_splits_per_frame = per_frame if on else orig
+
+
 SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup, "mfold": set_mfold, "pfold": set_pfold,
-            "fold_v6": set_fold_v6, "gn_apply": set_gn_apply, "gn_split": set_gn_split, "skinny": set_skinny, "gn_grec": set_gn_grec}
+            "fold_v6": set_fold_v6, "gn_apply": set_gn_apply, "gn_split": set_gn_split, "skinny": set_skinny, "gn_grec": set_gn_grec, "gn_mframe": set_gn_mframe}
 
 
 def main():
