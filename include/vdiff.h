@@ -197,6 +197,15 @@ int vd_gn_apply_g(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int6
                   int32_t n_split_total, int32_t groups, float eps, const float* gamma,
                   const float* beta, int32_t silu, void* y, int64_t ldy, int64_t rows_per_blk,
                   vd_stream_t stream);
+/* One-launch GroupNorm (+SiLU) for small image instances (round 5): one workgroup per (instance,
+ * chunk of whole groups) holding its rows in registers, exact two-pass statistics, then the apply.
+ * Taken when C / groups is a multiple of 8 and a chunk's rows fit 16 pieces of 8 channels per
+ * thread (the UNet's levels 3-4 and mid block: pix <= 256); otherwise VD_EUNSUPPORTED, decided
+ * from (pix_per_inst, C, groups) before any operand is read — callers may probe with null pointers
+ * (vdiff.ops.gn_small_chunk mirrors the rule). */
+int vd_gn_small(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1, int64_t C,
+                int64_t n_inst, int64_t pix_per_inst, int32_t groups, float eps, const float* gamma,
+                const float* beta, int32_t silu, void* y, int64_t ldy, vd_stream_t stream);
 /* vd_gn_finalize over vd_gn_partial_g's per-group records (ws: n_inst*n_split_total*groups
  * float4, e.g. all-gathered from frame-sharded ranks) -> scale_shift[inst][C] {a, b}: the
  * motion-module norm, whose video instances need more records than vd_gn_apply_g's prologue

@@ -417,6 +417,32 @@ def test_gemm_row_map(cuda, path, M, N, K):
     close_bf16(got, rev3_reference(a.float() @ w.float().T + bias, n1, n2, inner) + res.float())
 
 
+@pytest.mark.parametrize("n,pix,C,c0,silu", [(4, 256, 1280, 1280, True), (4, 64, 1280, 1280, True),
+                                           (2, 64, 2560, 1280, True), (3, 256, 2560, 1280, True),
+                                           (4, 256, 1280, 1280, False), (1, 100, 1280, 1280, True)])
+def test_gn_small_one_launch(cuda, n, pix, C, c0, silu):
+    """vd_gn_small (the one-launch GroupNorm of levels 3-4 / mid, incl. the up blocks' skip concat
+    x0 | x1 and a ragged row count) against fp64 GroupNorm (+SiLU) at bf16 output rounding, and
+    against the two-launch path it replaces."""
+    G, eps = 32, 1e-5
+    assert ops.gn_small_chunk(pix, C, G)
+    x0 = bf(torch.randn(n * pix, c0, device=cuda) * 1.5 + 0.7)
+    x1 = bf(torch.randn(n * pix, C - c0, device=cuda) - 0.3) if c0 < C else None
+    g = 1 + 0.2 * torch.randn(C, device=cuda)
+    b = 0.2 * torch.randn(C, device=cuda)
+    got = ops.group_norm(x0, n, pix, G, eps, g, b, silu=silu, x1=x1)
+    two = ops.group_norm_2pass(x0, n, pix, G, eps, g, b, silu=silu, x1=x1)
+    torch.cuda.synchronize()
+    x = (torch.cat([x0, x1], 1) if x1 is not None else x0).double().view(n, pix, G, C // G)
+    mean, var = x.mean((1, 3), keepdim=True), x.var((1, 3), unbiased=False, keepdim=True)
+    ref = ((x - mean) / (var + eps).sqrt()).view(n * pix, C) * g.double() + b.double()
+    if silu:
+        ref = F.silu(ref)
+    close_bf16(got, ref)
+    close_bf16(two, ref)
+    assert (got.float() - two.float()).abs().max().item() <= 2 * 2 ** -7 * ref.abs().max().item()
+
+
 def test_gn_finalize_group_records(cuda):
     """vd_gn_finalize_g (the motion norm on vd_gn_partial_g's per-group records): fp64 GroupNorm
     statistics over (C/G, F, H, W) within fp32 rounding, and the records of a video's frames made

@@ -102,6 +102,22 @@ def _plan(d):
     return k.value, sp.value
 
 
+def test_gn_small_rule_mirrors_library():
+    """vd_gn_small decides from (pix, C, groups) before reading any operand: with null pointers it
+    returns VD_EUNSUPPORTED exactly where vdiff.ops.gn_small_chunk says 0, and VD_EINVAL (the
+    null operands) where the mirror takes the shape; the UNet's levels 3-4 / mid norms are taken,
+    levels 1-2 (C / groups = 10, 20) are not."""
+    cases = [(pix, C) for pix in (16, 64, 256, 1024, 4096, 100) for C in (320, 640, 960, 1280, 1920, 2560)]
+    for pix, C in cases:
+        rc = L.lib().vd_gn_small(None, C, C, None, 0, C, 4, pix, 32, 1e-5, None, None, 1, None, C, None)
+        taken = ops.gn_small_chunk(pix, C, 32)
+        assert rc == (1000 if taken else 1001), (pix, C, rc, taken)
+    assert ops.gn_small_chunk(256, 1280, 32) == 80 and ops.gn_small_chunk(64, 1280, 32) == 320
+    assert ops.gn_small_chunk(64, 2560, 32) == 320 and ops.gn_small_chunk(256, 2560, 32) == 80
+    assert ops.gn_small_chunk(4096, 320, 32) == 0 and ops.gn_small_chunk(1024, 640, 32) == 0
+    assert ops.gn_small_chunk(256, 1920, 32) == 0   # C / groups = 60: a piece would straddle groups
+
+
 def test_plan_skinny_m_takes_v9():
     """vd_gemm_plan: M <= 16 dense rows (the time-embedding MLP, M = the UNet batch) run on v9
     (bit-identical to v1); a forced v1, a GEGLU, a folded LayerNorm or M = 17 keep the other plans."""

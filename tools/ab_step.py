@@ -20,6 +20,7 @@ Switches:
              per-channel ones (vd_gn_partial + vd_gn_finalize);
   gn_mframe  the motion norm's records per frame (ops.gn_splits_per_frame) capped at GN_MFRAME_CAP
              (default 64) against the product choice;
+  gn_small   the one-launch small-image GroupNorm (vd_gn_small) against the two-launch form there;
   skinny     the time-embedding GEMMs (M = 2) on v9 against v1 (forced path 1);
   gn_split   vd_gn_partial_g's records per image (ops.gn_image_splits) capped at GN_SPLIT_CAP
              (default 64) and at least GN_SPLIT_ROWS (default 16) rows each."""
@@ -149,8 +150,14 @@ def set_gn_mframe(unet, on, saved):
     ops.gn_splits_per_frame = per_frame if on else orig
 
 
+def set_gn_small(unet, on, saved):
+    from vdiff import ops
+    orig = saved.setdefault("gn_small_chunk", ops.gn_small_chunk)
+    ops.gn_small_chunk = orig if on else (lambda pix, C, groups: 0)
+
+
 SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup, "mfold": set_mfold, "pfold": set_pfold,
-            "fold_v6": set_fold_v6, "gn_apply": set_gn_apply, "gn_split": set_gn_split, "skinny": set_skinny, "gn_grec": set_gn_grec, "gn_mframe": set_gn_mframe}
+            "fold_v6": set_fold_v6, "gn_apply": set_gn_apply, "gn_split": set_gn_split, "skinny": set_skinny, "gn_grec": set_gn_grec, "gn_mframe": set_gn_mframe, "gn_small": set_gn_small}
 
 
 def main():

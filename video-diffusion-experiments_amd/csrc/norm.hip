@@ -350,6 +350,98 @@ __global__ __launch_bounds__(NT) void gn_apply_g_kernel(const bf16_t* x0, int64_
   }
 }
 
+// One-launch GroupNorm (+SiLU) for small image instances (levels 3-4 and the mid block, where the
+// two-launch form is two ~10 us launch floors on a few hundred KB): one workgroup per (instance,
+// chunk of CG channels = whole groups), the chunk's rows held in registers (<= GNS_MAXR 16-byte
+// pieces per thread), exact two-pass statistics per group (the mean, then the sum of squared
+// deviations, both summed in a fixed order), then the apply — the rows are read once.  Thread t
+// owns the 8-channel piece c8 = t % n8 of rows t / n8 + k * rpt (cpg % 8 == 0: one group each).
+constexpr int GNS_MAXR = 16, GNS_GMAX = 32;
+__global__ __launch_bounds__(NT) void gn_small_kernel(const bf16_t* x0, int64_t ldx0, int64_t c0, const bf16_t* x1,
+                                                      int64_t ldx1, int64_t C, int pix, int CG, int cpg, float eps,
+                                                      const float* gamma, const float* beta, int silu, bf16_t* y,
+                                                      int64_t ldy) {
+  __shared__ float red[NT];
+  __shared__ float gmean[GNS_GMAX], grstd[GNS_GMAX];
+  const int n8 = CG / 8, rpt = NT / n8, ngl = CG / cpg, tpg = cpg / 8;
+  const int nchunk = (int)(C / CG);
+  const int inst = blockIdx.x / nchunk, chunk = blockIdx.x % nchunk;
+  const int t = threadIdx.x;
+  const bool act = t < rpt * n8;
+  const int c8 = t % n8, r0 = t / n8, gl = c8 / tpg;
+  const int64_t c = (int64_t)chunk * CG + c8 * 8;
+  const int64_t row0 = (int64_t)inst * pix;
+  uint4 v[GNS_MAXR];
+#pragma unroll
+  for (int k = 0; k < GNS_MAXR; ++k) {
+    const int r = r0 + k * rpt;
+    v[k] = make_uint4(0, 0, 0, 0);
+    if (act && r < pix) v[k] = *(const uint4*)gn_src(x0, ldx0, c0, x1, ldx1, row0 + r, c);
+  }
+  const float inv_n = 1.0f / (float)(pix * cpg);
+  // group g's threads: c8 in [g * tpg, (g + 1) * tpg) of every row slot rr < rpt
+  auto group_sum = [&](int g) {
+    float a = 0.f;
+    for (int rr = 0; rr < rpt; ++rr)
+      for (int q = 0; q < tpg; ++q) a += red[rr * n8 + g * tpg + q];
+    return a;
+  };
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < GNS_MAXR; ++k) {
+    if (act && r0 + k * rpt < pix) {
+      float f[8];
+      unpack8(v[k], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += f[e];
+    }
+  }
+  red[t] = s;
+  __syncthreads();
+  if (t < ngl) gmean[t] = group_sum(t) * inv_n;
+  __syncthreads();
+  const float mean = gmean[gl];
+  float m2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < GNS_MAXR; ++k) {
+    if (act && r0 + k * rpt < pix) {
+      float f[8];
+      unpack8(v[k], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = f[e] - mean;
+        m2 = fmaf(d, d, m2);
+      }
+    }
+  }
+  red[t] = m2;  // every read of red's first values happened before the barrier above
+  __syncthreads();
+  if (t < ngl) grstd[t] = rsqrtf(group_sum(t) * inv_n + eps);
+  __syncthreads();
+  if (!act) return;
+  const float rstd = grstd[gl];
+  float a[8], b[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    a[e] = rstd * gamma[c + e];
+    b[e] = beta[c + e] - mean * a[e];
+  }
+#pragma unroll
+  for (int k = 0; k < GNS_MAXR; ++k) {
+    const int r = r0 + k * rpt;
+    if (r < pix) {
+      float f[8];
+      unpack8(v[k], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        f[e] = fmaf(f[e], a[e], b[e]);
+        if (silu) f[e] = silu_f(f[e]);
+      }
+      *(uint4*)(y + (row0 + r) * ldy + c) = pack8(f);
+    }
+  }
+}
+
 // One wave per row; up to LNCH 16-byte chunks per lane (C <= 64*8*LNCH).
 constexpr int LNCH = 4;
 __global__ __launch_bounds__(NT) void layernorm_kernel(const bf16_t* x, int64_t ldx, int64_t rows,
@@ -511,6 +603,36 @@ extern "C" int vd_gn_partial_g(const void* x0, int64_t ldx0, int64_t c0, const v
   hipLaunchKernelGGL(gn_partial_kernel<true>, dim3((unsigned)(n_inst * n_split)), dim3(NT), 0,
                      (hipStream_t)stream, (const bf16_t*)x0, ldx0, c0, (const bf16_t*)x1, ldx1, C,
                      pix_per_inst, n_split, (float4*)ws, groups);
+  return vd_launch_status();
+}
+
+// The channel chunk of the one-launch small GroupNorm (0 = not taken): the widest whole-group chunk
+// dividing C whose rows fit GNS_MAXR pieces per thread (cpg % 8 == 0: levels 3-4 and the mid block
+// of the UNet; pix <= 256 there).  vdiff.ops.gn_small_chunk mirrors this rule.
+static int gn_small_chunk(int64_t pix, int64_t C, int64_t groups) {
+  if (groups <= 0 || C <= 0 || C % groups || pix <= 0 || pix > (int64_t)NT * GNS_MAXR) return 0;
+  const int64_t cpg = C / groups;
+  if (cpg % 8) return 0;
+  for (int64_t cg = (C / cpg) * cpg; cg >= cpg; cg -= cpg) {
+    if (C % cg || cg / 8 > NT || cg / cpg > GNS_GMAX) continue;
+    const int64_t rpt = NT / (cg / 8);
+    if ((pix + rpt - 1) / rpt <= GNS_MAXR) return (int)cg;
+  }
+  return 0;
+}
+
+extern "C" int vd_gn_small(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_t ldx1, int64_t C,
+                           int64_t n_inst, int64_t pix_per_inst, int32_t groups, float eps, const float* gamma,
+                           const float* beta, int32_t silu, void* y, int64_t ldy, vd_stream_t stream) {
+  const int cg = gn_small_chunk(pix_per_inst, C, groups);
+  if (!cg) return VD_EUNSUPPORTED;  // the shape rule first: callers probe it without operands
+  VD_CHECK_ARG(x0 && y && gamma && beta && C % 8 == 0 && c0 % 8 == 0 && c0 > 0 && c0 <= C);
+  VD_CHECK_ARG(ldx0 % 8 == 0 && ldy % 8 == 0 && al16(x0) && al16(y));
+  if (c0 < C) VD_CHECK_ARG(x1 && ldx1 % 8 == 0 && al16(x1));
+  VD_CHECK_ARG(n_inst > 0 && n_inst * (C / cg) < 0x7fffffff);
+  hipLaunchKernelGGL(gn_small_kernel, dim3((unsigned)(n_inst * (C / cg))), dim3(NT), 0, (hipStream_t)stream,
+                     (const bf16_t*)x0, ldx0, c0, (const bf16_t*)x1, ldx1, C, (int)pix_per_inst, cg,
+                     (int)(C / groups), eps, gamma, beta, silu, (bf16_t*)y, ldy);
   return vd_launch_status();
 }
 

@@ -351,11 +351,16 @@ def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, ga
     (round 3; the four-launch path was 1-2 us faster on a 2-frame rank's few deep-level
     instances, tools/gn_bench.py).  A one-launch form (blocks waiting for their image's other
     blocks on an arrival counter) was slower at every image norm of the step and is gone
-    (round 4, profiles/r04_gn_one_launch_refuted.txt)."""
+    (round 4, profiles/r04_gn_one_launch_refuted.txt).  Round 5: small image instances (levels
+    3-4, the mid block) take vd_gn_small instead — one workgroup per (image, whole-group chunk),
+    no cross-block wait, chosen from (pix, C, groups) alone, so the sharded run still matches."""
     C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
     grec = C <= 2560 and 256 % groups == 0
-    if two_pass and gather is None and rev3 is None and grec:
-        return group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=silu, x1=x1)
+    if two_pass and gather is None and rev3 is None:
+        if gn_small_chunk(pix, C, groups):  # round 5: one launch at the small levels
+            return gn_small(x, n_inst, pix, groups, eps, gamma, beta, silu=silu, x1=x1)
+        if grec:
+            return group_norm_2pass(x, n_inst, pix, groups, eps, gamma, beta, silu=silu, x1=x1)
     n_split = n_split or gn_splits(n_inst, pix)
     if grec:  # per-group records (round 5: C/groups times fewer for the gather and the finalize)
         ws = gn_partial_g(x, C, n_inst, pix, n_split, groups, x1=x1)
@@ -368,6 +373,39 @@ def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, ga
             ws = gather(ws)
         ss = gn_finalize(ws, groups, eps, gamma, beta)
     return gn_apply(x, ss, pix, silu, x1=x1, rev3=rev3)
+
+
+GNS_NT, GNS_MAXR, GNS_GMAX = 256, 16, 32
+
+
+def gn_small_chunk(pix: int, C: int, groups: int) -> int:
+    """The channel chunk vd_gn_small takes for this image norm (0 = not taken): the widest whole-group
+    chunk dividing C whose rows fit 16 pieces of 8 channels per thread, C / groups a multiple of 8
+    (csrc/norm.hip gn_small_chunk; tests/test_ln_fold.py checks the mirror against the library)."""
+    if groups <= 0 or C <= 0 or C % groups or pix <= 0 or pix > GNS_NT * GNS_MAXR:
+        return 0
+    cpg = C // groups
+    if cpg % 8:
+        return 0
+    for cg in range((C // cpg) * cpg, cpg - 1, -cpg):
+        if C % cg or cg // 8 > GNS_NT or cg // cpg > GNS_GMAX:
+            continue
+        rpt = GNS_NT // (cg // 8)
+        if -(-pix // rpt) <= GNS_MAXR:
+            return cg
+    return 0
+
+
+def gn_small(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, out=None):
+    """vd_gn_small: the one-launch GroupNorm of a small image instance."""
+    _dev(x, x1, gamma, beta, out)
+    C = x.shape[1] + (x1.shape[1] if x1 is not None else 0)
+    if out is None:
+        out = torch.empty(x.shape[0], C, device=x.device, dtype=BF16)
+    x1p, ld1 = (_p(x1), _rows(x1)) if x1 is not None else (None, 0)
+    check(lib().vd_gn_small(_p(x), _rows(x), x.shape[1], x1p, ld1, C, n_inst, pix, groups, eps, _p(gamma), _p(beta),
+                            int(silu), _p(out), _rows(out), _stream()), "vd_gn_small")
+    return out
 
 
 def gn_image_splits(pix: int) -> int:
