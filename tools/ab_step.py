@@ -21,6 +21,9 @@ Switches:
   gn_mframe  the motion norm's records per frame (ops.gn_splits_per_frame) capped at GN_MFRAME_CAP
              (default 64) against the product choice;
   gn_small   the one-launch small-image GroupNorm (vd_gn_small) against the two-launch form there;
+  fold_force_v6  LayerNorm folds on a forced unsplit v6 wherever the automatic plan would not fold
+             (M <= 4096: a rank's level-2 QKV; with FOLD_V6_GEGLU=1 also the GEGLU) against the
+             unfolded norm -> v2 there;
   skinny     the time-embedding GEMMs (M = 2) on v9 against v1 (forced path 1);
   gn_split   vd_gn_partial_g's records per image (ops.gn_image_splits) capped at GN_SPLIT_CAP
              (default 64) and at least GN_SPLIT_ROWS (default 16) rows each."""
@@ -156,8 +159,35 @@ def set_gn_small(unet, on, saved):
     ops.gn_small_chunk = orig if on else (lambda pix, C, groups: 0)
 
 
+def set_fold_force_v6(unet, on, saved):
+    from vdiff import ops
+    from vdiff.models.layers import LnFold
+    orig_runs = saved.setdefault("ln_fold_runs", ops.ln_fold_runs)
+    orig_gemm = saved.setdefault("lnfold_gemm", LnFold.gemm)
+    geglu = os.environ.get("FOLD_V6_GEGLU", "0") == "1"
+
+    def forced(M, act):
+        return M <= 4096 and (geglu or act != ops.ACT_GEGLU)
+
+    def runs(M, w, s, *, act=0, rowbias=False):
+        if orig_runs(M, w, s, act=act, rowbias=rowbias):
+            return True
+        if not forced(M, act):
+            return False
+        with ops.gemm_plan(path=6):
+            return orig_runs(M, w, s, act=act, rowbias=rowbias)
+
+    def gemm(self, x, act=0, pe_div=1, pe_period=1, pe_off=0):
+        if orig_runs(x.shape[0], self.w, self.s, act=act, rowbias=self.pe_b is not None) or not forced(x.shape[0], act):
+            return orig_gemm(self, x, act, pe_div, pe_period, pe_off)
+        with ops.gemm_plan(path=6):
+            return orig_gemm(self, x, act, pe_div, pe_period, pe_off)
+    ops.ln_fold_runs = runs if on else orig_runs
+    LnFold.gemm = gemm if on else orig_gemm
+
+
 SWITCHES = {"ln_fold": set_ln_fold, "cfg_dedup": set_cfg_dedup, "mfold": set_mfold, "pfold": set_pfold,
-            "fold_v6": set_fold_v6, "gn_apply": set_gn_apply, "gn_split": set_gn_split, "skinny": set_skinny, "gn_grec": set_gn_grec, "gn_mframe": set_gn_mframe, "gn_small": set_gn_small}
+            "fold_v6": set_fold_v6, "gn_apply": set_gn_apply, "gn_split": set_gn_split, "skinny": set_skinny, "gn_grec": set_gn_grec, "gn_mframe": set_gn_mframe, "gn_small": set_gn_small, "fold_force_v6": set_fold_force_v6}
 
 
 def main():
