@@ -153,10 +153,11 @@ def set_gn_mframe(unet, on, saved):
     ops.gn_splits_per_frame = per_frame if on else orig
 
 
-def set_gn_small(unet, on, saved):
+def set_gn_small(unet, on, saved):  # GN_SMALL_OFF_MAXPIX=P: the off arm keeps vd_gn_small for pix <= P
     from vdiff import ops
     orig = saved.setdefault("gn_small_chunk", ops.gn_small_chunk)
-    ops.gn_small_chunk = orig if on else (lambda pix, C, groups: 0)
+    pmax = int(os.environ.get("GN_SMALL_OFF_MAXPIX", "0"))
+    ops.gn_small_chunk = orig if on else (lambda pix, C, groups: orig(pix, C, groups) if pix <= pmax else 0)
 
 
 def set_fold_force_v6(unet, on, saved):
