@@ -207,6 +207,30 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def visible_gpus():
+    """GPUs this process could use, counted WITHOUT touching the HIP runtime (the launcher parent
+    must not initialise it: torch.cuda.device_count() falls back to hipGetDeviceCount when amdsmi
+    is absent — ADVICE r05): the *_VISIBLE_DEVICES lists if set, else the KFD topology nodes with
+    SIMDs.  None when neither is readable (the ranks then find out themselves)."""
+    counts = []
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:  # an empty list is left to the ranks (its meaning differs between runtimes)
+            counts.append(len([t for t in v.split(",") if t.strip()]))
+    if counts:
+        return min(counts)
+    nodes = Path("/sys/class/kfd/kfd/topology/nodes")
+    try:
+        n = 0
+        for props in nodes.glob("*/properties"):
+            for line in props.read_text().splitlines():
+                if line.startswith("simd_count") and int(line.split()[1]) > 0:
+                    n += 1
+        return n or None
+    except (OSError, ValueError):
+        return None
+
+
 def launch_ranks(n: int, argv) -> int:
     """Start n ranks of this script under torch.distributed.run as a child process (never an
     exec: nothing here has touched the GPU, and the children initialise it themselves);
@@ -286,8 +310,9 @@ def main():
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        if not args.dry_run and torch.cuda.device_count() < args.gpus:  # counts devices without initialising HIP
-            print(f"bench.py: --gpus {args.gpus} but {torch.cuda.device_count()} GPUs visible", file=sys.stderr)
+        n_vis = None if args.dry_run else visible_gpus()
+        if n_vis is not None and n_vis < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but {n_vis} GPUs visible", file=sys.stderr)
             raise SystemExit(2)
         raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = check_world(args)

@@ -110,8 +110,8 @@ typedef struct vd_gemm_desc {
    * plan).  path: 0 = automatic; 1 = v1 (register-staged, any shape), 2 = v2 (256 x {128,160}
    * persistent LDS-DMA), 3 = v3 (256 x 256 ping-pong, dense A), 5 = v5 (256 x 320, BK 32),
    * 6 = v6 (64 x 64, split K toward 2 workgroups per CU), 8 = v8 (weight-stationary, dense
-   * K = 320, M >= 4096; automatic at M >= 16384); M <= 16 rows (the time-embedding MLP) run
-   * automatically on v9 (one wave per 16 columns, weight streaming; v1's arithmetic) — forced wherever that kernel takes the
+   * K = 320, M >= 4096; automatic at M >= 16384), 9 = v9 (M <= 16 rows: one wave per 16
+   * columns streaming W, v1's arithmetic; never automatic since round 6) — forced wherever that kernel takes the
    * shape, else the automatic choice; every path computes the same arithmetic for an
    * unsplit K (the K order of each output is fixed), the parity tests run each one.
    * plan_m > 0: choose kernel, split-K and LayerNorm fusion as if M were plan_m, launch over

@@ -226,12 +226,13 @@ def test_gemm_v8_weight_stationary(cuda, M, N, kind):
                                         (1, 52, 264, "res"), (5, 1292, 776, "rowbias"), (16, 4096, 2560, "gelu"),
                                         (3, 640, 96, "nobias")])
 def test_gemm_v9_skinny(cuda, M, N, K, kind):
-    """v9 (M <= 16: the time-embedding MLP and the resnets' concatenated time_emb_proj): the plan
-    takes it; every epilogue it carries, a partial last 16-column block (N = 52, 1292) and a
+    """v9 (M <= 16: the time-embedding MLP and the resnets' concatenated time_emb_proj; forced,
+    path 9): every epilogue it carries, a partial last 16-column block (N = 52, 1292) and a
     partial last 32-k step (K = 264, 776, 96); bit-equal to v1, whose MFMA chain it keeps, and
     within bf16 output rounding of fp32."""
-    assert ops.gemm_plan_of(GemmDesc(a0=256, lda0=K, k0=K, a_mode=0, w=256, ldw=K, M=M, N=N, K=K, out=256,
-                                     ldc=N))[0] == 9
+    with ops.gemm_plan(path=9):
+        assert ops.gemm_plan_of(GemmDesc(a0=256, lda0=K, k0=K, a_mode=0, w=256, ldw=K, M=M, N=N, K=K, out=256,
+                                         ldc=N))[0] == 9
     a = rnd(M, K)
     w = rnd(N, K, std=K ** -0.5)
     bias = None if kind == "nobias" else torch.randn(N, device=cuda)
@@ -244,7 +245,8 @@ def test_gemm_v9_skinny(cuda, M, N, K, kind):
         kw["res"] = rnd(M, N)
     elif kind == "rowbias":
         kw["rowbias"], kw["rb_div"] = torch.randn(M, N, device=cuda), 1
-    got = ops.gemm(a, w, bias=bias, **kw)
+    with ops.gemm_plan(path=9):
+        got = ops.gemm(a, w, bias=bias, **kw)
     with ops.gemm_plan(path=1):
         ref = ops.gemm(a, w, bias=bias, **kw)
     torch.cuda.synchronize()
@@ -291,17 +293,22 @@ def test_gemm_v8_strided_operands(cuda):
     (16384, 960, 320, "plain", 0.0, 8), (16384 + 37, 320, 320, "plain", 30.0, 8),
     (65536 + 16 * 5 + 3, 2560, 320, "geglu", 0.0, 8), (20000, 2560, 320, "geglu", 30.0, 8),
     (131072, 960, 320, "plain", 0.0, 8),
+    # rows offset by 100 / 300 std: the exact second pass of the ill-conditioned variance
+    (16384 + 37, 320, 320, "plain", 100.0, 8), (20000, 2560, 320, "geglu", 300.0, 8),
     # the unsplit v6 of a frame shard's small M (L2-L4 at 4 images per rank)
     (1024, 3840, 1280, "plain", 0.0, 6), (4096 + 37, 640, 640, "plain", 30.0, 6),
-    (256, 10240, 1280, "geglu", 0.0, 6), (700, 2560, 640, "geglu", 30.0, 6), (256, 1280, 1280, "plain", 0.0, 6)])
+    (256, 10240, 1280, "geglu", 0.0, 6), (700, 2560, 640, "geglu", 30.0, 6), (256, 1280, 1280, "plain", 0.0, 6),
+    (4096 + 37, 640, 640, "plain", 300.0, 6), (700, 2560, 640, "geglu", 100.0, 6)])
 def test_gemm_ln_fold(cuda, M, N, K, kind, offset, kern):
     """vd_gemm_desc.ln_fold_s (round 5): Linear(LayerNorm(x)) as ONE GEMM over the un-normalised
     rows (LnFold: W' = W∘gamma in bf16, s = its row sums, b' = b + W·beta; each row's mean / rstd
     from the A fragments by two extra MFMAs per X fragment, on v8 and v6).  Within bf16 output
     rounding of fp64 of the same folded arithmetic; within the unfolded path's own rounding (bf16
     normalised rows) of fp64 LayerNorm -> Linear and of the unfolded device path (vd_layernorm +
-    GEMM); rows whose mean is 30 std exercise the fp32 one-pass variance; ragged M (partial row
-    block, unequal XCD ranges / a partial 64-row tile)."""
+    GEMM); rows whose mean is 30 std exercise the fp32 one-pass variance, 100 / 300 std the exact
+    second pass it falls back to past 16 std (round 6, ADVICE r05: E[x²] − mean² alone loses
+    ~1e-7·(mean/std)² of the variance); ragged M (partial row block, unequal XCD ranges / a
+    partial 64-row tile)."""
     g = torch.Generator(device=cuda).manual_seed(0)
     x = bf(1.7 * (torch.randn(M, K, device=cuda, generator=g) + offset
                   + 0.5 * torch.randn(M, 1, device=cuda, generator=g)))
@@ -1223,13 +1230,15 @@ def test_motion_qkv_attention(cuda, batch, positions, unit):
     assert ops.motion_qkv_takes(batch, F, positions, heads, d) and not ops.motion_qkv_takes(1, F, 64, heads, d)
 
 
-@pytest.mark.parametrize("batch,positions,offset", [(2, 4096, 0.0), (1, 4100, 30.0), (1, 2048, 0.0)])
+@pytest.mark.parametrize("batch,positions,offset", [(2, 4096, 0.0), (1, 4100, 30.0), (1, 2048, 0.0),
+                                                     (1, 2048, 300.0)])
 def test_motion_qkv_attention_ln_fold(cuda, batch, positions, offset):
     """vd_motion_qkv_attention with ln_fold_tab (round 5): the motion block's LayerNorm + PE by
     frame folded into the fused QKV attention (MotionLnFold: W' = W∘gamma, per head the row sums
     and W·(beta + pe[f])), over the UN-normalised rows — against the unfolded device path
     (vd_layernorm with PE, then the same kernel on bf16(W)) within the two paths' bf16 roundings,
-    and against fp64 LayerNorm + PE -> QKV -> SDPA; rows offset by 30 std; both PW forms."""
+    and against fp64 LayerNorm + PE -> QKV -> SDPA; rows offset by 30 std (one-pass variance) and
+    300 std (its exact second pass); both PW forms."""
     from vdiff.models.layers import MotionLnFold
     C, d, heads, NF = 320, 40, 8, 16
     g = torch.Generator(device=cuda).manual_seed(3)

@@ -118,11 +118,15 @@ def test_gn_small_rule_mirrors_library():
     assert ops.gn_small_chunk(256, 1920, 32) == 0   # C / groups = 60: a piece would straddle groups
 
 
-def test_plan_skinny_m_takes_v9():
-    """vd_gemm_plan: M <= 16 dense rows (the time-embedding MLP, M = the UNet batch) run on v9
-    (bit-identical to v1); a forced v1, a GEGLU, a folded LayerNorm or M = 17 keep the other plans."""
+def test_plan_skinny_m_v9_forced_only():
+    """vd_gemm_plan: M <= 16 dense rows (the time-embedding MLP, M = the UNet batch) run on v1 in
+    the product plan and on v9 (bit-identical to v1) only when forced (path 9; round 6: v9's
+    rank-step gain and 16-frame loss come from the same M = 2 GEMMs); a forced v9 on a GEGLU, a
+    folded LayerNorm or M = 17 keeps the automatic plan."""
     d = _desc(2, 1280, K=1280)
     d.ln_fold_s = None
+    assert _plan(d)[0] == 1
+    d.path = 9
     assert _plan(d) == (9, 1)
     d.M = 16
     assert _plan(d) == (9, 1)
@@ -132,6 +136,7 @@ def test_plan_skinny_m_takes_v9():
     assert _plan(d)[0] == 1
     g = _desc(2, 2560, K=1280, act=ops.ACT_GEGLU)
     g.ln_fold_s = None
+    g.path = 9
     assert _plan(g)[0] == 1
     assert _plan(_desc(2, 1280, K=1280))[0] == 0  # a fold at M = 2: no kernel, the unfolded form
 

@@ -1,6 +1,7 @@
 """Where the v2 GEMM's k-tile loop spends its cycles: a DIAGNOSTIC build of the library with
-s_memtime stamps in gemm2_kernel (-DVD_G2_STAMPS; cdna_hip_programming.md "In-kernel stamps"),
-never the product library.  Read the SHARES, not the run time (the stamps' lgkmcnt(0) fences
+s_memtime stamps in gemm2_kernel (cdna_hip_programming.md "In-kernel stamps"), never the product
+library: the stamps live HERE (STAMPS below) and are spliced into a copy of csrc/gemm.hip at build
+time, so the shipping kernel carries no diagnostic code.  Read the SHARES, not the run time (the stamps' lgkmcnt(0) fences
 forbid overlaps the real kernel has).
 
     python tools/g2_stamps.py --build          # here (CPU): tools/diag_build/libvdiff_diag.so
@@ -23,13 +24,72 @@ OUT = ROOT / "tools" / "diag_build"
 LIB = OUT / "libvdiff_diag.so"
 
 
+# The stamps: (anchor inside gemm2_kernel, text inserted before it / after it).  Each anchor
+# must occur exactly once in the kernel's body; instrument() fails loudly when the kernel changes.
+PRELUDE = r"""
+__device__ unsigned long long g2_diag[4096 * 8 * 6];
+#define G2_STAMP(t)                                                                      \
+  do {                                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+  } while (0)
+"""
+EPILOGUE = r"""
+extern "C" int vd_diag_g2_read(void* host, int64_t n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g2_diag), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int vd_diag_g2_clear() {
+  static unsigned long long z[4096 * 8 * 6];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g2_diag), z, sizeof(z), 0, hipMemcpyHostToDevice);
+}
+"""
+STAMPS = [  # (anchor, before, after)
+    ("  int stage = 0;\n", "",
+     "  unsigned long long st0, st1, st2, st3, st4, sw = 0, sb = 0, sm = 0, stl = 0, tbeg;\n  G2_STAMP(tbeg);\n"),
+    ("  for (int it = 0; it < n_it; ++it) {\n", "", "    G2_STAMP(st0);\n"),
+    ('    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");\n    __builtin_amdgcn_s_barrier();',
+     "    G2_STAMP(st1);\n", "\n    G2_STAMP(st2);"),
+    ("    if (++ckt == ckt1) {", "    G2_STAMP(st3);\n", ""),
+    ("    stage = stage == 2 ? 0 : stage + 1;\n", "",
+     "    G2_STAMP(st4);\n    sw += st1 - st0; sb += st2 - st1; sm += st3 - st2; stl += st4 - st3;\n"),
+]
+TAIL = """  unsigned long long tend;
+  G2_STAMP(tend);
+  if (lane == 0 && blockIdx.x < 4096) {
+    unsigned long long* o = g2_diag + ((size_t)blockIdx.x * 8 + wid) * 6;
+    o[0] = sw; o[1] = sb; o[2] = sm; o[3] = stl; o[4] = tend - tbeg; o[5] = (unsigned long long)n_it;
+  }
+"""
+
+
+def instrument(text: str) -> str:
+    """gemm.hip with the stamps spliced into gemm2_kernel (a diagnostic copy under diag_build/src)."""
+    sig = "template <int BN, int MODE>\n__global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel("
+    i0 = text.index(sig)
+    i1 = text.index("\n}\n", i0) + 1  # the kernel's closing brace (column 0)
+    body = text[i0:i1]
+    for anchor, before, after in STAMPS:
+        if body.count(anchor) != 1:
+            raise RuntimeError(f"stamp anchor not unique in gemm2_kernel: {anchor!r}")
+        body = body.replace(anchor, before + anchor + after)
+    body = body + TAIL
+    return text[:i0] + PRELUDE + body + text[i1:] + EPILOGUE
+
+
 def build():
     sys.path.insert(0, str(PKG))
     import build_ext as B
     OUT.mkdir(exist_ok=True)
-    defs = ['-DVD_BUILD_HASH="diag"', f'-DVD_BUILD_ARCH="{B.ARCH}"', "-DVD_G2_STAMPS"]
+    src_dir = OUT / "src"
+    src_dir.mkdir(exist_ok=True)
+    for f in B.CSRC.iterdir():
+        if f.suffix in (".hip", ".h"):
+            text = f.read_text()
+            (src_dir / f.name).write_text(instrument(text) if f.name == "gemm.hip" else text)
+    defs = ['-DVD_BUILD_HASH="diag"', f'-DVD_BUILD_ARCH="{B.ARCH}"', f"-I{B.CSRC}", f"-I{ROOT / 'include'}"]
     objs = []
-    for src in sorted(B.CSRC.glob("*.hip")):
+    for src in sorted(src_dir.glob("*.hip")):
         obj = OUT / (src.stem + ".o")
         subprocess.run([B.HIPCC, *B.CFLAGS, *defs, "-c", str(src), "-o", str(obj)], check=True)
         objs.append(str(obj))

@@ -142,3 +142,27 @@ struct Rev3 {
     return (int)(((((i2 << sh1) + i1) * (uint32_t)n0 + i0) << shi) + j);
   }
 };
+
+// LayerNorm-fold statistics (v8 / the fused motion QKV attention): var1 = E[x²] − mean² from the
+// fp32 MFMA sums, relative error ≈ 1e-7·(1 + mean²/var).  Where any row of the wave has
+// |mean| / std > 16 (mean² > 256 var1), the wave takes the exact second pass Σ(x − mean)² over
+// the row fragments it holds — lane (fr, fq) has row fr's elements 32 ks + 8 fq .. +7, so the
+// four lanes fr + 16 fq hold the whole row.  The branch is wave-uniform and never
+// taken on the UNet's rows (|mean| / std ≤ 0.1).
+template <int KS>
+__device__ __forceinline__ float row_var_guarded(const bf16x8 (&x)[KS], float mean, float var1, float rk) {
+  if (__any(mean * mean > 256.f * var1)) {
+    float ss = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = (float)x[ks][e] - mean;
+        ss = fmaf(v, v, ss);
+      }
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    return ss * rk;
+  }
+  return fmaxf(var1, 0.f);
+}

@@ -502,17 +502,6 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // after the barrier (sched_barrier), then k-step 1's reads interleave one per two of k-step 0's
 // MFMAs (sched_group_barrier), so the MFMA chain waits on counted lgkmcnt only (52.79 vs 53.50
 // ms/step for the unpinned order, 53.11 with all reads ahead; profiles/r02f_fragment_order.txt).
-#ifdef VD_G2_STAMPS
-// Diagnostic build only (tools/g2_stamps.py; never in libvdiff_hip.so): per-wave cycle sums of the
-// k-tile loop's segments — ring wait, barrier, fragment reads + MFMA issue, epilogue + DMA issue.
-__device__ unsigned long long g2_diag[4096 * 8 * 6];
-#define G2_STAMP(t)                                                                      \
-  do {                                                                                   \
-    __builtin_amdgcn_sched_barrier(0);                                                   \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");            \
-    __builtin_amdgcn_sched_barrier(0);                                                   \
-  } while (0)
-#endif
 
 template <int BN, int MODE>
 __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
@@ -690,14 +679,7 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
   unit_kr(cu, ckt, ckt1);
   const int fr = lane & 15, fq = lane >> 4;
   int stage = 0;
-#ifdef VD_G2_STAMPS
-  unsigned long long st0, st1, st2, st3, st4, sw = 0, sb = 0, sm = 0, stl = 0, tbeg;
-  G2_STAMP(tbeg);
-#endif
   for (int it = 0; it < n_it; ++it) {
-#ifdef VD_G2_STAMPS
-    G2_STAMP(st0);
-#endif
     // this wave's DMA for k-tile `it` has landed once at most k-tile it+1's remain
     // outstanding (everything issued before that, epilogue stores included, is done)
     if (it + 1 < n_it) {
@@ -706,14 +688,8 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     } else {
       wait_vm<0>();
     }
-#ifdef VD_G2_STAMPS
-    G2_STAMP(st1);
-#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's DMA for `it` landed; stage (it-1)%3 fully read
-#ifdef VD_G2_STAMPS
-    G2_STAMP(st2);
-#endif
     const char* sbase = smem + stage * C::STAGE;
     {
       bf16x8 wf[BK / 32][C::NB], xf[BK / 32][C::MB];
@@ -743,9 +719,6 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
         __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
       }
     }
-#ifdef VD_G2_STAMPS
-    G2_STAMP(st3);
-#endif
     if (++ckt == ckt1) {  // unit finished: epilogue (its memory ops precede the next DMA)
       const int tile = cu / split, sp = cu % split;
       const int64_t m0 = (int64_t)(tile / tiles_n) * G2_BM, n0 = (int64_t)(tile % tiles_n) * BN;
@@ -774,30 +747,9 @@ __global__ __launch_bounds__(G2_NT, 1) void gemm2_kernel(const vd_gemm_desc d, u
     }
     if (it + 2 < n_it) issue(stage == 0 ? 2 : stage - 1);
     stage = stage == 2 ? 0 : stage + 1;
-#ifdef VD_G2_STAMPS
-    G2_STAMP(st4);
-    sw += st1 - st0; sb += st2 - st1; sm += st3 - st2; stl += st4 - st3;
-#endif
   }
-#ifdef VD_G2_STAMPS
-  unsigned long long tend;
-  G2_STAMP(tend);
-  if (lane == 0 && blockIdx.x < 4096) {
-    unsigned long long* o = g2_diag + ((size_t)blockIdx.x * 8 + wid) * 6;
-    o[0] = sw; o[1] = sb; o[2] = sm; o[3] = stl; o[4] = tend - tbeg; o[5] = (unsigned long long)n_it;
-  }
-#endif
 }
 
-#ifdef VD_G2_STAMPS
-extern "C" int vd_diag_g2_read(void* host, int64_t n) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g2_diag), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
-}
-extern "C" int vd_diag_g2_clear() {
-  static unsigned long long z[4096 * 8 * 6];
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g2_diag), z, sizeof(z), 0, hipMemcpyHostToDevice);
-}
-#endif
 
 
 // Load-free epilogue (v5, split == 1, bf16 out, no residual / row bias): the bias
@@ -1645,6 +1597,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, WM * WN * 64), amdgpu_w
 // these M (dot-2 VALU for the same sums cost ≈ 10 cycles each beside the MFMAs and 1.5-3x the time,
 // MI355X_MICROARCH.md "price of one filler"); the accumulators become rstd·(acc − mean·s[n]) before
 // the common epilogue adds b' (the folded bias) and any row bias (the motion block's W·pe[frame]).
+// Rows with |mean| / std > 16 take v8's exact second pass (re-read from L2).
 constexpr int G6_BM = 64, G6_BN = 64, G6_NT = 256;
 constexpr int G6_A = G6_BM * BK * 2, G6_W = G6_BN * BK * 2, G6_STAGE = G6_A + G6_W;  // 8 + 8 KiB
 
@@ -1809,7 +1762,27 @@ __global__ __launch_bounds__(G6_NT, G6_S == 3 ? 3 : (G6_S == 4 ? 2 : 1)) void ge
       const float gd = j3 == 0 ? gacc[b][0] : j3 == 1 ? gacc[b][1] : j3 == 2 ? gacc[b][2] : gacc[b][3];
       const float sxx = __shfl(gd, fr + 16 * (fr >> 2), 64);
       const float mean = sacc[b][0] * rk;
-      const float rstd = rsqrtf(fmaxf(fmaf(sxx, rk, -mean * mean), 0.f) + d.ln_fold_eps);
+      float var = fmaf(sxx, rk, -mean * mean);
+      if (__any(mean * mean > 256.f * var)) {  // ill-conditioned row(s): exact second pass from L2 (v8's)
+        const int m = mbase + b * 16 + fr;
+        float ss = 0.f;
+#pragma unroll 1
+        for (int kk = 8 * fq; kk < (int)K; kk += 32) {
+          const bool s0 = kk < (int)d.k0;
+          const uint32_t o = m < (int)M ? (uint32_t)m * (uint32_t)((s0 ? d.lda0 : d.lda1) * 2) +
+                                              (uint32_t)(s0 ? kk : kk - (int)d.k0) * 2u : G2_OOB;
+          const bf16x8 v = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(s0 ? ra0 : ra1, o, 0, 0));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float t = (float)v[e] - mean;
+            ss = fmaf(t, t, ss);
+          }
+        }
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        var = ss * rk;
+      }
+      const float rstd = rsqrtf(fmaxf(var, 0.f) + d.ln_fold_eps);
 #pragma unroll
       for (int a = 0; a < NB; ++a) {
         const int n = nbase + a * 16 + 4 * fq;
@@ -2020,9 +1993,10 @@ constexpr int G8_SUB = G8_BN * BK * 2;  // one 64-deep W sub-tile: 20 KiB
 // more MFMAs on the A fragments the wave already holds — ones·x (every output column = the row
 // sum) and x·xᵀ (the 16 x 16 Gram block, whose diagonal is the row's sum of squares) — so the
 // statistics cost no VALU inside the loop; the epilogue forms rstd·(acc − mean·s[n]) + b'[n]
-// with s and b' in LDS next to the bias.  var = E[x²] − mean² in fp32: its relative error is
-// ≈ 1e-7·(1 + mean²/var), below bf16 rounding for |mean| / std up to ~100
-// (tests/test_gpu_kernels.py::test_gemm_ln_fold covers a row offset of 30 std).
+// with s and b' in LDS next to the bias.  var = E[x²] − mean² in fp32 has a relative error of
+// ≈ 1e-7·(1 + mean²/var); where a row's |mean| / std passes 16 (never in the UNet: ≤ 0.1,
+// profiles/r06_motion_bisect.txt) the wave takes the exact second pass Σ(x − mean)², re-reading
+// its rows from L2 (test_gemm_ln_fold runs rows offset by 30 / 100 / 300 std).
 template <bool RES, bool GEGLU, bool PERM = false, bool LNF = false>
 __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc d, uint32_t a0_bytes,
                                                              uint32_t w_bytes, uint32_t c_bytes, int tiles_n,
@@ -2128,7 +2102,25 @@ __global__ __launch_bounds__(G8_NW * 64, 1) void gemm8_kernel(const vd_gemm_desc
       const float sxx = __shfl(gd, fr + 16 * (fr >> 2), 64);
       constexpr float RK = 1.0f / (float)G8_KMAX;
       const float mean = sacc[0] * RK;
-      rstd = rsqrtf(fmaxf(fmaf(sxx, RK, -mean * mean), 0.f) + d.ln_fold_eps);
+      float var = fmaf(sxx, RK, -mean * mean);
+      if (__any(mean * mean > 256.f * var)) {  // ill-conditioned row(s): exact second pass (see above)
+        const int m = rb * 16 + fr;
+        const uint32_t o = m < M ? (uint32_t)m * (uint32_t)(d.lda0 * 2) + (uint32_t)(fq * 16) : G2_OOB;
+        float ss = 0.f;
+#pragma unroll 1
+        for (int ks = 0; ks < KS; ++ks) {  // re-read from L2 (the fragments' registers are not kept live)
+          const bf16x8 v = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, o + (uint32_t)(ks * 64), 0, 0));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float t = (float)v[e] - mean;
+            ss = fmaf(t, t, ss);
+          }
+        }
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        var = ss * RK;
+      }
+      rstd = rsqrtf(fmaxf(var, 0.f) + d.ln_fold_eps);
       nmean = -mean;
     }
     if constexpr (GEGLU) {
@@ -2418,8 +2410,11 @@ Plan plan_core(const vd_gemm_desc& d) {
   Plan p;
   int path = d.path;
   const int64_t M = d.plan_m > 0 ? d.plan_m : d.M;  // the row count the plan is made for
-  // v9 (M <= 16 rows, dense, one operand, no GEGLU / LayerNorm / row map): bit-identical to v1
-  if (path == 0 && M <= G9_MMAX && d.M <= G9_MMAX && d.a_mode == VD_A_DENSE && d.k0 == d.K &&
+  // v9 (M <= 16 rows, dense, one operand, no GEGLU / LayerNorm / row map): bit-identical to v1.
+  // Forced only (path 9): its same-process A/Bs were -0.04 ms on the 8-way rank step and
+  // +0.04..0.12 ms on the 16-frame step (profiles/r05_gemm_v9_skinny_ab.txt), and both run the
+  // same M = 2 time-embedding GEMMs, so no row count separates the gain from the loss (round 6).
+  if (path == 9 && M <= G9_MMAX && d.M <= G9_MMAX && d.a_mode == VD_A_DENSE && d.k0 == d.K &&
       d.act != VD_ACT_GEGLU && !d.ln_out && !d.ln_fold_s && !d.rmap_inner) {
     p.ver = 9;
     return p;

@@ -212,7 +212,8 @@ __global__ __launch_bounds__(MqCfg<D>::NT, 1) void motion_qkv_attn2_kernel(
       const float sxx = __shfl(gd, fr + 16 * (fr >> 2), 64);
       constexpr float RK = 1.0f / (float)Cf::C;
       const float mean = sacc[0] * RK;
-      if (fq == 0) st_l[pw * MF + fr] = make_float2(-mean, rsqrtf(fmaxf(fmaf(sxx, RK, -mean * mean), 0.f) + eps));
+      const float var = row_var_guarded<Cf::C / 32>(xf[pw], mean, fmaf(sxx, RK, -mean * mean), RK);
+      if (fq == 0) st_l[pw * MF + fr] = make_float2(-mean, rsqrtf(var + eps));
     }
   }
 

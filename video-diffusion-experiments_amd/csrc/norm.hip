@@ -254,7 +254,8 @@ __global__ __launch_bounds__(NT) void gn_apply_kernel(const bf16_t* x0, int64_t 
 #pragma unroll
       for (int e = 0; e < 8; ++e) f[e] = silu_f(f[e]);
     }
-    *(uint4*)(y + (int64_t)perm((int)row) * ldy + c) = pack8(f);
+    // identity map (inner == 0): the 64-bit row as is; a row map needs rows < 2^31 (checked)
+    *(uint4*)(y + (perm.shi < 0 ? row : (int64_t)perm((int)row)) * ldy + c) = pack8(f);
   }
 }
 
@@ -683,7 +684,8 @@ extern "C" int vd_gn_apply_rev3(const void* x0, int64_t ldx0, int64_t c0, const 
   VD_CHECK_ARG(ldx0 % 8 == 0 && ldy % 8 == 0 && al16(x0) && al16(y) && al16(scale_shift));
   if (c0 < C) VD_CHECK_ARG(x1 && ldx1 % 8 == 0 && al16(x1));
   const int64_t rows = n_inst * pix_per_inst;
-  VD_CHECK_ARG(rows < 0x7fffffff && inner >= 0 && Rev3::ok(rows, n1, n2, inner));
+  // rows < 2^31 only where a row map is applied (vd_gn_apply keeps its 64-bit rows)
+  VD_CHECK_ARG(inner >= 0 && (inner == 0 || rows < 0x7fffffff) && Rev3::ok(rows, n1, n2, inner));
   const int64_t total = rows * (C / 8);
   const int64_t blocks = (total + NT - 1) / NT;
   const unsigned grid = (unsigned)(blocks < 8192 ? blocks : 8192);
