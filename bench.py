@@ -51,6 +51,14 @@ METRIC = "denoising steps/sec (whole node) at 16-frame 512×512 bf16; 1/2/4/8-GP
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 STEP_TFLOP = {"full": 35.496, "tiny": 0.234}   # BASELINE.md §2 / SURVEY App. B, CFG batch, F=16 / F=4
+# FLOPs of the CFG batch that the CFG dedup (DenoiseLoop.cfg_dedup, round 5) does not execute — the
+# two guidance halves are the same latents and timestep until the first cross-attention, so these
+# run on one half (per 16 frames, full model): conv_in 1.510 + down_blocks[0].resnets[0]'s two 3x3
+# convs 241.592 + proj_in 13.422 + QKV 40.265 + the L1 self-attention 343.597 + to_out 13.422 +
+# attn2.to_q 13.422 GFLOP (+ time_emb_proj 0.001) = 667.23 GFLOP.  step_mfma's `achieved` keeps the
+# algorithmic CFG-batch count (the outputs are bit-identical to the undeduplicated step); the
+# executed-FLOP rate is reported beside it.
+CFG_DEDUP_TFLOP = {"full": 0.66723}
 WARM_ATTN = 10                 # untimed launches before each roofline timing (tools/prof_summary.py skips them)
 
 
@@ -444,6 +452,16 @@ def main():
     roof["kernel_src_hash"] = roof_src_hash()
     gpu_tflop = STEP_TFLOP[cfg_name] * frames / (16 if cfg_name == "full" else 4) / (1 if replicas else world)
     step_tf = gpu_tflop / (ms * 1e-3)
+    step_mfma = {"algorithmic_tflop_per_step_per_gpu": round(gpu_tflop, 3),
+                 "achieved": round(step_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                 "frac": round(step_tf / PEAK_BF16_TFLOPS, 4)}
+    dedup = getattr(loop, "cfg_dedup", False) and lay.cfg_shard is None and cfg_name in CFG_DEDUP_TFLOP
+    if dedup:  # the duplicated CFG-half work the step skips (bit-identical outputs): labelled, not hidden
+        saved = CFG_DEDUP_TFLOP[cfg_name] * frames / 16 / (1 if replicas else world)
+        step_mfma["cfg_dedup_tflop_saved"] = round(saved, 3)
+        step_mfma["executed_tflop_per_step_per_gpu"] = round(gpu_tflop - saved, 3)
+        step_mfma["executed_achieved"] = round((gpu_tflop - saved) / (ms * 1e-3), 1)
+        step_mfma["executed_frac"] = round((gpu_tflop - saved) / (ms * 1e-3) / PEAK_BF16_TFLOPS, 4)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[bench] timing the CPU oracle baseline ...")
@@ -475,9 +493,7 @@ def main():
                 "hipgraph": graph_ok,
             },
             "roofline": roof,
-            "step_mfma": {"algorithmic_tflop_per_step_per_gpu": round(gpu_tflop, 3),
-                          "achieved": round(step_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                          "frac": round(step_tf / PEAK_BF16_TFLOPS, 4)},
+            "step_mfma": step_mfma,
             "cpu_baseline": cpu,
             "no_cfg": nocfg,
             "replicas_control": rep,

@@ -213,6 +213,14 @@ int vd_gn_small(const void* x0, int64_t ldx0, int64_t c0, const void* x1, int64_
 int vd_gn_finalize_g(const float* ws, int64_t n_inst, int32_t n_split_total, int64_t C,
                      int32_t groups, float eps, const float* gamma, const float* beta,
                      float* scale_shift, vd_stream_t stream);
+/* vd_gn_finalize_g over RANK-MAJOR records: ws = [n_ranks][n_inst][n_split_per_rank][groups]
+ * float4, the frame-sharded ranks' all-gather output as it lands (round 6: no transpose copy into
+ * vd_gn_finalize_g's [n_inst][n_ranks * n_split_per_rank][groups] order).  Split s of an instance
+ * is rank s / n_split_per_rank's split s % n_split_per_rank, merged in vd_gn_finalize_g's order:
+ * the result equals vd_gn_finalize_g on the transposed records bit for bit. */
+int vd_gn_finalize_g_ranks(const float* ws, int64_t n_inst, int32_t n_ranks, int32_t n_split_per_rank,
+                           int64_t C, int32_t groups, float eps, const float* gamma, const float* beta,
+                           float* scale_shift, vd_stream_t stream);
 
 /* ---------------------------------------------------------------- LayerNorm
  * BasicTransformerBlock.norm1/2/3 (eps 1e-5) over the last dim of bf16 rows,

@@ -75,6 +75,9 @@ def _worker(rank, world, port, out_path, layout="frame", cfg="tiny", steps=2, ov
         def gather_gn_partials(self, ws):
             return super().gather_gn_partials(ws.cpu()).to(ws.device)
 
+        def gather_gn_records(self, ws):
+            return super().gather_gn_records(ws.cpu()).to(ws.device)
+
         def _a2a(self, x, out=None):
             got = super()._a2a(x.cpu()).to(x.device)
             return got if out is None else out.copy_(got)

@@ -476,6 +476,28 @@ def test_gn_finalize_group_records(cuda):
     torch.testing.assert_close(ss[..., 1].double(), sh, rtol=0, atol=2e-5 * a.abs().max().item())
 
 
+@pytest.mark.parametrize("ranks", [1, 2, 4])
+def test_gn_finalize_rank_major_records(cuda, ranks):
+    """vd_gn_finalize_g_ranks (round 6): the frame-sharded ranks' records in the
+    all-gather's rank-major order [rank, video, split, group] — no transpose copy — give the same
+    scale / shift bits as vd_gn_finalize_g on the split-concatenated records."""
+    B, F, HW, C, G, eps = 2, 8, 256, 1280, 32, 1e-6
+    x = bf(torch.randn(B * F * HW, C, device=cuda) * 1.5 - 0.2)
+    g = 1 + 0.1 * torch.randn(C, device=cuda)
+    b = 0.1 * torch.randn(C, device=cuda)
+    sp = ops.gn_splits_per_frame(HW)
+    Fl = F // ranks
+    xv = x.view(B, F, HW, C)
+    parts = [ops.gn_partial_g(xv[:, r * Fl:(r + 1) * Fl].reshape(-1, C).contiguous(), C, B, Fl * HW, Fl * sp, G)
+             for r in range(ranks)]
+    ss_cat = ops.gn_finalize_g(torch.cat(parts, 1), C, eps, g, b)
+    ss_rm = ops.gn_finalize_g(torch.stack(parts, 0), C, eps, g, b)
+    ss_one = ops.gn_finalize_g(ops.gn_partial_g(x, C, B, F * HW, F * sp, G), C, eps, g, b)
+    torch.cuda.synchronize()
+    assert torch.equal(ss_rm, ss_cat)
+    assert torch.equal(ss_rm, ss_one)
+
+
 def test_gn_apply_rev3(cuda):
     """vd_gn_apply_rev3: the motion norm writing the all-to-all's send order directly equals the
     plain apply followed by the row permutation, bit for bit."""

@@ -5,12 +5,15 @@ copy of csrc/gemm.hip at build time:
   a6   the A (activation) pieces of a k-tile cut from 32 to 6 (waves 0-5 issue one piece each):
        the traffic a halo-tiled conv would move per tap (a 6 x 66-pixel, 64-channel patch = 49.5
        KiB serves all 9 taps, ~5.5 KiB per tap against 32 KiB);
-  w1   the W (weight) pieces cut to one per k-tile (wave 0).
+  w1   the W (weight) pieces cut to one per k-tile (wave 0);
+  gn   (a pricing build) the landed A tile GroupNorm-applied and SiLU'd in
+       place in LDS once per k-tile (one FMA + SiLU per element, a row mask for the conv padding)
+       behind a second barrier: what Conv + GroupNorm + SiLU fused into the conv costs.
 
 The counted ring waits follow each wave's actual piece count.  Compared against the product
 library on the UNet's stride-1 conv shapes (path 2 forced, 32 images):
 
-    python tools/g2_ablate.py --build      # here (CPU): tools/diag_build/libvdiff_{a6,w1}.so
+    python tools/g2_ablate.py --build      # here (CPU): tools/diag_build/libvdiff_{a6,gn,w1}.so
     python tools/g2_ablate.py              # GPU box
 """
 from __future__ import annotations
@@ -46,10 +49,45 @@ BDMA_OLD = """#pragma unroll
       if (j < nbw) dma16(rw, lb + (j * 8 + wid) * 1024, boff[j] + (uint32_t)kb * 2);"""
 NBW_OLD = "  const int nbw = (C::NBI - wid + 7) / 8;  // this wave's B DMA instructions per K-tile"
 
+SBASE_OLD = "    const char* sbase = smem + stage * C::STAGE;\n"
+# the Conv+GroupNorm+SiLU form VERDICT r05 item 5 asked to price: the landed A tile normalised and
+# SiLU'd once, in place in LDS, by the whole workgroup (thread: one 16-B channel chunk of 4 rows;
+# its 8 channels' (a, b) from LDS — a stand-in for the tile's per-(image, channel) table; a row
+# mask so a conv tap outside the image stays zero), then a second barrier before the fragment reads
+GN_PASS = SBASE_OLD + """    if constexpr (MODE == VD_A_CONV3X3) {
+      char* sa = smem + stage * C::STAGE;
+      const int c8 = tid & 7, r0 = tid >> 3;
+      const float4* abp = (const float4*)(sa + C::A_BYTES + c8 * 64);
+      const float4 a0 = abp[0], a1 = abp[1], b0 = abp[2], b1 = abp[3];
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = r0 + 64 * j;
+        uint4* pp = (uint4*)(sa + r * 128 + ((c8 ^ (r & 7)) << 4));
+        float f[8];
+        unpack8(*pp, f);
+        const bool ok = ((r + it) & 63) != 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float y = fmaf(f[e], av[e], bv[e]);
+          f[e] = ok ? silu_f(y) : 0.f;
+        }
+        *pp = pack8(f);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+"""
+
 VARIANTS = {
     "a6": {
         "na": "(wid < 6 ? 1 : 0)",
         ADMA_OLD: """      if (wid < 6) dma16(s0 ? ra0 : ra1, la + (wid * 4) * 1024, (s0 ? aoff0[0] : aoff1[0]) + coff);""",
+    },
+    "gn": {
+        "na": "C::NA",
+        SBASE_OLD: GN_PASS,
     },
     "w1": {
         "na": "C::NA",

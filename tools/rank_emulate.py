@@ -49,6 +49,12 @@ class EmulatedShard(FrameShard):
     def gather_gn_partials(self, ws):
         return ws.repeat_interleave(self.world, dim=1) if self.world > 1 else ws
 
+    def gather_gn_records(self, ws):  # the all-gather's output write, as _all_gather
+        out = torch.empty((self.world,) + tuple(ws.shape), device=ws.device, dtype=ws.dtype)
+        if self.comm == "copy":
+            out.copy_(ws.unsqueeze(0).expand(self.world, *ws.shape))
+        return out
+
     def all_gather_frames(self, x):
         return x
 

@@ -179,10 +179,14 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
 // One block per (instance, group): Chan-combine the n_split x (C/groups) records
 // of the group in parallel (per-thread, then an LDS tree), then write {a, b}.  GREC: the
 // records are vd_gn_partial_g's, one per (instance, split, group) — C/groups times fewer.
+// n_ranks > 1 (GREC, round 6): the records are rank-major, [rank][instance][split of the
+// rank][group] — the frame-sharded ranks' all-gather output as it lands, with no transpose
+// copy — and global split s = rank * (n_split / n_ranks) + local split, so the merge order
+// over s (hence every bit) is the one-rank layout's.
 template <bool GREC>
 __global__ __launch_bounds__(NT) void gn_finalize_kernel(const float4* ws, int n_split, int64_t C,
                                                          int groups, float eps, const float* gamma,
-                                                         const float* beta, float2* ss) {
+                                                         const float* beta, float2* ss, int n_ranks = 1) {
   __shared__ float3 red[NT];
   const int inst = blockIdx.x / groups;
   const int g = blockIdx.x % groups;
@@ -190,7 +194,9 @@ __global__ __launch_bounds__(NT) void gn_finalize_kernel(const float4* ws, int n
   const int rpg = GREC ? 1 : cpg;  // records per (split, group)
   const int64_t rstride = GREC ? groups : C;
   const int nrec = n_split * rpg;
-  const float4* src = ws + (int64_t)inst * n_split * rstride + (int64_t)g * rpg;
+  const int nsl = n_split / n_ranks;                        // splits per rank
+  const int64_t rank_stride = (int64_t)(gridDim.x / groups) * nsl * rstride;  // one rank's records
+  const float4* src = ws + (int64_t)inst * nsl * rstride + (int64_t)g * rpg;
   // 4 independent accumulators: 4 record loads in flight and 4 merge chains
   float n[4] = {0.f, 0.f, 0.f, 0.f}, mean[4] = {0.f, 0.f, 0.f, 0.f}, m2[4] = {0.f, 0.f, 0.f, 0.f};
   for (int r0 = threadIdx.x; r0 < nrec; r0 += 4 * NT) {
@@ -199,7 +205,8 @@ __global__ __launch_bounds__(NT) void gn_finalize_kernel(const float4* ws, int n
     for (int u = 0; u < 4; ++u) {
       const int r = r0 + u * NT;
       const int s = r / rpg, q = r - s * rpg;
-      v[u] = r < nrec ? src[(int64_t)s * rstride + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int w = s / nsl;  // (n_ranks == 1: w = 0, the split is s)
+      v[u] = r < nrec ? src[w * rank_stride + (int64_t)(s - w * nsl) * rstride + q] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) chan_merge(n[u], mean[u], m2[u], v[u].x, v[u].y, v[u].z);
@@ -673,6 +680,18 @@ extern "C" int vd_gn_finalize_g(const float* ws, int64_t n_inst, int32_t n_split
   hipLaunchKernelGGL(gn_finalize_kernel<true>, dim3((unsigned)(n_inst * groups)), dim3(NT), 0,
                      (hipStream_t)stream, (const float4*)ws, n_split_total, C, groups, eps, gamma,
                      beta, (float2*)scale_shift);
+  return vd_launch_status();
+}
+
+extern "C" int vd_gn_finalize_g_ranks(const float* ws, int64_t n_inst, int32_t n_ranks, int32_t n_split_per_rank,
+                                      int64_t C, int32_t groups, float eps, const float* gamma, const float* beta,
+                                      float* scale_shift, vd_stream_t stream) {
+  VD_CHECK_ARG(ws && gamma && beta && scale_shift && n_inst > 0 && n_ranks > 0 && n_split_per_rank > 0);
+  VD_CHECK_ARG((int64_t)n_ranks * n_split_per_rank < 0x7fffffff);
+  VD_CHECK_ARG(groups > 0 && C % groups == 0 && n_inst * groups < 0x7fffffff);
+  hipLaunchKernelGGL(gn_finalize_kernel<true>, dim3((unsigned)(n_inst * groups)), dim3(NT), 0,
+                     (hipStream_t)stream, (const float4*)ws, n_ranks * n_split_per_rank, C, groups, eps, gamma,
+                     beta, (float2*)scale_shift, (int)n_ranks);
   return vd_launch_status();
 }
 

@@ -31,6 +31,7 @@ SIGNATURES = {
     "vd_gn_partial": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp], c_i32),
     "vd_gn_finalize": ([c_vp, c_i64, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp], c_i32),
     "vd_gn_finalize_g": ([c_vp, c_i64, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp], c_i32),
+    "vd_gn_finalize_g_ranks": ([c_vp, c_i64, c_i32, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp], c_i32),
     "vd_gn_small": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_f32, c_vp, c_vp, c_i32, c_vp, c_i64,
                      c_vp], c_i32),
     "vd_gn_apply": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp, c_i64, c_vp], c_i32),

@@ -70,6 +70,15 @@ class FrameShard:
         dist.all_gather_into_tensor(out, ws.contiguous().reshape(-1), group=self.group)
         return out.reshape((self.world,) + tuple(ws.shape)).transpose(0, 1).reshape(ws.shape[0], self.world * ws.shape[1], *ws.shape[2:]).contiguous()
 
+    def gather_gn_records(self, ws: torch.Tensor) -> torch.Tensor:
+        """[inst, splits, G, 4] per rank -> rank-major [world, inst, splits, G, 4] on every rank: the
+        all-gather's output as it lands, a view (vdiff.ops.gn_finalize_g merges it in
+        gather_gn_partials' split order through vd_gn_finalize_g_ranks, so the result is the same
+        bits without the transpose copy — round 6)."""
+        out = torch.empty(self.world * ws.numel(), device=ws.device, dtype=ws.dtype)
+        dist.all_gather_into_tensor(out, ws.contiguous().reshape(-1), group=self.group)
+        return out.reshape((self.world,) + tuple(ws.shape))
+
     # -- temporal window re-shard ---------------------------------------------
     def _a2a(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         out = torch.empty_like(x) if out is None else out

@@ -423,7 +423,8 @@ class AnimateDiffTransformer3D(nn.Module):
         hw = x.h * x.w
         B, Fl = ctx.batch, ctx.frames
         dist = ctx.dist
-        gather = dist.gather_gn_partials if dist is not None else None
+        # the motion norm's records (C <= 2560: per-group) all-gathered rank-major, no transpose copy
+        gather = dist.gather_gn_records if dist is not None else None
         blk = self.transformer_blocks[0]
         if dist is not None and dist.fused_ok(B, Fl, hw):
             # the fused re-shard (FrameShard.send_perm): norm -> send order, one all-to-all, the

@@ -319,6 +319,14 @@ def gn_partial_g(x, C, n_inst, pix, n_split, groups, x1=None):
 
 
 def gn_finalize_g(ws, C, eps, gamma, beta):
+    """ws: [inst, splits, groups, 4] records, or rank-major [ranks, inst, splits of a rank, groups, 4]
+    (FrameShard.gather_gn_records: the all-gather output as it lands, vd_gn_finalize_g_ranks)."""
+    if ws.dim() == 5:
+        n_ranks, n_inst, nsl, groups, _ = ws.shape
+        ss = torch.empty(n_inst, C, 2, device=ws.device, dtype=torch.float32)
+        check(lib().vd_gn_finalize_g_ranks(_p(ws), n_inst, n_ranks, nsl, C, groups, eps, _p(gamma), _p(beta),
+                                           _p(ss), _stream()), "vd_gn_finalize_g_ranks")
+        return ss
     n_inst, n_split, groups, _ = ws.shape
     ss = torch.empty(n_inst, C, 2, device=ws.device, dtype=torch.float32)
     check(lib().vd_gn_finalize_g(_p(ws), n_inst, n_split, C, groups, eps, _p(gamma), _p(beta), _p(ss),
@@ -365,12 +373,14 @@ def group_norm(x, n_inst, pix, groups, eps, gamma, beta, silu=False, x1=None, ga
     if grec:  # per-group records (round 5: C/groups times fewer for the gather and the finalize)
         ws = gn_partial_g(x, C, n_inst, pix, n_split, groups, x1=x1)
         if gather is not None:
-            ws = gather(ws)
+            ws = gather(ws)  # [inst, ranks*splits, G, 4], or rank-major [ranks, inst, splits, G, 4]
         ss = gn_finalize_g(ws, C, eps, gamma, beta)
     else:
         ws = gn_partial(x, C, n_inst, pix, n_split, x1=x1)
         if gather is not None:
             ws = gather(ws)
+            if ws.dim() == 5:  # rank-major records: vd_gn_finalize takes [inst, ranks*splits, C, 4]
+                ws = ws.transpose(0, 1).reshape(n_inst, -1, C, 4).contiguous()
         ss = gn_finalize(ws, groups, eps, gamma, beta)
     return gn_apply(x, ss, pix, silu, x1=x1, rev3=rev3)
 
