@@ -401,6 +401,7 @@ def main():
     videos = world if replicas else 1           # independent videos the node denoised per step
     sps = videos * args.steps / elapsed
     graph_ok = loop.graph is not None
+    cfg_dedup = bool(getattr(loop, "cfg_dedup", False))  # the loop's CFG dedup (step_mfma labels it)
     ms = 1e3 * elapsed / args.steps
     del loop
 
@@ -455,7 +456,7 @@ def main():
     step_mfma = {"algorithmic_tflop_per_step_per_gpu": round(gpu_tflop, 3),
                  "achieved": round(step_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                  "frac": round(step_tf / PEAK_BF16_TFLOPS, 4)}
-    dedup = getattr(loop, "cfg_dedup", False) and lay.cfg_shard is None and cfg_name in CFG_DEDUP_TFLOP
+    dedup = cfg_dedup and lay.cfg_shard is None and cfg_name in CFG_DEDUP_TFLOP
     if dedup:  # the duplicated CFG-half work the step skips (bit-identical outputs): labelled, not hidden
         saved = CFG_DEDUP_TFLOP[cfg_name] * frames / 16 / (1 if replicas else world)
         step_mfma["cfg_dedup_tflop_saved"] = round(saved, 3)

@@ -638,12 +638,19 @@ __device__ __forceinline__ bool f32_loop(bf16_t* lds, const bf16_t* kb_ptr, cons
 // waves per SIMD measured slower, 1010 vs 878 us: profiles/r02_attn_occupancy_ab.txt).
 // FIX: flash40's exact fix-up pass — a block whose first output element is a NaN flag (flash40
 // found a score jump past its fast pass's range there) recomputes its 256 queries with the exact
-// pass; every other block returns at once.
+// pass.  Round 6: one workgroup per F32_FIXW blocks (fix_blocks in all), whose first F32_FIXW
+// lanes read those blocks' flags at once (one load latency) and which then recomputes the flagged
+// ones in turn — the launch that follows every flash40 call was one workgroup per block, 4096 at
+// the level-1 self-attention, ~8 us with nothing flagged.  The fix-up runs QB = 1 (128-query
+// blocks, two per flagged quarter; a query's exact-pass arithmetic does not depend on QB): the
+// block loop at QB = 2's 256 VGPRs spilled.  Both halves of a quarter sit in one workgroup
+// (F32_FIXW even) and every flag is read before any block overwrites one.
+constexpr int F32_FIXW = 16;
 template <int D, bool UNITC, bool FIX = false, int QB = 2>
 __global__ __launch_bounds__(NT, 2) void flash32_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
     const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
-    int64_t sq, int64_t skv, int64_t kv_div, float c, int out_f32 = 0) {
+    int64_t sq, int64_t skv, int64_t kv_div, float c, int out_f32 = 0, int64_t fix_blocks = 0) {
   using C = F32Cfg<D>;
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * C::STAGE];
 
@@ -653,7 +660,14 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
   // consecutive logical ids and xcd_remap keeps consecutive ids on one XCD, so
   // that head's K/V is fetched into one L2 instead of eight.
   const int nqb = (int)((sq + 4 * 32 * QB - 1) / (4 * 32 * QB));
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  auto flag_of = [&](int64_t lid) {  // the block's flag: a NaN in the first output element of its
+    const int qblk = (int)(lid % nqb);  // flash40 256-query quarter
+    const int h = (int)((lid / nqb) % heads);
+    const int64_t b = (lid / nqb) / heads;
+    const int64_t f = (b * sq + (((int64_t)qblk * (4 * 32 * QB)) & ~(int64_t)255)) * ldo + (int64_t)h * D;
+    return out_f32 ? __builtin_isnan(((const float*)o)[f]) : ((o[f] & 0x7FFF) > 0x7F80);
+  };
+  auto block = [&](int lid) {
   const int qblk = lid % nqb;
   const int h = (lid / nqb) % heads;
   const int64_t b = (lid / nqb) / heads;
@@ -662,11 +676,6 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
   const bf16_t* qb_ptr = q + b * sq * ldq + (int64_t)h * D;
   const bf16_t* kb_ptr = k + bkv * skv * ldk + (int64_t)h * D;
   const bf16_t* vb_ptr = v + bkv * skv * ldv + (int64_t)h * D;
-  if constexpr (FIX) {
-    const int64_t f = (b * sq + (int64_t)qblk * (4 * 32 * QB)) * ldo + (int64_t)h * D;
-    const bool flagged = out_f32 ? __builtin_isnan(((const float*)o)[f]) : ((o[f] & 0x7FFF) > 0x7F80);
-    if (!flagged) return;
-  }
 
   // Q'^T fragments: lane holds Q'[q0 + qb*32 + r32][16*ks + 8*hh .. +7].  Q is
   // used as given (no bf16 prescale: that second rounding costs ~0.4% in P); with
@@ -762,6 +771,28 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
         if (qi < sq && dd + 8 <= D) *(uint4*)(orow + dd) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
       }
     }
+  }
+  };
+  if constexpr (FIX) {
+    __shared__ unsigned long long fmask;
+    if (wave == 0) {
+      const int64_t j = (int64_t)blockIdx.x * F32_FIXW + lane;
+      const unsigned long long m = __ballot(lane < F32_FIXW && j < fix_blocks && flag_of(j));
+      if (lane == 0) fmask = m;
+    }
+    __syncthreads();
+    // workgroup-uniform: kept in SGPRs (a VGPR copy live across the exact pass spilled)
+    const unsigned long long fm = fmask;
+    unsigned long long m = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(fm >> 32)) << 32) |
+                           __builtin_amdgcn_readfirstlane((uint32_t)fm);
+    while (m) {
+      const int bit = __builtin_ctzll(m);
+      m &= m - 1;
+      block((int)((int64_t)blockIdx.x * F32_FIXW + bit));
+      __syncthreads();  // the next block rewrites the LDS tiles and padding
+    }
+  } else {
+    block(xcd_remap(blockIdx.x, gridDim.x));
   }
 }
 
@@ -1302,17 +1333,20 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
       const int64_t nblk = (sq + F4_QWG - 1) / F4_QWG * heads * batch;
       if (nblk > 0x7fffffff) return VD_EINVAL;
       const dim3 grid((unsigned)nblk);
-      const dim3 fix((unsigned)((sq + 255) / 256 * heads * batch));
+      const int64_t nfix = (sq + 127) / 128 * heads * batch;  // 128-query blocks of the exact pass (QB = 1)
+      const dim3 fix((unsigned)((nfix + F32_FIXW - 1) / F32_FIXW));
       if (c == 1.0f) {
         hipLaunchKernelGGL((flash40_kernel<true>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,
                            ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-        hipLaunchKernelGGL((flash32_kernel<D, true, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+        hipLaunchKernelGGL((flash32_kernel<D, true, true, 1>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32,
+                           nfix);
       } else {
         hipLaunchKernelGGL((flash40_kernel<false>), grid, dim3(F4_NT), 0, s, (const bf16_t*)q, ldq, (const bf16_t*)k,
                            ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
-        hipLaunchKernelGGL((flash32_kernel<D, false, true>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
-                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32);
+        hipLaunchKernelGGL((flash32_kernel<D, false, true, 1>), fix, dim3(NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c, out_f32,
+                           nfix);
       }
       return vd_launch_status();
     }
