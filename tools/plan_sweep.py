@@ -13,7 +13,7 @@ import torch  # noqa: E402
 from vdiff import ops  # noqa: E402
 from vdiff._lib import lib  # noqa: E402
 
-PATHS = {"auto": 0, "v2": 2, "v3": 3, "v5": 5, "v6": 6}
+PATHS = {"auto": 0, "v2": 2, "v3": 3, "v5": 5, "v6": 6, "v8": 8}
 g = torch.Generator(device="cuda").manual_seed(0)
 
 
