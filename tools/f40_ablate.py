@@ -8,7 +8,9 @@ bench.py's `synthetic` inputs), arms interleaved in one process:
   pv1half half of the PV d-block-1 MFMAs skipped (4 of the 28 per wave-tile): what a 16x16x32 PV for
           d 32..47 (the d = 40 -> 48 pad instead of -> 64) would save in matrix-pipe time, before
           the 16 permlane16_swap per wave-tile that form needs to re-lay P;
-  qk2     one of QK^T's three k-steps per key block skipped (12 -> 8 MFMAs): the QK share.
+  qk2     one of QK^T's three k-steps per key block skipped (12 -> 8 MFMAs): the QK share;
+  ord_qpq / ord_qqp  the M phase as PV(d0) QK(k0) PV(d1) QK(k1) / PV(d0) QK QK PV(d1) instead of
+          PV(d0) PV(d1) QK QK — schedule variants with the same arithmetic (F40_VARIANTS=... selects).
 
     python tools/f40_ablate.py --build    # here (CPU): tools/diag_f40/libvdiff_f40_*.so
     python tools/f40_ablate.py            # GPU box
@@ -49,6 +51,35 @@ PV_HALF = """  auto pv = [&](int db) {
           if (db == 0 || s2 == 0)
             oacc[db][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[db][kb][s2], pf[kb][s2][qb], oacc[db][qb], 0, 0, 0);
   };"""
+M_OLD = """    v1_join();
+    if (more) read_k(t + 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    pv(1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      qk(0);
+      qk(1);
+    }
+"""
+M_QPQ = """    v1_join();
+    if (more) read_k(t + 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) qk(0);
+    __builtin_amdgcn_sched_barrier(0);
+    pv(1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) qk(1);
+"""
+M_QQP = """    v1_join();
+    if (more) read_k(t + 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      qk(0);
+      qk(1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    pv(1);
+"""
 QK_OLD = """  auto qk = [&](int kb) {  // S(kb) = K'.Q'^T from the fragments read_k left
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks)"""
@@ -69,13 +100,16 @@ def instrument(text: str, name: str) -> str:
     elif name == "pv1half":
         assert body.count(PV_OLD) == 1
         body = body.replace(PV_OLD, PV_HALF)
+    elif name in ("ord_qpq", "ord_qqp"):  # schedule variants with the product's arithmetic (same bits)
+        assert body.count(M_OLD) == 1
+        body = body.replace(M_OLD, M_QPQ if name == "ord_qpq" else M_QQP)
     elif name == "qk2":
         assert body.count(QK_OLD) == 1
         body = body.replace(QK_OLD, QK_2)
     return text[:i0] + body + text[i1:]
 
 
-VARIANTS = ("noexp", "pv1half", "qk2")
+VARIANTS = tuple(os.environ.get("F40_VARIANTS", "noexp,pv1half,qk2").split(","))
 
 
 def build():
