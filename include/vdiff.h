@@ -41,7 +41,7 @@ enum vd_status {
 };
 
 const char* vd_strerror(int code);
-int vd_version(void);  /* 5 */
+int vd_version(void);  /* 6 */
 /* Content hash (16 hex digits) of the sources and compile flags the library was built from
  * (video-diffusion-experiments_amd/build_ext.py); the Python loader compares it with the tree. */
 const char* vd_build_hash(void);

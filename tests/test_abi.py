@@ -27,7 +27,7 @@ def test_library_loads_and_exports_every_symbol():
     h = L.lib()
     for name in header_functions():
         assert hasattr(h, name), name
-    assert h.vd_version() == 5
+    assert h.vd_version() == 6
     from vdiff._srchash import source_hash
     import build_ext
     assert h.vd_build_hash().decode() == source_hash(build_ext.HASH_FLAGS)  # a build of THIS tree

@@ -252,7 +252,7 @@ extern "C" const char* vd_strerror(int code) {
   }
 }
 
-extern "C" int vd_version(void) { return 5; }  // 5: vd_gemm_desc rmap_* / ln_fold_*, vd_gemm_plan, vd_gn_apply_rev3, fp8 q_scale (round 5)
+extern "C" int vd_version(void) { return 6; }  // 6: vd_gn_finalize_g_ranks (round 6); 5: vd_gemm_desc rmap_* / ln_fold_*, vd_gemm_plan, vd_gn_apply_rev3, fp8 q_scale (round 5)
 
 #ifndef VD_BUILD_HASH
 #define VD_BUILD_HASH "unhashed"
