@@ -172,6 +172,12 @@ def _worker(rank, world, port, errq):
         got = torch.nn.functional.conv3d(hv, wt, padding=(0, 1, 1))
         err = (got - full[:, :, rank * Fl:(rank + 1) * Fl]).abs().max().item()
         assert err < 1e-4, f"halo'd temporal conv max err {err}"
+        # ---- 3b. the GroupNorm records rank-major (round 6: FrameShard.gather_gn_records, what
+        # vd_gn_finalize_g_ranks merges) hold exactly gather_gn_partials' records, split order kept
+        recs = torch.randn(B, 3, 32, 4) + rank
+        rm = fs.gather_gn_records(recs)
+        assert rm.shape == (world, B, 3, 32, 4)
+        assert torch.equal(rm.transpose(0, 1).reshape(B, world * 3, 32, 4), fs.gather_gn_partials(recs))
         # ---- 4. latent all-gather over frames
         lat = torch.full((1, 4, Fl, 2, 2), float(rank))
         g = fs.all_gather_frames(lat)
