@@ -9,6 +9,10 @@ bench.py's `synthetic` inputs), arms interleaved in one process:
           d 32..47 (the d = 40 -> 48 pad instead of -> 64) would save in matrix-pipe time, before
           the 16 permlane16_swap per wave-tile that form needs to re-lay P;
   qk2     one of QK^T's three k-steps per key block skipped (12 -> 8 MFMAs): the QK share;
+  novphase / nomphase  one phase's work removed (V: decide, softmax, V reads; M: its MFMAs and
+          reads): each phase alone, behind the same barriers and DMA;
+  vread_early  the V phase's V^T fragment reads issued before its exps (their LDS latency under
+          the exps instead of after them) — a schedule variant with the same arithmetic;
   ord_qpq / ord_qqp  the M phase as PV(d0) QK(k0) PV(d1) QK(k1) / PV(d0) QK QK PV(d1) instead of
           PV(d0) PV(d1) QK QK — schedule variants with the same arithmetic (F40_VARIANTS=... selects).
 
@@ -88,6 +92,15 @@ QK_2 = """  auto qk = [&](int kb) {  // S(kb) = K'.Q'^T from the fragments read_
     for (int ks = 0; ks < 3; ks += 2)"""
 
 
+SOFTMAX_CALL = """    if (t > 0) decide(t);
+    softmax();
+    __builtin_amdgcn_sched_barrier(0);
+    read_v(t, 0);
+"""
+MPHASE_CALL = """    mphase(t);
+"""
+
+
 def instrument(text: str, name: str) -> str:
     i0 = text.index("// ============================================================ flash40")
     i1 = text.index("// kernel (per call, test hook")
@@ -103,10 +116,31 @@ def instrument(text: str, name: str) -> str:
     elif name in ("ord_qpq", "ord_qqp"):  # schedule variants with the product's arithmetic (same bits)
         assert body.count(M_OLD) == 1
         body = body.replace(M_OLD, M_QPQ if name == "ord_qpq" else M_QQP)
+    elif name == "vread_early":  # schedule variant (same bits): tile t's V^T reads before the exps
+        assert body.count(SOFTMAX_CALL) == 1
+        body = body.replace(SOFTMAX_CALL, """    read_v(t, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (t > 0) decide(t);
+    softmax();
+    __builtin_amdgcn_sched_barrier(0);
+""")
+    elif name == "novphase":  # the V phase's work removed (decide, softmax, V reads): M phase alone
+        assert body.count(SOFTMAX_CALL) == 1
+        body = body.replace(SOFTMAX_CALL, "")
+        assert body.count("    bad |= __any(over);") == 1  # garbage P: never flag the block (no fix-up pass)
+        body = body.replace("    bad |= __any(over);", "")
+    elif name == "nomphase":  # the M phase's MFMAs and reads removed: V phase alone
+        assert body.count(MPHASE_CALL) == 1
+        body = body.replace(MPHASE_CALL, "")
     elif name == "qk2":
         assert body.count(QK_OLD) == 1
         body = body.replace(QK_OLD, QK_2)
-    return text[:i0] + body + text[i1:]
+    out = text[:i0] + body + text[i1:]
+    if name in ("novphase", "nomphase"):  # their outputs are garbage / NaN: keep the exact fix-up pass out
+        flag = "    return out_f32 ? __builtin_isnan(((const float*)o)[f]) : ((o[f] & 0x7FFF) > 0x7F80);"
+        assert out.count(flag) == 1
+        out = out.replace(flag, "    return false;")
+    return out
 
 
 VARIANTS = tuple(os.environ.get("F40_VARIANTS", "noexp,pv1half,qk2").split(","))
