@@ -13,6 +13,9 @@ bench.py's `synthetic` inputs), arms interleaved in one process:
           reads): each phase alone, behind the same barriers and DMA;
   vread_early  the V phase's V^T fragment reads issued before its exps (their LDS latency under
           the exps instead of after them) — a schedule variant with the same arithmetic;
+  dma_v   group 1's LDS-DMA pieces issued at the start of its V phase (the round-5 schedule) instead
+          of its M phase (as group 0's; adopted in round 6 after the dma_m arm of this tool measured
+          -1.6 %) — a schedule variant with the same arithmetic;
   ord_qpq / ord_qqp  the M phase as PV(d0) QK(k0) PV(d1) QK(k1) / PV(d0) QK QK PV(d1) instead of
           PV(d0) PV(d1) QK QK — schedule variants with the same arithmetic (F40_VARIANTS=... selects).
 
@@ -124,6 +127,12 @@ def instrument(text: str, name: str) -> str:
     softmax();
     __builtin_amdgcn_sched_barrier(0);
 """)
+    elif name == "dma_v":  # schedule variant (same bits): group 1's DMA back in its V phase (the
+        # round-5 schedule; the product adopted dma_m — group 1 issues in its M phase — in round 6)
+        top = "  for (int t = 0; t < T; ++t) {\n"
+        assert body.count(top) == 1 and body.count("    issue(t + 3);\n    mphase(t);\n") == 1
+        body = body.replace(top, top + "    if (!g0) issue(t + 3);\n")
+        body = body.replace("    issue(t + 3);\n    mphase(t);\n", "    if (g0) issue(t + 3);\n    mphase(t);\n")
     elif name == "novphase":  # the V phase's work removed (decide, softmax, V reads): M phase alone
         assert body.count(SOFTMAX_CALL) == 1
         body = body.replace(SOFTMAX_CALL, "")

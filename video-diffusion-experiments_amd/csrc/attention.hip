@@ -821,7 +821,7 @@ __global__ __launch_bounds__(NT, 2) void flash32_kernel(
 // buffer's range — reads all zeros: score 0, P = 1, V row and ones column 0, i.e. no
 // contribution, with no masking code.  The K' ds_read_b128 of 32 keys is 512 contiguous bytes
 // and the V tr-read of 4 keys x 32 d 256 contiguous bytes: conflict-free.  Tile u is issued at
-// phase 2u-4 and waited for (counted vmcnt; the DMA is inline asm so hipcc neither counts it nor
+// phase 2u-4 (group 0) / 2u-3 (group 1) and waited for (counted vmcnt; the DMA is inline asm so hipcc neither counts it nor
 // drains it before the LDS reads) before the barrier that ends phase 2u-1; the slot it
 // overwrites (tile u-4) was last read in phase 2u-6.
 constexpr int F4_NW = 8, F4_NT = 512, F4_QB = 2, F4_QWG = F4_NW * 32 * F4_QB;
@@ -1109,7 +1109,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
     }
     __builtin_amdgcn_s_setprio(0);
   };
-  // tile u's DMA: issued at phase 2u-4 (u >= 2), waited for at the end of phase 2u-1
+  // tile u's DMA: issued at phase 2u-4 (group 0) / 2u-3 (group 1) (u >= 3), waited for at the end of phase 2u-1
   auto issue = [&](int u) {
     if (issuer && u < T) f4_issue<2>(dma, lds0, u, skv);
   };
@@ -1126,7 +1126,10 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   bar();
   // one instruction stream for both groups; group 1 (waves 4-7) runs one phase behind:
   //   group 0: ph 0 [DMA 2, QK(0)] | ph 2t+1 [V(t), wait t+1] | ph 2t+2 [DMA t+3, M(t)] | ph 2T+1 []
-  //   group 1: ph 0 [DMA 2] | ph 1 [QK(0), wait 1] | ph 2t+2 [DMA t+3, V(t)] | ph 2t+3 [M(t), wait t+2]
+  //   group 1: ph 0 [DMA 2] | ph 1 [QK(0), wait 1] | ph 2t+2 [V(t)] | ph 2t+3 [DMA t+3, M(t), wait t+2]
+  // (round 6: group 1's DMA moved from its V phase to its M phase, like group 0's — the V phase is the
+  // longer one, 609 vs 406 us of the L1 launch with the other phase's work removed; -1.6 % per launch,
+  // profiles/r06_flash40_ablations.txt)
   issue(2);
   if (!g0) bar();
   read_k(0, 0);
@@ -1137,7 +1140,6 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   if (!g0) wait_tile(1);
   bar();
   for (int t = 0; t < T; ++t) {
-    if (!g0) issue(t + 3);
     // tile t's decisions open its V phase (round 4; they closed the M phase that computed S(t)):
     // the same data at the same point of the tile order — after QK^T(t), before softmax(t),
     // PV(t) and QK^T(t+1) — but the M wave now reaches the barrier straight after its last MFMA
@@ -1157,7 +1159,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
       }
     if (g0) wait_tile(t + 1);
     bar();
-    if (g0) issue(t + 3);
+    issue(t + 3);
     mphase(t);
     if (!g0) wait_tile(t + 2);
     bar();
