@@ -141,9 +141,35 @@ def instrument(text: str, name: str) -> str:
     elif name == "nomphase":  # the M phase's MFMAs and reads removed: V phase alone
         assert body.count(MPHASE_CALL) == 1
         body = body.replace(MPHASE_CALL, "")
+    elif name == "stamps":  # s_memtime stamps at the phase boundaries (shares, not the run time)
+        assert body.count(LOOP_OLD) == 1
+        body = body.replace(LOOP_OLD, LOOP_STAMPED)
+        ret = "  return bad;\n}\n"
+        assert body.count(ret) == 1
+        body = body.replace(ret, STAMP_STORE + ret)
+    elif name == "dec1":  # schedule variant (same bits): decide(t > 1) with the partner exchange up
+        # front (the round-5 form; the product adopted dec2 in round 6)
+        assert body.count(DEC_NEW_PRODUCT) == 1
+        body = body.replace(DEC_NEW_PRODUCT, DEC_OLD)
+    elif name == "dma_gap":  # schedule variant (same bits)
+        if True:
+            assert body.count(GAP_OLD) == 1 and body.count("    issue(t + 3);\n    mphase(t);\n") == 1
+            body = body.replace(GAP_OLD, GAP_NEW)
+            body = body.replace("    issue(t + 3);\n    mphase(t);\n", "    mphase(t);\n")
+            anchor = "template <bool UNITC>\n__device__ __forceinline__ bool f4_loop("
+            assert body.count(anchor) == 1
+            body = body.replace(anchor, ISSUE_ONE + anchor)
     elif name == "qk2":
         assert body.count(QK_OLD) == 1
         body = body.replace(QK_OLD, QK_2)
+    if name == "stamps":
+        anchor = "  // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere\n"
+        assert body.count(anchor) == 1
+        body = body.replace(anchor, "  unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};\n" + anchor)
+        top = "  for (int t = 0; t < T; ++t) {\n"
+        assert body.count(top) == 1
+        body = body.replace(top, "  unsigned long long tp_ = f4_stamp();\n" + top)
+        body = STAMP_DEFS + body
     out = text[:i0] + body + text[i1:]
     if name in ("novphase", "nomphase"):  # their outputs are garbage / NaN: keep the exact fix-up pass out
         flag = "    return out_f32 ? __builtin_isnan(((const float*)o)[f]) : ((o[f] & 0x7FFF) > 0x7F80);"
@@ -151,6 +177,140 @@ def instrument(text: str, name: str) -> str:
         out = out.replace(flag, "    return false;")
     return out
 
+
+LOOP_OLD = """    if (t > 0) decide(t);
+    softmax();
+    __builtin_amdgcn_sched_barrier(0);
+    read_v(t, 0);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        f4_pin(vfr[0][kb][s2]);
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) f4_pin(pf[kb][s2][qb]);
+      }
+    if (g0) wait_tile(t + 1);
+    bar();
+    issue(t + 3);
+    mphase(t);
+    if (!g0) wait_tile(t + 2);
+    bar();
+  }
+"""
+LOOP_STAMPED = """    if (t > 0) decide(t);
+    F4ST(0);
+    softmax();
+    __builtin_amdgcn_sched_barrier(0);
+    F4ST(1);
+    read_v(t, 0);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        f4_pin(vfr[0][kb][s2]);
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) f4_pin(pf[kb][s2][qb]);
+      }
+    if (g0) wait_tile(t + 1);
+    F4ST(2);
+    bar();
+    F4ST(3);
+    issue(t + 3);
+    F4ST(4);
+    mphase(t);
+    F4ST(5);
+    if (!g0) wait_tile(t + 2);
+    F4ST(6);
+    bar();
+    F4ST(7);
+  }
+"""
+# the stamp (MI355X guide idiom: s_memtime + lgkmcnt(0) in one statement, sched barriers around it),
+# the per-wave scalar sums, and their store after the loop (lane 0 of each wave, a buffer of its own)
+STAMP_DEFS = """
+__device__ unsigned long long f4_stamp_buf[256][8][9];
+__device__ __forceinline__ unsigned long long f4_stamp() {
+  unsigned long long x;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\\n\\ts_waitcnt lgkmcnt(0)" : "=s"(x) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return x;
+}
+#define F4ST(i) do { const unsigned long long a_ = f4_stamp(); st_[i] += a_ - tp_; tp_ = a_; } while (0)
+extern "C" int f4_stamp_read(void* dst) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(f4_stamp_buf), sizeof(f4_stamp_buf));
+}
+"""
+STAMP_STORE = """  {
+    const int w_ = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (blockIdx.x < 256 && (threadIdx.x & 63) == 0) {
+      for (int i = 0; i < 8; ++i) f4_stamp_buf[blockIdx.x][w_][i] = st_[i];
+      f4_stamp_buf[blockIdx.x][w_][8] = (unsigned long long)T;
+    }
+  }
+"""
+
+# decide(t > 1) without the partner exchange: the wave-wide any() over the lanes that hold a row
+# sum (half L_H) is the same decision; the exchange moves into the (rare) rescale branch
+DEC_OLD = """      float lq[QB];
+      bool resc = false, over = false;
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const float lown = oacc[C::L_DB][qb][C::L_I];
+        const float lp = partner32(lown);
+        lq[qb] = hh == C::L_H ? lown : lp;
+        resc |= lq[qb] > RESCALE;
+        over |= !(lq[qb] < BAD);
+      }
+      if (__any(over)) {
+        bad = true;
+      } else if (__any(resc)) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {"""
+DEC_NEW = """      bool resc = false, over = false;
+      const bool own = hh == C::L_H;
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) {
+        const float lown = oacc[C::L_DB][qb][C::L_I];
+        resc |= own && lown > RESCALE;
+        over |= own && !(lown < BAD);
+      }
+      if (__any(over)) {
+        bad = true;
+      } else if (__any(resc)) {
+        float lq[QB];
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          const float lown = oacc[C::L_DB][qb][C::L_I];
+          const float lp = partner32(lown);
+          lq[qb] = own ? lown : lp;
+        }
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {"""
+DEC_NEW_PRODUCT = DEC_NEW.replace(
+    "      bool resc = false, over = false;\n      const bool own = hh == C::L_H;",
+    "      // the wave-wide any() over the lanes that hold a row sum (half L_H) is the decision; the\n"
+    "      // partner exchange is needed only for a rescale (round 6: -0.7 %, profiles/r06_flash40_ablations.txt)\n"
+    "      bool resc = false, over = false;\n      const bool own = hh == C::L_H;")
+# the M phase's two DMA pieces in PV(d-block 0)'s empty MFMA gaps 6 and 7 instead of before its first MFMA
+GAP_OLD = """        if (r < 8) read_v1_piece(t, r);
+        else if (r < 11 && more) read_k0_piece(t + 1, r - 8);
+      }
+"""
+GAP_NEW = """        if (r < 8) read_v1_piece(t, r);
+        else if (r < 11 && more) read_k0_piece(t + 1, r - 8);
+      }
+      if (i >= 6 && issuer && t + 3 < T) f4_issue_one(dma, lds0, t + 3, skv, i - 6);
+"""
+ISSUE_ONE = """__device__ __forceinline__ void f4_issue_one(const F4Dma& m, uint32_t lds0, int t, int64_t skv, int i) {
+  const uint32_t key0 = (uint32_t)t * KT;
+  const uint32_t slot = lds0 + (uint32_t)(t % F4_RING) * F4_SLOT;
+  const uint32_t off = m.step[i] ? m.voff[i] + key0 * m.step[i] : ((int64_t)(key0 + m.row[i]) < skv ? 0u : 16u);
+  f4_dma(m.rs[i], slot + m.lds[i], off);
+}
+
+"""
 
 VARIANTS = tuple(os.environ.get("F40_VARIANTS", "noexp,pv1half,qk2").split(","))
 
@@ -199,6 +359,14 @@ def run(rounds: int):
         assert rc == 0, rc
 
     fl = 4.0 * S * S * d * heads * imgs
+    call(libs["product"])
+    ref = out.clone()
+    for a, lb in libs.items():
+        if a != "product":
+            out.zero_()
+            call(lb)
+            torch.cuda.synchronize()
+            print(f"{a:8s} output {'bit-identical to' if torch.equal(out, ref) else 'DIFFERS from'} the product's", flush=True)
     res = {a: [] for a in libs}
     for r in range(rounds + 1):
         for a, lb in libs.items():
@@ -212,6 +380,24 @@ def run(rounds: int):
             torch.cuda.synchronize()
             if r:
                 res[a].append(e0.elapsed_time(e1) * 100.0)
+    if "stamps" in libs:
+        import numpy as np
+        buf = np.zeros((256, 8, 9), dtype=np.uint64)
+        lb = libs["stamps"]
+        lb.f4_stamp_read.argtypes, lb.f4_stamp_read.restype = [C.c_void_p], C.c_int
+        torch.cuda.synchronize()
+        assert lb.f4_stamp_read(buf.ctypes.data) == 0
+        segs = ["decide", "softmax", "vtail+wait", "bar(V end)", "dma issue", "mphase", "wait(g1)", "bar(M end)"]
+        per = buf[:, :, :8].astype(np.float64) / np.maximum(buf[:, :, 8:9].astype(np.float64), 1)
+        print("stamps: cycles per loop iteration (s_memtime ticks), mean over the first 256 workgroups of the "
+              "last stamped launch; each stamp itself costs ~40", flush=True)
+        for gname, ws in (("group 0 (waves 0-3)", slice(0, 4)), ("group 1 (waves 4-7)", slice(4, 8))):
+            m = per[:, ws, :].mean(axis=(0, 1))
+            print(f"  {gname}: " + "  ".join(f"{s} {v:6.0f}" for s, v in zip(segs, m)) + f"  | total {m.sum():6.0f}",
+                  flush=True)
+        for w in range(8):
+            m = per[:, w, :].mean(axis=0)
+            print(f"    wave {w}: " + " ".join(f"{v:6.0f}" for v in m), flush=True)
     base = sorted(res["product"])[len(res["product"]) // 2]
     for a, t in res.items():
         t = sorted(t)

@@ -1040,19 +1040,26 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
         }
       }
     } else if (t > 1) {
-      float lq[QB];
+      // the wave-wide any() over the lanes that hold a row sum (half L_H) is the decision; the
+      // partner exchange is needed only for a rescale (round 6: -0.7 %, profiles/r06_flash40_ablations.txt)
       bool resc = false, over = false;
+      const bool own = hh == C::L_H;
 #pragma unroll
       for (int qb = 0; qb < QB; ++qb) {
         const float lown = oacc[C::L_DB][qb][C::L_I];
-        const float lp = partner32(lown);
-        lq[qb] = hh == C::L_H ? lown : lp;
-        resc |= lq[qb] > RESCALE;
-        over |= !(lq[qb] < BAD);
+        resc |= own && lown > RESCALE;
+        over |= own && !(lown < BAD);
       }
       if (__any(over)) {
         bad = true;
       } else if (__any(resc)) {
+        float lq[QB];
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+          const float lown = oacc[C::L_DB][qb][C::L_I];
+          const float lp = partner32(lown);
+          lq[qb] = own ? lown : lp;
+        }
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb) {
           const float step = lq[qb] > RESCALE ? __builtin_amdgcn_logf(lq[qb]) : 0.f;
@@ -1168,11 +1175,7 @@ __device__ __forceinline__ bool f4_loop(const char* smem, uint32_t lds0, const F
   {  // the last tiles' row sums were not checked in the loop
     bool over = false;
 #pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-      const float lown = oacc[C::L_DB][qb][C::L_I];
-      const float lp = partner32(lown);
-      over |= !((hh == C::L_H ? lown : lp) < BAD);
-    }
+    for (int qb = 0; qb < QB; ++qb) over |= hh == C::L_H && !(oacc[C::L_DB][qb][C::L_I] < BAD);
     bad |= __any(over);
   }
   return bad;
