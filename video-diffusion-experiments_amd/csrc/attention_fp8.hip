@@ -455,7 +455,14 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
   uint32_t pw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int t = 0; t < ntiles; ++t) {
     const int ahead = (ntiles - 1 - t) < (F8S - 2) ? (ntiles - 1 - t) : (F8S - 2);
-    f8_wait(ahead * npc);                               // this wave's pieces of tile t landed
+    // this wave's pieces of tile t landed; the steady state as two constant waits (round 6: a
+    // runtime count became a ~50-instruction branch tree of s_waitcnt immediates per tile)
+    if (ahead == F8S - 2) {
+      if (wave == 0) f8_wait(3 * (F8S - 2));
+      else f8_wait(2 * (F8S - 2));
+    } else {
+      f8_wait(ahead * npc);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                       // everyone's; stage (t-1) % S free
     asm volatile("" ::: "memory");
