@@ -497,9 +497,11 @@ __global__ __launch_bounds__(NT, 2) void flash_fp8_v2_kernel(
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kb][i]);
-    mt = fmaxf(mt, partner32f(mt));
-    const float mab = FOLDED ? mt + m : mt * c;  // the tile's row max, log2 units
-    if (t == 0 || __any(mab > m + 8.f)) {         // wave-uniform
+    // the offset test on each lane's own half-row max: x -> fl(x + m) (or x c) is monotone, so the
+    // any() over lanes equals the any() over the row maxes; the partner exchange only when it moves
+    if (t == 0 || __any((FOLDED ? mt + m : mt * c) > m + 8.f)) {  // wave-uniform
+      mt = fmaxf(mt, partner32f(mt));
+      const float mab = FOLDED ? mt + m : mt * c;  // the tile's row max, log2 units
       const float mn = t == 0 ? mab : fmaxf(m, mab);
       const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(m - mn);
       if constexpr (FOLDED) {
