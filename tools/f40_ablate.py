@@ -162,6 +162,41 @@ def instrument(text: str, name: str) -> str:
     elif name == "qk2":
         assert body.count(QK_OLD) == 1
         body = body.replace(QK_OLD, QK_2)
+    # round 6, session 3: rebalancing the two sides of a phase (the V side: decide at its head and the
+    # V^T read latency drained before its barrier; the M side: the DMA issue at its head)
+    if name in ("dec_even", "dec_even_vnw", "dec_even_vnw_dmav"):  # row-sum check on even tiles only
+        assert body.count("    if (t > 0) decide(t);\n") == 1
+        body = body.replace("    if (t > 0) decide(t);\n", "    if (t > 0 && (t & 1) == 0) decide(t);\n")
+    if name in ("vnowait", "dec_even_vnw", "dec_even_vnw_dmav", "vnw_dmav"):
+        # the V-end barrier without lgkmcnt(0) (V^T(t)'s slot is next overwritten two phases later; the
+        # M-end barrier still drains), and no pin on the V^T fragments: their wait moves to PV's first MFMA
+        old = """    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        f4_pin(vfr[0][kb][s2]);
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) f4_pin(pf[kb][s2][qb]);
+      }
+    if (g0) wait_tile(t + 1);
+    bar();
+"""
+        new = """    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) f4_pin(pf[kb][s2][qb]);
+      }
+    if (g0) wait_tile(t + 1);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+"""
+        assert body.count(old) == 1
+        body = body.replace(old, new)
+    if name in ("dec_even_vnw_dmav", "vnw_dmav"):  # group 1's DMA in its V phase (as dma_v)
+        top = "  for (int t = 0; t < T; ++t) {\n"
+        assert body.count(top) == 1 and body.count("    issue(t + 3);\n    mphase(t);\n") == 1
+        body = body.replace(top, top + "    if (!g0) issue(t + 3);\n")
+        body = body.replace("    issue(t + 3);\n    mphase(t);\n", "    if (g0) issue(t + 3);\n    mphase(t);\n")
     if name == "stamps":
         anchor = "  // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere\n"
         assert body.count(anchor) == 1
