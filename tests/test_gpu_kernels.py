@@ -1031,6 +1031,46 @@ def test_flash_attention_deferred_max_unit_scale(attn_path, kind):
     close_bf16(got, want, abs_frac=2e-3 * v.float().abs().max().item() / want.abs().max().item())
 
 
+@pytest.mark.parametrize("kind", ["ramp", "creep", "late_spike", "huge_spike", "offset", "negative"])
+@pytest.mark.parametrize("unit", [False, True])
+def test_flash80_deferred_max(cuda, kind, unit):
+    """flash80 (round 6: the level-2 d = 80 self-attention on flash40's schedule, exact deferred max
+    decided on P = exp2(S)) through the deferred-max score patterns at d = 80, prescaled and on the
+    model's unit scale: "huge_spike" sends a P to inf (the rare branch recomputes it from the exact
+    tile max), "ramp" rescales every tile, "negative" needs mu from the data — no fix-up pass."""
+    q, k, v = _deferred_max_case(kind, d=80)
+    sq, skv, d = q.shape[0], k.shape[0], q.shape[1]
+    sc = None
+    if unit:
+        q = bf(q.float() * d ** -0.5 * math.log2(math.e))
+        sc = 1.0 / math.log2(math.e)
+    got = ops.attention(q, k, v, 1, 1, sq, skv, d, scale=sc, kernel="flash40")
+    assert torch.isfinite(got.float()).all()
+    want = sdpa_ref(q, k, v, 1, 1, sq, skv, d, scale=sc)
+    close_bf16(got, want, abs_frac=2e-3 * v.float().abs().max().item() / want.abs().max().item())
+
+
+@pytest.mark.parametrize("sq,skv,batch,kv_div", [(1024, 1024, 2, 1), (300, 300, 3, 1), (777, 640, 2, 2),
+                                               (1024, 128, 1, 1)])
+def test_flash80_matches_fp64(cuda, sq, skv, batch, kv_div):
+    """flash80 on the model's real-valued level-2 inputs (q, k, v ~ N(0, 1.5^2), fused-QKV row
+    strides, the softmax scale folded into q), ragged query blocks (sq not a multiple of its 256),
+    ragged key tiles, a K/V shared by kv_div query batches and the 2-tile minimum: bf16 output
+    within bf16 rounding of fp64 SDPA, and the automatic choice equal to the forced one."""
+    torch.manual_seed(sq + skv + 80)
+    heads, d = 8, 80
+    C = heads * d
+    q = rnd(batch * sq, 3 * C, std=1.5)[:, :C]
+    q = bf(q.float() * d ** -0.5 * math.log2(math.e))
+    kv = rnd(batch // kv_div * skv, 2 * C, std=1.5)
+    sc = 1.0 / math.log2(math.e)
+    got = ops.attention(q, kv[:, :C], kv[:, C:], batch, heads, sq, skv, d, kv_div=kv_div, scale=sc, kernel="flash40")
+    close_bf16(got, sdpa_ref(q, kv[:, :C], kv[:, C:], batch, heads, sq, skv, d, kv_div=kv_div, scale=sc))
+    if skv >= 256:
+        auto = ops.attention(q, kv[:, :C], kv[:, C:], batch, heads, sq, skv, d, kv_div=kv_div, scale=sc)
+        assert torch.equal(auto, got)
+
+
 def test_flash_attention_unit_scale(cuda):
     """c = scale*log2(e) == 1 exactly skips the in-kernel Q prescale (callers that fold
     the softmax scale into the Q projection); must equal the prescaled path's math."""

@@ -1,9 +1,11 @@
-"""Same-process A/B of the d = 40 attention kernels that vd_attention_ex selects per call
-(kernel ids: 2 flash32, 3 flash40; 4 = flash48 on branch flash48-pv16-experiment, profiles/r06_flash48_refuted.txt), on the level-1 shape (32 images x 8 heads,
-S = 4096, d = 40, the model's unit scale), arms interleaved, each launch incl. the exact fix-up
-launch that follows flash40/flash48.  Also prints the arms' output differences (fp32 outputs).
+"""Same-process A/B of the attention kernels that vd_attention_ex selects per call (kernel ids:
+1 the 16x16x32 flash kernel, 2 flash32, 3 flash40 at d = 40 / flash80 at d = 80; 4 = flash48 on
+branch flash48-pv16-experiment, profiles/r06_flash48_refuted.txt), on the level-1 shape (32 images
+x 8 heads, S = 4096, d = 40) or with --d 80 --S 1024 the level-2 one, the model's unit scale, arms
+interleaved, each launch incl. the exact fix-up launch that follows flash40.  Also prints the arms'
+output differences (fp32 outputs).
 
-    python tools/attn_kernel_ab.py [--arms 3,2] [--rounds 15]      # GPU box
+    python tools/attn_kernel_ab.py [--arms 3,2] [--d 40 --S 4096] [--rounds 15]      # GPU box
 """
 from __future__ import annotations
 
@@ -15,7 +17,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "video-diffusion-experiments_amd"))
 
-NAMES = {2: "flash32", 3: "flash40", 4: "flash48"}
+NAMES = {1: "v1", 2: "flash32", 3: "flash40", 4: "flash48"}
 
 
 def main():
@@ -23,12 +25,14 @@ def main():
     ap.add_argument("--arms", default="3,2")
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--imgs", type=int, default=32)
+    ap.add_argument("--d", type=int, default=40)
+    ap.add_argument("--S", type=int, default=4096)
     args = ap.parse_args()
     import torch
     from vdiff import ops
 
     arms = [int(a) for a in args.arms.split(",")]
-    imgs, heads, S, d = args.imgs, 8, 4096, 40
+    imgs, heads, S, d = args.imgs, 8, args.S, args.d
     C = heads * d
     g = torch.Generator(device="cuda").manual_seed(0)
     q = (torch.randn(imgs * S, C, device="cuda", generator=g) * 1.5 * d ** -0.5 * math.log2(math.e)).to(torch.bfloat16)
@@ -72,7 +76,7 @@ def main():
     for a, t in res.items():
         t = sorted(t)
         med = t[len(t) // 2]
-        print(f"{NAMES[a]:8s} median {med:7.1f} us ({med / base - 1:+6.1%})  min {t[0]:.1f} max {t[-1]:.1f}  "
+        print(f"{NAMES[a] if d == 40 or a != 3 else 'flash80':8s} median {med:7.1f} us ({med / base - 1:+6.1%})  min {t[0]:.1f} max {t[-1]:.1f}  "
               f"{fl / med / 1e6:7.1f} TF/s = {fl / med / 1e6 / 2500:.4f} of 2.5 PF", flush=True)
 
 

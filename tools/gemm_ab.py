@@ -6,7 +6,7 @@ descriptors), arms interleaved, outputs compared bit for bit against the product
 
 Cases: the UNet's 3x3 convs at the 16-frame CFG batch (32 images) — stride 1 at every level,
 the channel-concat convs of the up blocks, a stride-2 downsample, a nearest-x2 upsample — and a
-(2+1)D temporal conv (kt = 3, ks = 1).
+(2+1)D temporal conv (kt = 3, ks = 1); GEMM_AB_CASES=geglu: the four GEGLU projections instead.
 
     python tools/gemm_ab.py --save NAME [--rev REV]   # here: tools/diag_gemm/src_NAME/ from git REV (default HEAD)
     python tools/gemm_ab.py --build                   # here (CPU): tools/diag_gemm/libvdiff_gemm_NAME.so
@@ -86,19 +86,31 @@ def run(rounds: int):
         cases.append((name, lambda: ops.conv3x3(x, n, h, w, wt, x1=x1, stride=stride, upsample=upsample, bias=b)[0],
                       fl))
 
-    conv("L1 conv 320->320", 64, 64, 320, 320)
-    conv("L2 conv 640->640", 32, 32, 640, 640)
-    conv("L3 conv 1280->1280", 16, 16, 1280, 1280)
-    conv("L4 conv 1280->1280", 8, 8, 1280, 1280)
-    conv("L1 up concat 320+320", 64, 64, 320, 320, c1=320)
-    conv("L2 up concat 640+320", 32, 32, 640, 640, c1=320)
-    conv("L1 down stride 2", 64, 64, 320, 320, stride=2)
-    conv("L2 upsample x2", 16, 16, 640, 640, upsample=True)
-    # (2+1)D temporal half: kt = 3, ks = 1 over 2 videos x 16 frames at level 2
-    xt = rnd(n * 32 * 32, 640)
-    wtt = rnd(640, 3 * 640, scale=(3 * 640) ** -0.5)
-    cases.append(("L2 temporal kt3", lambda: ops.conv3d(xt, 2, 16, 32, 32, wtt, kt=3, ks=1)[0],
-                  2.0 * n * 32 * 32 * 640 * 3 * 640))
+    def geglu(name, M, N, K):  # GEGLU projection (hidden | gate interleaved, 2N rows of W) with its GELU epilogue
+        a = rnd(M, K)
+        wt = rnd(2 * N, K, scale=K ** -0.5)
+        b = torch.randn(2 * N, device=dev, generator=g)
+        cases.append((name, lambda: ops.gemm(a, wt, bias=b, act=ops.ACT_GEGLU), 2.0 * M * 2 * N * K))
+
+    if os.environ.get("GEMM_AB_CASES") == "geglu":
+        geglu("L1 GEGLU 320->2x1280", n * 64 * 64, 1280, 320)
+        geglu("L2 GEGLU 640->2x2560", n * 32 * 32, 2560, 640)
+        geglu("L3 GEGLU 1280->2x5120", n * 16 * 16, 5120, 1280)
+        geglu("L4 GEGLU 1280->2x5120", n * 8 * 8, 5120, 1280)
+    else:
+        conv("L1 conv 320->320", 64, 64, 320, 320)
+        conv("L2 conv 640->640", 32, 32, 640, 640)
+        conv("L3 conv 1280->1280", 16, 16, 1280, 1280)
+        conv("L4 conv 1280->1280", 8, 8, 1280, 1280)
+        conv("L1 up concat 320+320", 64, 64, 320, 320, c1=320)
+        conv("L2 up concat 640+320", 32, 32, 640, 640, c1=320)
+        conv("L1 down stride 2", 64, 64, 320, 320, stride=2)
+        conv("L2 upsample x2", 16, 16, 640, 640, upsample=True)
+        # (2+1)D temporal half: kt = 3, ks = 1 over 2 videos x 16 frames at level 2
+        xt = rnd(n * 32 * 32, 640)
+        wtt = rnd(640, 3 * 640, scale=(3 * 640) ** -0.5)
+        cases.append(("L2 temporal kt3", lambda: ops.conv3d(xt, 2, 16, 32, 32, wtt, kt=3, ks=1)[0],
+                      2.0 * n * 32 * 32 * 640 * 3 * 640))
 
     def with_lib(h, fn):
         saved = L._lib

@@ -1321,6 +1321,352 @@ __global__ __launch_bounds__(F4_NT, 1) void flash40_kernel(
   f4_block<UNITC>(smem, q, ldq, k, ldk, v, ldv, o, ldo, heads, sq, skv, kv_div, c, out_f32);
 }
 
+// ============================================================ flash80
+// The d = 80 spatial self-attention (SD-1.5 level 2: S = 1024, 8 heads) on flash40's schedule
+// (round 6): 8 waves in two groups one barrier apart, per 64-key tile V(t) = the softmax of S(t)
+// (VALU) and M(t) = PV(t) then QK^T(t+1) (24 x 32x32x16: 12 + 12), K/V by LDS-DMA into a 4-slot ring
+// issued three tiles ahead.  One 32-query block per wave (256 queries per workgroup): d = 80's
+// fragments (Q' 6 k-steps, K' 12 per tile, V^T 12) leave no room for a second.  QK^T's contraction is
+// padded 81 -> 96 (K' chunk 10 = the -mu column's ones, chunk 11 zeros), PV's rows 81 -> 96 (d-block 2
+// = V d 64..79 | the ones column | zeros): 20 of every 24 MFMAs are algorithmic, against flash40's
+// 20 of 28, so the tile is matrix-bound where flash40's is issue-bound.
+// Softmax: flash32's exact deferred max, without its per-score maxes on the MFMA results — the
+// decision reads P = exp2(S) (VALU results: plain v_max3, no canonicalising maxes): a row whose P
+// passes 2^THR (a score THR past mu) raises mu to the bf16 of its exact tile max (taken, with P, in
+// that rare branch), O and the row sum rescale, P is recomputed.  So P <= 2^THR always: no
+// overflow, no flags, no fix-up launch (flash40 needs flash32's exact pass; d = 80 has none).
+// Row sum = V's ones column (d = 80: d-block 2, accumulator row 16 = register 8 of lanes 0-31).
+constexpr int F8K_QWG = F4_NW * 32;                     // queries per workgroup
+constexpr int F8K_K = 0, F8K_VA = 12 * 1024, F8K_VB = F8K_VA + 4096, F8K_VC0 = F8K_VB + 4096,
+              F8K_VC1 = F8K_VC0 + 1024, F8K_VONE = F8K_VC1 + 1024, F8K_SLOT = F8K_VONE + 1024;
+constexpr int F8K_LDS = F4_RING * F8K_SLOT;             // 92 KiB
+constexpr int F8K_NP = 3;                               // LDS-DMA pieces per wave and tile (wave 7: 2)
+
+struct F80Dma {  // this wave's pieces of every tile (piece p = 3 wave + i, see f80_dma_setup)
+  u32x4 rs[F8K_NP];
+  uint32_t voff[F8K_NP], step[F8K_NP], row[F8K_NP], lds[F8K_NP];
+};
+
+// pieces per tile (23): 0-9 = K chunk p (d 8p .. 8p + 7) of the 64 keys (lane = key), 10 = K' ones chunk
+// (the -mu column), 11 = K' zero chunk (d 88..95: the constant read past its 16 bytes), 12-15 = V
+// d 0..31 of keys 16 (p - 12) + lane / 4 (lane % 4 = chunk), 16-19 = V d 32..63 likewise, 20 / 21 =
+// V d 64..71 / 72..79 (lane = key), 22 = V's ones chunk.  Keys past skv read zeros (range check).
+__device__ __forceinline__ void f80_dma_setup(F80Dma& dma, int wave, int lane, const bf16_t* kb_ptr, int64_t ldk,
+                                              const bf16_t* vb_ptr, int64_t ldv, int64_t skv) {
+  constexpr int D = 80;
+  const uint32_t ldkb = (uint32_t)ldk * 2, ldvb = (uint32_t)ldv * 2;
+  const u32x4 rk = f4_rsrc(kb_ptr, (uint32_t)(skv - 1) * ldkb + 2 * D);
+  const u32x4 rv = f4_rsrc(vb_ptr, (uint32_t)(skv - 1) * ldvb + 2 * D);
+  const u32x4 r1 = f4_rsrc(f4_ones, 16);
+#pragma unroll
+  for (int i = 0; i < F8K_NP; ++i) {
+    const int p = F8K_NP * wave + i;
+    uint32_t row = lane, col = 0, step = 0, lds = 0;
+    u32x4 rs = r1;
+    if (p < 10) {
+      rs = rk; col = 16 * p; step = ldkb; lds = F8K_K + 1024 * p;
+    } else if (p == 10) {
+      lds = F8K_K + 1024 * 10;
+    } else if (p == 11) {
+      row = 1u << 30; lds = F8K_K + 1024 * 11;  // never a valid key: the zero half of the constant's range
+    } else if (p < 20) {
+      const int q = p < 16 ? p - 12 : p - 16;
+      rs = rv; row = 16 * q + (lane >> 2); col = (p < 16 ? 0 : 64) + 16 * (lane & 3); step = ldvb;
+      lds = (p < 16 ? F8K_VA : F8K_VB) + 1024 * q;
+    } else if (p < 22) {
+      rs = rv; col = p == 20 ? 128 : 144; step = ldvb; lds = p == 20 ? F8K_VC0 : F8K_VC1;
+    } else {
+      lds = F8K_VONE;
+    }
+    dma.rs[i] = rs; dma.row[i] = row; dma.step[i] = step; dma.lds[i] = lds;
+    dma.voff[i] = step ? row * step + col : 0u;
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void f80_issue(const F80Dma& m, uint32_t lds0, int t, int64_t skv) {
+  const uint32_t key0 = (uint32_t)t * KT;
+  const uint32_t slot = lds0 + (uint32_t)(t % F4_RING) * F8K_SLOT;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const uint32_t off = m.step[i] ? m.voff[i] + key0 * m.step[i] : ((int64_t)(key0 + m.row[i]) < skv ? 0u : 16u);
+    f4_dma(m.rs[i], slot + m.lds[i], off);
+  }
+}
+
+template <bool UNITC>
+__device__ __forceinline__ void f80_loop(const char* smem, uint32_t lds0, const F80Dma& dma, int wave, bool g0,
+                                         int64_t skv, bf16x8 (&qf)[6], f32x16 (&oacc)[3], uint32_t kl0,
+                                         uint32_t vl0, uint32_t vl2, int hh, float c) {
+  constexpr int MU_KS = 5, MU_H = 0, MU_J = 0;  // d = 80 in the Q' fragments
+#pragma unroll
+  for (int db = 0; db < 3; ++db)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) oacc[db][i] = 0.f;
+  float mu = 0.f;
+  const int T = (int)((skv + KT - 1) / KT);  // >= 4 (launch condition)
+  constexpr float PTHR = 64.0f;  // 2^F32_THR: a P above it = a score THR past mu
+
+  f32x16 s[2];
+  bf16x8 pf[2][2];
+  bf16x8 vfr[3][2][2];
+  bf16x8 kfr[2][6];
+
+  auto tr = [&](uint32_t a) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(smem + a));
+  };
+  // V^T fragment (d-block db, key block kb, k-step s2) of tile t: flash32's key order, lo keys
+  // 16 s2 + 4 hh + 0..3, hi + 8; d-blocks 0-1 from the 64-B rows of V d 0..31 / 32..63, d-block 2
+  // from the 16-B rows of V d 64..71 / 72..79 / the ones chunk
+  auto read_v = [&](int t, int db, int kb, int s2) {
+    const uint32_t sb = (uint32_t)((t % F4_RING) * F8K_SLOT);
+    const uint32_t R = (uint32_t)(kb * 32 + 16 * s2);
+    const uint32_t a = db < 2 ? sb + vl0 + (db == 1 ? 4096u : 0u) + R * 64 : sb + vl2 + R * 16;
+    const uint32_t ah = a + (db < 2 ? 512 : 128);
+    const bf16x4 lo = tr(a), hi = tr(ah);
+    vfr[db][kb][s2] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  auto read_k = [&](int t, int kb, int ks) {
+    kfr[kb][ks] = *(const bf16x8*)(smem + (t % F4_RING) * F8K_SLOT + kl0 + 512 * kb + 2048 * ks);
+  };
+  auto qk = [&](int kb) {
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) {
+      if (ks == 0) {
+        f32x16 z;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) z[i] = 0.f;
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[ks], z, 0, 0, 0);
+      } else {
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kb][ks], qf[ks], s[kb], 0, 0, 0);
+      }
+    }
+  };
+  auto pv = [&](int db, int kb, int s2) {
+    oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[db][kb][s2], pf[kb][s2], oacc[db], 0, 0, 0);
+  };
+  f32x16 pe[2];       // P = exp2(S), fp32
+  auto exps = [&]() {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) pe[kb][i] = __builtin_amdgcn_exp2f(UNITC ? s[kb][i] : s[kb][i] * c);
+  };
+  // V(t): P = exp2(S(t)); a row whose P passes 2^THR (or the first tile) moves mu to the bf16 of its
+  // exact tile max and P is recomputed; then the bf16 packs.  The maxes over P are compiler-visible
+  // (VALU results: hipcc adds no canonicalising max and pads the exp -> max hazards itself)
+  auto vphase = [&](int t) {
+    exps();
+    float pm0 = pe[0][0], pm1 = pe[1][0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) {
+      pm0 = __builtin_fmaxf(pm0, pe[0][i]);
+      pm1 = __builtin_fmaxf(pm1, pe[1][i]);
+    }
+    const float pm = __builtin_fmaxf(pm0, pm1);
+    if (t == 0 || __any(!(pm <= PTHR))) {  // wave-uniform; !(<=): an inf / NaN P takes the branch too
+      float tm = s[0][0];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tm = __builtin_fmaxf(tm, s[kb][i]);
+      tm = __builtin_fmaxf(tm, partner32(tm));
+      const float tmc = UNITC ? tm : tm * c;
+      const bool up = t == 0 || tmc > F32_THR;
+      const float nmu = up ? (float)(__bf16)(mu + tm) : mu;
+      const float delta = nmu - mu;  // exact: both bf16 values
+      const float alpha = __builtin_amdgcn_exp2f(UNITC ? -delta : -delta * c);
+      mu = nmu;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[kb][i] -= delta;
+#pragma unroll
+      for (int db = 0; db < 3; ++db)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[db][i] *= alpha;
+      if (hh == MU_H) qf[MU_KS][MU_J] = (__bf16)(-nmu);
+      exps();
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (__bf16)pe[kb][8 * s2 + j];
+        pf[kb][s2] = f;
+      }
+  };
+  // M(t) = PV(t) (d-blocks 0, 1, 2) then QK^T(t+1); the next d-block's V^T reads and then K'(t+1)'s
+  // reads go out between the MFMAs
+  auto mphase = [&](int t) {
+    const bool more = t + 1 < T;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int db = 0; db < 3; ++db) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pv(db, i >> 1, i & 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (db < 2) {
+          read_v(t, db + 1, i >> 1, i & 1);
+        } else if (more) {
+          read_k(t + 1, 0, i);
+          if (i < 2) read_k(t + 1, 0, 4 + i);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) read_k(t + 1, 1, ks);
+      __builtin_amdgcn_sched_barrier(0);
+      qk(0);
+      qk(1);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const bool issuer7 = wave == 7;  // wave 7 moves two pieces (21, 22), the others three
+  auto issue = [&](int u) {
+    if (u < T) {
+      if (issuer7) f80_issue<2>(dma, lds0, u, skv);
+      else f80_issue<3>(dma, lds0, u, skv);
+    }
+  };
+  auto wait_tile = [&](int u) {
+    if (u < T) {
+      if (u + 1 < T) {
+        if (issuer7) f4_wait_vm<2>();
+        else f4_wait_vm<3>();
+      } else {
+        f4_wait_vm<0>();
+      }
+    }
+  };
+  auto bar = [&]() { f4_bar(); };
+  // flash40's prologue and phase order
+  issue(0);
+  issue(1);
+  wait_tile(0);
+  bar();
+  issue(2);
+  if (!g0) bar();
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) read_k(0, kb, ks);
+  qk(0);
+  qk(1);
+  if (!g0) wait_tile(1);
+  bar();
+  for (int t = 0; t < T; ++t) {
+    vphase(t);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) read_v(t, 0, kb, s2);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        f4_pin(vfr[0][kb][s2]);
+        f4_pin(pf[kb][s2]);
+      }
+    if (g0) wait_tile(t + 1);
+    bar();
+    issue(t + 3);
+    mphase(t);
+    if (!g0) wait_tile(t + 2);
+    bar();
+  }
+  if (g0) bar();
+}
+
+template <bool UNITC>
+__global__ __launch_bounds__(F4_NT, 1) void flash80_kernel(
+    const bf16_t* __restrict__ q, int64_t ldq, const bf16_t* __restrict__ k, int64_t ldk,
+    const bf16_t* __restrict__ v, int64_t ldv, bf16_t* __restrict__ o, int64_t ldo, int heads,
+    int64_t sq, int64_t skv, int64_t kv_div, float c, int out_f32) {
+  __shared__ __attribute__((aligned(1024))) char smem[F8K_LDS];
+  constexpr int D = 80;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool g0 = wave < 4;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int nqb = (int)((sq + F8K_QWG - 1) / F8K_QWG);
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qblk = lid % nqb;
+  const int h = (lid / nqb) % heads;
+  const int64_t b = (lid / nqb) / heads;
+  const int64_t q0 = (int64_t)qblk * F8K_QWG + wave * 32;
+  const int64_t bkv = b / kv_div;
+  const bf16_t* qb_ptr = q + b * sq * ldq + (int64_t)h * D;
+
+  bf16x8 qf[6];  // Q'^T (B operand): k-step ks, lane half hh = d 16 ks + 8 hh .. +7; d = 80 (-mu) starts at 0
+  {
+    const int64_t qi = q0 + r32;
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) {
+      const int dd = ks * 16 + 8 * hh;
+      uint4 u = make_uint4(0, 0, 0, 0);
+      if (qi < sq && dd < D) u = *(const uint4*)(qb_ptr + qi * ldq + dd);
+      qf[ks] = __builtin_bit_cast(bf16x8, u);
+    }
+  }
+  F80Dma dma;
+  f80_dma_setup(dma, wave, lane, k + bkv * skv * ldk + (int64_t)h * D, ldk, v + bkv * skv * ldv + (int64_t)h * D,
+                ldv, skv);
+  const uint32_t kl0 = F8K_K + hh * 1024 + r32 * 16;  // + 2048 ks + 512 kb: chunk 2 ks + hh, key 32 kb + r32
+  const int g16 = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+  const uint32_t vl0 = F8K_VA + (uint32_t)(((4 * hh + qq) * 32 + 16 * (g16 & 1) + 4 * pp) * 2);
+  // d-block 2: columns 64..79 (lanes of the even 16-lane groups) from V d 64..71 / 72..79, column 80
+  // = the ones chunk's 1, the rest its zero half
+  const uint32_t vl2 = ((g16 & 1) == 0 ? (pp < 2 ? F8K_VC0 + 8 * pp : F8K_VC1 + 8 * (pp - 2))
+                                       : F8K_VONE + (pp == 0 ? 0 : 8)) +
+                       (uint32_t)((4 * hh + qq) * 16);
+
+  f32x16 oacc[3];
+  f80_loop<UNITC>(smem, lds0, dma, wave, g0, skv, qf, oacc, kl0, vl0, vl2, hh, c);
+
+  // epilogue: O[q][d] = O^T[d][q] / l, the row sum in d-block 2, register 8 of lanes 0-31
+  const float lown = oacc[2][8];
+  const float lp = partner32(lown);
+  const float l = hh == 0 ? lown : lp;
+  const float inv = __builtin_amdgcn_rcpf(l);
+  const int64_t qi = q0 + r32;
+  if (out_f32) {
+    if (qi >= sq) return;
+    float* frow = (float*)o + (b * sq + qi) * ldo + (int64_t)h * D;
+#pragma unroll
+    for (int db = 0; db < 3; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = 32 * db + 8 * g + 4 * hh;
+        const f32x16& a = oacc[db];
+        if (d0 + 4 <= D)
+          *(float4*)(frow + d0) = make_float4(a[4 * g] * inv, a[4 * g + 1] * inv, a[4 * g + 2] * inv, a[4 * g + 3] * inv);
+      }
+    return;
+  }
+  bf16_t* orow = o + (b * sq + (qi < sq ? qi : 0)) * ldo + (int64_t)h * D;  // every lane takes part in the swaps
+#pragma unroll
+  for (int db = 0; db < 3; ++db) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const f32x16& a = oacc[db];
+      uint32_t x0 = pack2(a[8 * m + 0] * inv, a[8 * m + 1] * inv), x1 = pack2(a[8 * m + 2] * inv, a[8 * m + 3] * inv);
+      uint32_t y0 = pack2(a[8 * m + 4] * inv, a[8 * m + 5] * inv), y1 = pack2(a[8 * m + 6] * inv, a[8 * m + 7] * inv);
+      auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+      auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+      const int dd = 32 * db + 16 * m + 8 * hh;
+      if (qi < sq && dd + 8 <= D) *(uint4*)(orow + dd) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+  }
+}
+
 // kernel (per call, test hook; 0 everywhere in the product): 0 = automatic — d = 40: flash40 from
 // 4 key tiles, flash32 below (and for its text cross-attention), other d: flash_attn_kernel;
 // 1 = flash_attn_kernel (16x16x32) for any d; 2 = flash32 (d = 40); 3 = flash40 wherever it
@@ -1370,6 +1716,23 @@ int launch_flash(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
   }
   // (QBLK 4 only for D <= 40: wider heads' QBLK-4 instances spill 94-280 VGPRs, so they are
   // not instantiated at all)
+  if constexpr (D == 80) {
+    // flash80 (round 6): the level-2 self-attention, from 4 key tiles (kernel 3 forces it from 2)
+    const bool oal = ((uintptr_t)o & 15) == 0 && ldo % (out_f32 ? 4 : 8) == 0;
+    if ((kernel == 3 || (kernel == 0 && skv >= 4 * KT)) && skv >= 2 * KT && oal) {
+      const int64_t nblk = (sq + F8K_QWG - 1) / F8K_QWG * heads * batch;
+      if (nblk > 0x7fffffff) return VD_EINVAL;
+      if (c == 1.0f)
+        hipLaunchKernelGGL((flash80_kernel<true>), dim3((unsigned)nblk), dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
+                           out_f32);
+      else
+        hipLaunchKernelGGL((flash80_kernel<false>), dim3((unsigned)nblk), dim3(F4_NT), 0, s, (const bf16_t*)q, ldq,
+                           (const bf16_t*)k, ldk, (const bf16_t*)v, ldv, (bf16_t*)o, ldo, heads, sq, skv, kv_div, c,
+                           out_f32);
+      return vd_launch_status();
+    }
+  }
   if constexpr (D <= 40) {
     if (sq >= 1024) {
       const dim3 grid((unsigned)((sq + 255) / 256), (unsigned)heads, (unsigned)batch);
