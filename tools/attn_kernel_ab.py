@@ -17,7 +17,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "video-diffusion-experiments_amd"))
 
-NAMES = {1: "v1", 2: "flash32", 3: "flash40", 4: "flash48"}
+NAMES = {0: "auto", 1: "v1", 2: "flash32", 3: "flash40", 4: "flash48"}
 
 
 def main():
@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--imgs", type=int, default=32)
     ap.add_argument("--d", type=int, default=40)
     ap.add_argument("--S", type=int, default=4096)
+    ap.add_argument("--skv", type=int, default=0, help="keys (default S: self-attention)")
+    ap.add_argument("--kvdiv", type=int, default=1, help="query batches per K/V batch (cross-attention: frames)")
     args = ap.parse_args()
     import torch
     from vdiff import ops
@@ -35,14 +37,15 @@ def main():
     imgs, heads, S, d = args.imgs, 8, args.S, args.d
     C = heads * d
     g = torch.Generator(device="cuda").manual_seed(0)
+    skv, kvd = (args.skv or S), args.kvdiv
     q = (torch.randn(imgs * S, C, device="cuda", generator=g) * 1.5 * d ** -0.5 * math.log2(math.e)).to(torch.bfloat16)
-    k = (torch.randn(imgs * S, C, device="cuda", generator=g) * 1.5).to(torch.bfloat16)
-    v = (torch.randn(imgs * S, C, device="cuda", generator=g) * 1.5).to(torch.bfloat16)
+    k = (torch.randn(imgs // kvd * skv, C, device="cuda", generator=g) * 1.5).to(torch.bfloat16)
+    v = (torch.randn(imgs // kvd * skv, C, device="cuda", generator=g) * 1.5).to(torch.bfloat16)
     sc = 1.0 / math.log2(math.e)
     out = torch.empty(imgs * S, C, device="cuda", dtype=torch.bfloat16)
 
     def call(a, o=out, f32=False):
-        ops.attention(q, k, v, imgs, heads, S, S, d, scale=sc, out=o, out_f32=f32, kernel=NAMES[a])
+        ops.attention(q, k, v, imgs, heads, S, skv, d, kv_div=kvd, scale=sc, out=o, out_f32=f32, kernel=NAMES[a])
 
     ref = {}
     for a in arms:
@@ -58,7 +61,7 @@ def main():
         nbf = (ref[a][1] != ref[a0][1]).float().mean().item()
         print(f"{NAMES[a]} vs {NAMES[a0]}: fp32 out max |diff| {d32.max().item():.3e} (max rel {rel:.3e}); "
               f"bf16 out elements that differ {nbf:.2e}", flush=True)
-    fl = 4.0 * S * S * d * heads * imgs
+    fl = 4.0 * S * skv * d * heads * imgs
     res = {a: [] for a in arms}
     for r in range(args.rounds + 1):
         for a in arms:
