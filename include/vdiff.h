@@ -253,9 +253,10 @@ int vd_attention_f32(const void* q, int64_t ldq, const void* k, int64_t ldk, con
                      int64_t sq, int64_t skv, int32_t d, int64_t kv_div, float scale, vd_stream_t stream);
 /* vd_attention / vd_attention_f32 with an explicit kernel choice per call (the library keeps no
  * selector state): kernel 0 = the automatic choice (what vd_attention runs: d = 40 -> flash40
- * from 4 key tiles, flash32 below; other d -> the 16x16x32 flash kernel), 1 = the 16x16x32 flash
- * kernel for any d, 2 = flash32 (d = 40), 3 = flash40 wherever it applies (d = 40, >= 2 key
- * tiles); a kernel that does not take the shape falls through to the next one down.  All of
+ * from 4 key tiles, flash32 below; d = 80 -> flash80 from 4 key tiles (round 6); other d -> the
+ * 16x16x32 flash kernel), 1 = the 16x16x32 flash kernel for any d, 2 = flash32 (d = 40),
+ * 3 = flash40 / flash80 wherever they apply (d = 40 / 80, >= 2 key tiles); a kernel that does not
+ * take the shape falls through to the next one down.  All of
  * them compute softmax(q k^T * scale) v; flash40 is bit-identical to flash32 (the parity tests
  * run each).  out_f32 as vd_attention_f32. */
 int vd_attention_ex(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
